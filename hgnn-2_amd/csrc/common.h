@@ -1,0 +1,74 @@
+// Shared device helpers for the gfx950 kernels of hgnn_amd.
+//
+// Conventions used by every kernel in this directory:
+//  * wave = 64 lanes (CDNA4); block sizes are multiples of 64;
+//  * feature matrices are row-major [rows][C] fp32, one row per node or per
+//    line-graph edge slot, rows of a batch packed graph after graph;
+//  * sizes that depend on the batch content (packed row totals) live in device
+//    memory and are read by the kernels, so a forward needs no host sync; grids
+//    are sized from the dense padded capacities (bs*Nmax, bs*Emax) and blocks
+//    past the device total exit at once.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HGNN_WAVE 64
+
+#define HGNN_HOST_CHECK(expr)                                       \
+    do {                                                            \
+        hipError_t _e = (expr);                                     \
+        if (_e != hipSuccess) return HGNN_ERR_HIP;                  \
+    } while (0)
+
+#define HGNN_LAUNCH_CHECK()                                         \
+    do {                                                            \
+        hipError_t _e = hipGetLastError();                          \
+        if (_e != hipSuccess) return HGNN_ERR_HIP;                  \
+    } while (0)
+
+namespace hgnn {
+
+// Device-side error bits (OR-ed into a workspace word; see include/hgnn_amd.h).
+enum : uint32_t {
+    ERR_PAD_NONZERO = 1u << 0,   // operator entry outside the graph's real block
+    ERR_MASK = 1u << 1,          // mask[:, :, 0] disagrees with N_batch / E_batch
+    ERR_SIZES = 1u << 2,         // N_b > Nmax, E_b > Emax or negative count
+    ERR_CCN_SELFLOOP = 1u << 3,  // CCN adjacency without self loop (chi_ii absent)
+    ERR_CCN_DEGREE = 1u << 4,    // CCN degree above the compiled bound
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+template <typename T>
+__host__ __device__ __forceinline__ T ceil_div(T a, T b) { return (a + b - 1) / b; }
+
+// Entry of a per-row sparse operator list: packed column index and up to
+// three coefficients (J_TOT = 3 slices for J = 1, or {Pm, Pd}).  16 bytes so a
+// wave-uniform entry is one dwordx4 load.
+struct __align__(16) Entry3 {
+    int col;
+    float v0, v1, v2;
+};
+
+// Row descriptor: entries of row r live at [start, start + count) in the
+// structure's entry array (rows own fixed-capacity slots: no prefix sum, so
+// the extraction is a single pass with no inter-graph scan).
+struct __align__(8) RowInfo {
+    int start;
+    int count;
+};
+
+}  // namespace hgnn

@@ -1,0 +1,196 @@
+// Internal launch wrappers shared by the executor and the C-ABI layer.
+#pragma once
+
+#include "common.h"
+
+namespace hgnn {
+
+// ---------------------------------------------------------------- structure
+// Kinds of per-row operator lists built from the dense padded inputs.
+enum StructKind : int {
+    S_W = 0,    // node rows n, cols m:  W[b, n, m, :]           (graph_oper(W, X))
+    S_WT = 1,   // node rows m, cols n:  W[b, n, m, :]           (its transpose)
+    S_WL = 2,   // edge rows, WL[b, e, e', :]                    (graph_oper(WL, XL))
+    S_WLT = 3,  // transpose of WL
+    S_PN = 4,   // node rows n, edge cols m: {Pm, Pd}[b, n, m]    (P_multi(Pm, .))
+    S_PE = 5,   // edge rows m, node cols n: {Pm, Pd}[b, n, m]    (P_multi(Pm^T, .))
+    S_COUNT = 6
+};
+
+struct StructView {
+    const RowInfo* rows;   // per packed row: [start, start + count) in entries
+    const float* entries;  // (1 + ncoef) floats per entry, padded to 4 or 8 floats
+    int stride;            // floats per entry (4 or 8)
+};
+
+struct BatchMeta {
+    int* node_off;   // (bs + 1) packed node row offsets
+    int* edge_off;   // (bs + 1) packed edge row offsets
+    int* totals;     // [0] = total nodes, [1] = total edge slots
+    uint32_t* err;   // validation bits (ERR_*)
+};
+
+int launch_plan(const int64_t* nb, const int64_t* eb, int bs, int nmax, int emax, BatchMeta m,
+                hipStream_t s);
+
+struct ExtractArgs {
+    const float* W;
+    const float* WL;
+    const float* Pm;
+    const float* Pd;
+    const float* mask;
+    const float* mask_lg;
+    int bs, nmax, emax, jtot;
+    BatchMeta meta;
+    RowInfo* rows[S_COUNT];
+    float* entries[S_COUNT];
+    int entry_stride_w;   // floats per W/WL entry
+    int validate;
+    int dual;             // 0: GNN_simple (only S_W / S_WT)
+};
+int launch_extract(const ExtractArgs& a, hipStream_t s);
+
+// Pack X (bs, f, nmax) -> [nodes][f];  XL (bs, 1, emax) -> [edges][1].
+int launch_pack_nodes(const float* X, int bs, int f, int nmax, BatchMeta m, float* out, hipStream_t s);
+int launch_pack_edges(const float* XL, int bs, int emax, BatchMeta m, float* out, hipStream_t s);
+// Unpack [nodes][f] -> dense (bs, f, nmax), zero padding.
+int launch_unpack_nodes(const float* in, int bs, int f, int nmax, BatchMeta m, float* X, hipStream_t s);
+
+// ---------------------------------------------------------------- aggregation
+struct AggFwdArgs {
+    const int* total_rows;  // device
+    int cap_rows;
+    // G part: out[:, j*Cg + c] = sum_e v_j * Xg[col, c]
+    StructView g;
+    const float* xg;
+    int cg, jtot;
+    // P part: out[:, jtot*Cg + c] = sum pm * Xp[col, c];  [.. + Cp + c] = sum pd * Xp[col, c]
+    StructView p;
+    const float* xp;
+    int cp;
+    float* out;
+    int ldo;
+};
+int launch_agg_fwd(const AggFwdArgs& a, hipStream_t s);
+
+struct AggBwdArgs {
+    const int* total_rows;
+    int cap_rows;
+    // G part: out[r, c] += sum_e sum_j v_j * ing[col, gofs + j*C + c]
+    StructView g;
+    const float* ing;
+    int ldg, gofs, jtot;
+    // P part: out[r, c] += sum_e pm * inp[col, pofs_m + c] + pd * inp[col, pofs_d + c]
+    StructView p;
+    const float* inp;
+    int ldp, pofs_m, pofs_d;
+    int c;
+    float* out;
+    int ldo;
+    int accumulate;
+};
+int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- GEMM (fp32 MFMA)
+// Y = A . W^T + bias, relu on cols >= relu_from, BN partials over valid rows.
+struct GemmFwdArgs {
+    const float* a;
+    int lda;
+    const int* m_valid;  // device row count
+    int m_cap, k;
+    const float* w0;     // weights for output cols [0, split): row-major [split][k]
+    const float* w1;     // weights for output cols [split, n): row-major [n - split][k]
+    const float* b0;
+    const float* b1;
+    int n, split, relu_from;
+    float* y;
+    int ldy;
+    float* bn_part;      // [tiles_m][n][3] (count, mean, M2) or nullptr
+};
+int launch_gemm_fwd(const GemmFwdArgs& g, hipStream_t s);
+int gemm_fwd_tiles_m(int m_cap);
+
+// dA = dY . Wcat :  dA[m, k] = sum_o dY[m, o] * Wcat[o, k], Wcat rows split at `split`.
+struct GemmDaArgs {
+    const float* dy;
+    int lddy;
+    const int* m_valid;
+    int m_cap, o;       // o = 2d rows of Wcat
+    const float* w0;
+    const float* w1;
+    int split, k;       // k = output columns
+    float* da;
+    int ldda;
+};
+int launch_gemm_da(const GemmDaArgs& g, hipStream_t s);
+
+// dWcat[o, k] = sum_r dY[r, o] * A[r, k]; column k == kdim of the result is the bias
+// gradient (sum_r dY[r, o]).  Split over row chunks into slabs, then reduced.
+struct GemmDwArgs {
+    const float* dy;
+    int lddy;
+    const float* a;
+    int lda;
+    const int* r_valid;
+    int r_cap, o, k;
+    int split;
+    float* slabs;       // scratch
+    float* dw0;         // (split, k)
+    float* dw1;         // (o - split, k)
+    float* db0;         // (split,)
+    float* db1;         // (o - split,)
+};
+int launch_gemm_dw(const GemmDwArgs& g, hipStream_t s);
+size_t gemm_dw_slab_floats(int r_cap, int o, int k);
+
+// ---------------------------------------------------------------- BN
+struct BnFwdArgs {
+    const float* part;     // [tiles][c][3]
+    int tiles, c;
+    const int* count;      // device: total real rows (sum N_batch / E_batch)
+    const float* w;        // scalar
+    const float* b;        // scalar
+    float* mean;           // (c,) batch or running (eval) statistics in use
+    float* std;            // (c,)
+    float* run_mean;       // running stats (may be null)
+    float* run_std;
+    int training;
+    float momentum;
+};
+int launch_bn_finalize(const BnFwdArgs& a, hipStream_t s);
+
+int launch_bn_apply(const float* y, const int* total_rows, int cap_rows, int c,
+                    const float* mean, const float* std, const float* w, const float* b,
+                    float* z, hipStream_t s);
+
+// BN backward: dY = relu'(Y) * (w / std) * (dZ - mean(dZ.w) - H * mean(dZ.w . H)) (training)
+struct BnBwdArgs {
+    const float* y;        // pre-BN activations [rows][c]
+    const float* dz;       // gradient wrt BN output [rows][c]
+    const int* total_rows;
+    int cap_rows, c;
+    const float* mean;
+    const float* std;
+    const float* w;
+    int relu_from;
+    int training;
+    float* part;           // scratch [tiles][c][2]
+    float* sums;           // scratch [c][2] + [2]
+    float* dy;             // out [rows][c]
+    float* dw;             // scalar out
+    float* db;             // scalar out
+};
+int launch_bn_backward(const BnBwdArgs& a, hipStream_t s);
+int bn_bwd_tiles(int cap_rows);
+
+// ---------------------------------------------------------------- readout
+int launch_readout_fwd(const float* a, int k, const int* node_off, int bs, int nmax,
+                       const float* fcw, const float* fcb, int dim_out,
+                       float* colsum, float* out, hipStream_t s);
+int launch_readout_bwd_da(const float* dout, const int* node_off, int bs, int cap_rows,
+                          const int* total_rows, const float* fcw, int dim_out, int k,
+                          float* da, hipStream_t s);
+int launch_readout_bwd_params(const float* dout, const float* colsum, int bs, int nmax,
+                              int dim_out, int k, float* dfcw, float* dfcb, hipStream_t s);
+
+}  // namespace hgnn

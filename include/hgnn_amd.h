@@ -1,0 +1,172 @@
+/*
+ * hgnn_amd.h -- C ABI of the MI355X (gfx950) message-passing hot path.
+ *
+ * Drop-in boundary: these entry points are what the reference's nn.Module
+ * forward()/backward() calls become.  The reference is pure Python/PyTorch
+ * (SURVEY.md §0.1), so the Python layer in hgnn-2_amd/ (same import paths as
+ * the reference: models.gnns.model_mnb, models.layers.*, functions.*) binds
+ * this ABI through ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - every pointer named d_* is device memory (HBM) owned by the caller;
+ *  - fp32 tensors are dense, contiguous, in the reference's layouts:
+ *      X  (bs, f, Nmax)        node features, channel-major (functions/batching.py:198)
+ *      XL (bs, 1, Emax)        line-graph input (functions/batching.py:201,253)
+ *      W  (bs, Nmax, Nmax, J+2)  graph operators (functions/operators.py:19-29)
+ *      WL (bs, Emax, Emax, J+2)  line-graph operators (functions/operators.py:39-81)
+ *      Pm, Pd (bs, Nmax, Emax)   incidence operators (functions/operators.py:43-66)
+ *      mask (bs, Nmax, Nmax), mask_lg (bs, Emax, Emax)  (functions/batching.py:195-196)
+ *      N_batch, E_batch (bs,) int64  (functions/batching.py:181-185)
+ *  - outputs are caller-allocated; scratch comes from a caller-allocated
+ *    workspace whose size is queried first (no allocation inside any call, so
+ *    every call can be captured into a hipGraph);
+ *  - `stream` is a hipStream_t passed as void*; every call only enqueues work;
+ *  - return value: 0 = HGNN_OK, otherwise an HGNN_ERR_* code (the Python layer
+ *    raises RuntimeError, the reference's error behaviour);
+ *  - device-side input validation (operator entries outside a graph's real
+ *    block, mask/N_batch disagreement) ORs HGNN_DEVERR_* bits into a uint32
+ *    word inside the workspace; hgnn_*_error_word() gives its device address.
+ *  - no global mutable state: calls are re-entrant, one stream per call.
+ */
+#ifndef HGNN_AMD_H
+#define HGNN_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HGNN_ABI_VERSION 1
+
+#define HGNN_OK 0
+#define HGNN_ERR_ARG 1          /* invalid argument: null pointer, bad size   */
+#define HGNN_ERR_UNSUPPORTED 2  /* configuration not compiled (e.g. J > 3)    */
+#define HGNN_ERR_HIP 3          /* HIP launch / runtime failure               */
+
+#define HGNN_DEVERR_PAD_NONZERO 0x1u  /* operator entry outside the real block */
+#define HGNN_DEVERR_MASK 0x2u         /* mask[:, :, 0] != (n < N_batch[b])      */
+#define HGNN_DEVERR_SIZES 0x4u        /* N_batch > Nmax, E_batch > Emax, < 0   */
+#define HGNN_DEVERR_CCN_SELFLOOP 0x8u /* CCN adjacency lacks a self loop        */
+#define HGNN_DEVERR_CCN_DEGREE 0x10u  /* CCN degree above the compiled bound    */
+
+int hgnn_abi_version(void);
+const char* hgnn_status_string(int status);
+
+/* ------------------------------------------------------------------------
+ * Network executor: GNN_lg.forward / GNN_simple.forward + autograd backward.
+ *
+ * Replaces models/gnns/model_mnb.py:166-174 (GNN_simple.forward) and
+ * models/gnns/model_mnb.py:232-237 (GNN_lg.forward) with every layer
+ * (models/layers/layers_mnb.py:52-69, 88-95, 189-225, 256-290, 322-358,
+ * 379-388), BN (models/layers/batch_normalization.py:34-108) and the
+ * aggregation ops graph_oper / P_multi (layers_mnb.py:391-434) fused into one
+ * enqueue; hgnn_net_backward is the autograd backward of the same graph
+ * (scripts/train_mnb.py:90).
+ * ---------------------------------------------------------------------- */
+typedef struct hgnn_net_config {
+    int32_t kind;      /* 0 = GNN_simple, 1 = GNN_lg                              */
+    int32_t order;     /* GNN_lg update order 1, 2, 3 (model_mnb.py:210-227)      */
+    int32_t bs;        /* graphs in the batch                                     */
+    int32_t nmax;      /* padded node count Nmax (X.shape[2])                     */
+    int32_t emax;      /* padded edge-slot count Emax (XL.shape[2]); 0 for simple */
+    int32_t f_in;      /* dim_input (X.shape[1])                                  */
+    int32_t d;         /* n_features                                              */
+    int32_t n_layers;  /* >= 2: layer0, n_layers-2 middle layers, layerlast       */
+    int32_t j_tot;     /* J + 2 operator slices (W.shape[3])                      */
+    int32_t dim_out;   /* dim_output                                              */
+    int32_t training;  /* 1: batch BN statistics + running-stat update; 0: eval   */
+    int32_t need_dx;   /* backward: write dX (bs, f_in, nmax)                     */
+    int32_t need_dw;   /* backward: write dense dW (bs, nmax, nmax, j_tot)        */
+    int32_t reserved;
+} hgnn_net_config;
+
+typedef struct hgnn_net_inputs {
+    const float* d_X;
+    const float* d_XL;       /* NULL for GNN_simple */
+    const float* d_W;
+    const float* d_WL;       /* NULL for GNN_simple */
+    const float* d_Pm;       /* NULL for GNN_simple */
+    const float* d_Pd;       /* NULL for GNN_simple */
+    const int64_t* d_N_batch;
+    const int64_t* d_E_batch; /* NULL for GNN_simple */
+    const float* d_mask;
+    const float* d_mask_lg;   /* NULL for GNN_simple */
+} hgnn_net_inputs;
+
+/* Parameter pointer order (device fp32, contiguous), per layer l = 0..n_layers-2:
+ *   GNN_lg:     cv1.w cv1.b cv2.w cv2.b bn1.w bn1.b cv3.w cv3.b cv4.w cv4.b bn2.w bn2.b
+ *   GNN_simple: cv1.w cv1.b cv2.w cv2.b bn1.w bn1.b
+ * then layerlast.fc.w layerlast.fc.b.  BN weight/bias are 0-dim (scalar) tensors
+ * (batch_normalization.py:26-27).  Count: hgnn_net_param_count(). */
+int hgnn_net_param_count(const hgnn_net_config* cfg);
+
+/* Running BN statistics, per BN module in the order above (bn1, bn2 per layer):
+ * running_mean then running_std, each (2 d,).  Updated in place in training
+ * mode as r = 0.9 * batch + 0.1 * r (batch_normalization.py:37-38); read in
+ * eval mode (batch_normalization.py:41). */
+int hgnn_net_bn_count(const hgnn_net_config* cfg);
+
+size_t hgnn_net_workspace_bytes(const hgnn_net_config* cfg);
+
+/* Device address of the validation word inside `workspace` (uint32). */
+uint32_t* hgnn_net_error_word(const hgnn_net_config* cfg, void* workspace);
+
+/* out: (bs, dim_out).  The workspace keeps what backward needs; it must stay
+ * untouched between a forward and its backward. */
+int hgnn_net_forward(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
+                     const float* const* params, float* const* bn_running,
+                     void* workspace, float* d_out, void* stream);
+
+/* d_dout: (bs, dim_out).  grads: same order/shapes as params; every gradient
+ * buffer is OVERWRITTEN.  d_dX (bs, f_in, nmax) if cfg->need_dx, d_dW
+ * (bs, nmax, nmax, j_tot) if cfg->need_dw (else may be NULL). */
+int hgnn_net_backward(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
+                      const float* const* params, void* workspace,
+                      const float* d_dout, float* const* grads,
+                      float* d_dX, float* d_dW, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Layer-level drop-ins on dense padded tensors.
+ * ---------------------------------------------------------------------- */
+
+/* graph_oper.forward (models/layers/layers_mnb.py:395-411) == graph_op
+ * (functions/utils.py:24-52):  out[b, j*F+f, n] = sum_m A[b,n,m,j] X[b,f,m].
+ * A (bs, N, N, J), X (bs, F, N), out (bs, J*F, N). */
+int hgnn_graph_oper_forward(const float* d_A, const float* d_X, float* d_out,
+                            int bs, int n, int j, int f, void* stream);
+/* Backward: dX (bs, F, N) = sum_j A_j^T dOut_j (overwritten); dA (bs, N, N, J)
+ * = dOut_j X^T if d_dA != NULL (overwritten). */
+int hgnn_graph_oper_backward(const float* d_A, const float* d_X, const float* d_dout,
+                             float* d_dX, float* d_dA, int bs, int n, int j, int f,
+                             void* stream);
+
+/* P_multi.forward (layers_mnb.py:418-434) == Pmul (functions/utils.py:55-81):
+ * out[b, f, n] = sum_m P[b, n, m] X[b, f, m], P read as (bs, N, M) with strides
+ * (sb, sn, sm) so a transposed view (Pm.transpose(2,1)) needs no copy. */
+int hgnn_p_multi_forward(const float* d_P, long sb, long sn, long sm,
+                         const float* d_X, float* d_out, int bs, int n, int m, int f,
+                         void* stream);
+int hgnn_p_multi_backward(const float* d_P, long sb, long sn, long sm,
+                          const float* d_X, const float* d_dout, float* d_dX,
+                          float* d_dP, int bs, int n, int m, int f, void* stream);
+
+/* BN.forward (batch_normalization.py:34-43) with sb_normalization /
+ * mean_with_padding / mask_embedding (65-108).  X, out (bs, C, N); mask (bs, N, N);
+ * training: writes batch mean/std (C,) to d_mean/d_std; eval: reads them.
+ * w, b: 0-dim device scalars. */
+int hgnn_bn_forward(const float* d_X, const int64_t* d_nb, const float* d_mask,
+                    const float* d_w, const float* d_b, float* d_mean, float* d_std,
+                    float* d_out, int bs, int c, int n, int training, void* stream);
+/* dX (bs, C, N) overwritten; dw, db (scalars) overwritten. */
+int hgnn_bn_backward(const float* d_X, const int64_t* d_nb, const float* d_mask,
+                     const float* d_w, const float* d_mean, const float* d_std,
+                     const float* d_dout, float* d_dX, float* d_dw, float* d_db,
+                     int bs, int c, int n, int training, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HGNN_AMD_H */
