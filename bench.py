@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark: graphs/s forward+backward, QM9-shape batch=512, LG-GNN 5-layer d=64 (BASELINE.json).
+
+One step = one training pass of the drop-in GNN_lg (order 2, the reference's
+`--update 2`) over a batch of 512 synthetic QM9-shape graphs already resident
+in HBM: dense padded inputs as prepare_batch returns them, forward, MSE loss,
+backward (X and W require grad as in scripts/train_mnb.py:56-57), and with N>1
+GPUs the RCCL all-reduce of the gradient bucket (batch-axis data parallelism,
+512 graphs per GPU: weak scaling).
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Prints ONE JSON line (rank 0) with the BASELINE metric, a live roofline of the
+dominant kernel class (HIP events around its launches inside the timed
+region) and the oracle's CPU time on a bounded sample (rank 0, N=1 only).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "hgnn-2_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "graphs/sec forward+backward, QM9-shape batch=512, LG-GNN 5-layer d=64"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--bs", type=int, default=512, help="graphs per GPU")
+    ap.add_argument("--d", type=int, default=64)
+    ap.add_argument("--layers", type=int, default=5)
+    ap.add_argument("--order", type=int, default=2)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-bs", type=int, default=512)
+    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--roofline", type=int, default=1)
+    return ap.parse_args()
+
+
+def make_batch(bs, seed):
+    import hgnn_amd.datagen as dg
+    from functions.batching import prepare_batch
+    from functions.operators import graph_operators
+    graphs = dg.qm9_shape_dataset(bs, seed=seed)
+    data = [[X, A, t, *graph_operators([X, A], 1, True)] for X, A, t in graphs]
+    return list(prepare_batch(data, 0, 1))
+
+
+def cpu_baseline(args, batch_cpu, model):
+    """Oracle (CPU restatement of the reference, oracle/ref_mnb.py) fwd+bwd on a bounded sample."""
+    from oracle import ref_mnb as R
+    b = [t.clone() for t in batch_cpu]
+    if args.cpu_bs < args.bs:
+        b = make_batch(args.cpu_bs, 4242)
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = b
+    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    threads = torch.get_num_threads()
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        st = R.bn_states(args.layers, 2 * args.d)
+        Xr = X.clone().requires_grad_(True)
+        Wr = W.clone().requires_grad_(True)
+        out = R.gnn_lg(p, [Xr, XL, Wr, WL, Pm, Pd], Nb, mask, Eb, mask_lg, args.layers, args.order, st, True)
+        torch.nn.MSELoss()(out, T).backward()
+    dt = time.perf_counter() - t0
+    n = X.shape[0] * args.cpu_steps
+    return {"value": round(n / dt, 3), "unit": "graphs/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_steps} fwd+bwd step(s) of {X.shape[0]} QM9-shape graphs, d={args.d}, "
+                      f"L={args.layers}, order {args.order}, on oracle/ref_mnb.py (torch CPU, {threads} threads); "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from hgnn_amd import roofline as RF
+    from hgnn_amd.net import KernelTimer
+    from models.gnns.model_mnb import GNN_lg
+
+    torch.manual_seed(0)
+    model = GNN_lg(0, args.d, args.layers, 5, 1, 1, args.order).to(dev)
+    params = list(model.parameters())
+    batch_cpu = make_batch(args.bs, 1000 + rank)
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = [t.to(dev) for t in batch_cpu]
+    X.requires_grad_(True)
+    W.requires_grad_(True)
+    crit = torch.nn.MSELoss()
+
+    def step():
+        for p in params:
+            p.grad = None
+        X.grad = None
+        out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+        loss = crit(out, T)
+        loss.backward()
+        if world > 1:
+            grads = [p.grad for p in params]
+            flat = torch._utils._flatten_dense_tensors(grads)
+            dist.all_reduce(flat)
+            flat.div_(world)
+            for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+                g.copy_(f)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    dominant = None
+    if args.roofline:
+        with KernelTimer(4096, range(9)) as tm:
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            per = {k: tm.elapsed(k) for k in range(9)}
+        tm.close()
+        dominant = max(per, key=lambda k: per[k][0])
+        launches_per_step = per[dominant][1] // 2
+
+    timer = KernelTimer(max(1, launches_per_step * args.steps + 8), [dominant]) if dominant is not None else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if timer is not None:
+        with timer:
+            for _ in range(args.steps):
+                step()
+    else:
+        for _ in range(args.steps):
+            step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    roof = None
+    if timer is not None:
+        ms, n = timer.elapsed(dominant)
+        timer.close()
+        counts = RF.batch_counts(W.detach(), WL, Pm, Pd, Nb, Eb)
+        roof = RF.roofline_entry(dominant, ms, n, counts, args.order, 5, args.d, args.layers, args.steps)
+        roof["class_ms_per_step_profile"] = {RF.NAMES[k]: round(v[0] / 2, 4) for k, v in per.items()}
+
+    value = args.bs * world * args.steps / elapsed
+    res = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "graphs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: seeded QM9-shape graphs (SURVEY.md §8 d generator), random-init weights",
+        "config": {
+            "workload": f"GNN_lg order {args.order}, {args.layers} layers, d={args.d}, fwd+bwd, "
+                        f"{args.bs} QM9-shape graphs per GPU",
+            "graphs_per_gpu": args.bs,
+            "global_batch": args.bs * world,
+            "parallelism": f"dp{world}",
+        },
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(args, batch_cpu, model)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

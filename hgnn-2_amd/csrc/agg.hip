@@ -1,0 +1,251 @@
+// Sparse operator x feature aggregation (the graph_oper / P_multi hot loops).
+//
+// Forward (models/layers/layers_mnb.py:391-434): for one packed output row r
+//   out[r, j*Cg + c]          = sum_{e in G(r)} v_j(e) * Xg[col(e), c]   j < J+2
+//   out[r, J*Cg + c]          = sum_{e in P(r)} Pm(e)  * Xp[col(e), c]
+//   out[r, J*Cg + Cp + c]     = sum_{e in P(r)} Pd(e)  * Xp[col(e), c]
+// i.e. the reference's cat(graph_oper(W, X), P_multi(Pm, Y), P_multi(Pd, Y)) of
+// one layer, built row by row.  One wave per row; the row's entry list is
+// wave-uniform (scalar loads); each gathered feature row is one coalesced
+// vector load of 64 lanes x CPL channels and feeds all J+2 (or both P)
+// coefficients.  Variable degree = a loop of wave-uniform trip count, so the
+// segmented reduction needs no cross-lane traffic at all.
+//
+// Backward: the transposed lists (S_WT, S_PE/S_PN) gather the upstream
+// gradient blocks:  out[r, c] (+)= sum_e sum_j v_j * dA[col, j*C + c]
+//                                + sum_e Pm * dA[col, m_off + c] + Pd * dA[col, d_off + c].
+#include "kernels.h"
+
+namespace hgnn {
+
+template <int CPL>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, int C, int lane, float (&x)[CPL]) {
+    const int c0 = lane * CPL;
+    constexpr uintptr_t AL = (CPL >= 4 ? 16 : 4 * CPL) - 1;
+    if (C == 64 * CPL && (reinterpret_cast<uintptr_t>(p) & AL) == 0) {
+        if constexpr (CPL == 1) {
+            x[0] = p[c0];
+        } else if constexpr (CPL == 2) {
+            const float2 v = *reinterpret_cast<const float2*>(p + c0);
+            x[0] = v.x;
+            x[1] = v.y;
+        } else if constexpr (CPL == 4) {
+            const float4 v = *reinterpret_cast<const float4*>(p + c0);
+            x[0] = v.x;
+            x[1] = v.y;
+            x[2] = v.z;
+            x[3] = v.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPL; i += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(p + c0 + i);
+                x[i] = v.x;
+                x[i + 1] = v.y;
+                x[i + 2] = v.z;
+                x[i + 3] = v.w;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) x[i] = (c0 + i < C) ? p[c0 + i] : 0.f;
+    }
+}
+
+template <int CPL>
+__device__ __forceinline__ void store_row(float* __restrict__ p, int C, int lane, const float (&x)[CPL]) {
+    const int c0 = lane * CPL;
+    constexpr uintptr_t AL = (CPL >= 4 ? 16 : 4 * CPL) - 1;
+    if (C == 64 * CPL && (reinterpret_cast<uintptr_t>(p) & AL) == 0) {
+        if constexpr (CPL == 1) {
+            p[c0] = x[0];
+        } else if constexpr (CPL == 2) {
+            *reinterpret_cast<float2*>(p + c0) = make_float2(x[0], x[1]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPL; i += 4)
+                *reinterpret_cast<float4*>(p + c0 + i) = make_float4(x[i], x[i + 1], x[i + 2], x[i + 3]);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < CPL; ++i)
+            if (c0 + i < C) p[c0 + i] = x[i];
+    }
+}
+
+template <int JT, int CG, int CP>
+__global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
+    const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    if (r >= *a.total_rows) return;
+    float* o = a.out + (long long)r * a.ldo;
+    if constexpr (CG > 0) {
+        float acc[JT][CG];
+#pragma unroll
+        for (int j = 0; j < JT; ++j)
+#pragma unroll
+            for (int i = 0; i < CG; ++i) acc[j][i] = 0.f;
+        const RowInfo ri = a.g.rows[r];
+        const int stride = a.g.stride;
+        for (int e = 0; e < ri.count; ++e) {
+            const float* ent = a.g.entries + (long long)(ri.start + e) * stride;
+            const int col = __float_as_int(ent[0]);
+            float v[JT];
+#pragma unroll
+            for (int j = 0; j < JT; ++j) v[j] = ent[1 + j];
+            float x[CG];
+            load_row<CG>(a.xg + (long long)col * a.cg, a.cg, lane, x);
+#pragma unroll
+            for (int j = 0; j < JT; ++j)
+#pragma unroll
+                for (int i = 0; i < CG; ++i) acc[j][i] = fmaf(v[j], x[i], acc[j][i]);
+        }
+#pragma unroll
+        for (int j = 0; j < JT; ++j) store_row<CG>(o + j * a.cg, a.cg, lane, acc[j]);
+    }
+    if constexpr (CP > 0) {
+        float am[CP], ad[CP];
+#pragma unroll
+        for (int i = 0; i < CP; ++i) am[i] = ad[i] = 0.f;
+        const RowInfo ri = a.p.rows[r];
+        for (int e = 0; e < ri.count; ++e) {
+            const float4 ent = *reinterpret_cast<const float4*>(a.p.entries + (long long)(ri.start + e) * 4);
+            const int col = __float_as_int(ent.x);
+            float x[CP];
+            load_row<CP>(a.xp + (long long)col * a.cp, a.cp, lane, x);
+#pragma unroll
+            for (int i = 0; i < CP; ++i) {
+                am[i] = fmaf(ent.y, x[i], am[i]);
+                ad[i] = fmaf(ent.z, x[i], ad[i]);
+            }
+        }
+        const int base = JT * a.cg;
+        store_row<CP>(o + base, a.cp, lane, am);
+        store_row<CP>(o + base + a.cp, a.cp, lane, ad);
+    }
+}
+
+static int cpl_of(int c) {
+    if (c <= 0) return 0;
+    if (c <= 64) return 1;
+    if (c <= 128) return 2;
+    if (c <= 256) return 4;
+    if (c <= 512) return 8;
+    return -1;
+}
+
+template <int JT, int CG>
+static int agg_fwd_cp(const AggFwdArgs& a, dim3 g, hipStream_t s) {
+    switch (cpl_of(a.xp ? a.cp : 0)) {
+        case 0: hipLaunchKernelGGL((k_agg_fwd<JT, CG, 0>), g, dim3(256), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_agg_fwd<JT, CG, 1>), g, dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_agg_fwd<JT, CG, 2>), g, dim3(256), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_agg_fwd<JT, CG, 4>), g, dim3(256), 0, s, a); break;
+        case 8: hipLaunchKernelGGL((k_agg_fwd<JT, CG, 8>), g, dim3(256), 0, s, a); break;
+        default: return 2;
+    }
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int JT>
+static int agg_fwd_cg(const AggFwdArgs& a, dim3 g, hipStream_t s) {
+    switch (cpl_of(a.xg ? a.cg : 0)) {
+        case 1: return agg_fwd_cp<JT, 1>(a, g, s);
+        case 2: return agg_fwd_cp<JT, 2>(a, g, s);
+        case 4: return agg_fwd_cp<JT, 4>(a, g, s);
+        case 8: return agg_fwd_cp<JT, 8>(a, g, s);
+        default: return 2;
+    }
+}
+
+int launch_agg_fwd(const AggFwdArgs& a, hipStream_t s) {
+    if (a.cap_rows <= 0) return 0;
+    const dim3 g(ceil_div(a.cap_rows, 4));
+    switch (a.jtot) {
+        case 3: return agg_fwd_cg<3>(a, g, s);
+        case 4: return agg_fwd_cg<4>(a, g, s);
+        case 5: return agg_fwd_cg<5>(a, g, s);
+        default: return 2;
+    }
+}
+
+template <int JT, int C, bool HG, bool HP>
+__global__ void __launch_bounds__(256) k_agg_bwd(AggBwdArgs a) {
+    const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    if (r >= *a.total_rows) return;
+    float acc[C];
+    float* o = a.out + (long long)r * a.ldo;
+    if (a.accumulate) {
+        load_row<C>(o, a.c, lane, acc);
+    } else {
+#pragma unroll
+        for (int i = 0; i < C; ++i) acc[i] = 0.f;
+    }
+    if constexpr (HG) {
+        const RowInfo ri = a.g.rows[r];
+        const int stride = a.g.stride;
+        for (int e = 0; e < ri.count; ++e) {
+            const float* ent = a.g.entries + (long long)(ri.start + e) * stride;
+            const int col = __float_as_int(ent[0]);
+            const float* src = a.ing + (long long)col * a.ldg + a.gofs;
+#pragma unroll
+            for (int j = 0; j < JT; ++j) {
+                const float v = ent[1 + j];
+                float x[C];
+                load_row<C>(src + j * a.c, a.c, lane, x);
+#pragma unroll
+                for (int i = 0; i < C; ++i) acc[i] = fmaf(v, x[i], acc[i]);
+            }
+        }
+    }
+    if constexpr (HP) {
+        const RowInfo ri = a.p.rows[r];
+        for (int e = 0; e < ri.count; ++e) {
+            const float4 ent = *reinterpret_cast<const float4*>(a.p.entries + (long long)(ri.start + e) * 4);
+            const int col = __float_as_int(ent.x);
+            const float* src = a.inp + (long long)col * a.ldp;
+            float xm[C], xd[C];
+            load_row<C>(src + a.pofs_m, a.c, lane, xm);
+            load_row<C>(src + a.pofs_d, a.c, lane, xd);
+#pragma unroll
+            for (int i = 0; i < C; ++i) acc[i] = fmaf(ent.z, xd[i], fmaf(ent.y, xm[i], acc[i]));
+        }
+    }
+    store_row<C>(o, a.c, lane, acc);
+}
+
+template <int JT, int C>
+static int agg_bwd_parts(const AggBwdArgs& a, dim3 g, hipStream_t s) {
+    const bool hg = a.ing != nullptr, hp = a.inp != nullptr;
+    if (hg && hp) hipLaunchKernelGGL((k_agg_bwd<JT, C, true, true>), g, dim3(256), 0, s, a);
+    else if (hg) hipLaunchKernelGGL((k_agg_bwd<JT, C, true, false>), g, dim3(256), 0, s, a);
+    else if (hp) hipLaunchKernelGGL((k_agg_bwd<JT, C, false, true>), g, dim3(256), 0, s, a);
+    else return 1;
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int JT>
+static int agg_bwd_c(const AggBwdArgs& a, dim3 g, hipStream_t s) {
+    switch (cpl_of(a.c)) {
+        case 1: return agg_bwd_parts<JT, 1>(a, g, s);
+        case 2: return agg_bwd_parts<JT, 2>(a, g, s);
+        case 4: return agg_bwd_parts<JT, 4>(a, g, s);
+        case 8: return agg_bwd_parts<JT, 8>(a, g, s);
+        default: return 2;
+    }
+}
+
+int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s) {
+    if (a.cap_rows <= 0) return 0;
+    const dim3 g(ceil_div(a.cap_rows, 4));
+    switch (a.jtot) {
+        case 3: return agg_bwd_c<3>(a, g, s);
+        case 4: return agg_bwd_c<4>(a, g, s);
+        case 5: return agg_bwd_c<5>(a, g, s);
+        default: return 2;
+    }
+}
+
+}  // namespace hgnn

@@ -1,0 +1,297 @@
+// Masked batch normalisation with scalar affine parameters
+// (models/layers/batch_normalization.py:23-108) and the readout of the last
+// layer (models/layers/layers_mnb.py:88-95, 379-388).
+//
+// BN statistics are over the REAL rows of the whole batch (mean_with_padding:
+// sum over (b, n) of the masked tensor / sum(N_batch)), var = 1e-5 + mean of
+// squared deviations, std = sqrt(var).  Rows are packed, so "real" = every
+// packed row.  The GEMM epilogue already produced per-64-row-tile (count,
+// mean, M2); they are combined in fp64 (Chan) per channel, which keeps the
+// two-pass accuracy of the reference without a second pass over Y.
+#include "kernels.h"
+
+namespace hgnn {
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+    v = wave_sum_d(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    const int nw = blockDim.x >> 6;
+    for (int i = 0; i < nw; ++i) t += red[i];
+    return t;
+}
+
+__global__ void __launch_bounds__(256) k_bn_finalize(BnFwdArgs a) {
+    __shared__ double red[4];
+    const int ch = blockIdx.x;
+    if (!a.training) {
+        if (threadIdx.x == 0) {
+            a.mean[ch] = a.run_mean[ch];
+            a.std[ch] = a.run_std[ch];
+        }
+        return;
+    }
+    const int rows = *a.count;
+    const int tiles = ceil_div(rows, 64);
+    double n = 0.0, s = 0.0;
+    for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
+        const float* p = a.part + ((long long)t * a.c + ch) * 3;
+        n += (double)p[0];
+        s += (double)p[0] * (double)p[1];
+    }
+    const double N = block_sum_d(n, red);
+    const double S = block_sum_d(s, red);
+    const double mean = N > 0.0 ? S / N : 0.0;
+    double q = 0.0;
+    for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
+        const float* p = a.part + ((long long)t * a.c + ch) * 3;
+        const double dm = (double)p[1] - mean;
+        q += (double)p[2] + (double)p[0] * dm * dm;
+    }
+    const double M2 = block_sum_d(q, red);
+    if (threadIdx.x == 0) {
+        const double var = 1e-5 + (N > 0.0 ? M2 / N : 0.0);
+        const float mf = (float)mean;
+        const float sf = (float)sqrt(var);
+        a.mean[ch] = mf;
+        a.std[ch] = sf;
+        if (a.run_mean) {
+            // running = (1 - momentum) * batch + momentum * running (batch_normalization.py:37-38)
+            const float m1 = 1.0f - a.momentum;
+            a.run_mean[ch] = __fadd_rn(__fmul_rn(m1, mf), __fmul_rn(a.momentum, a.run_mean[ch]));
+            a.run_std[ch] = __fadd_rn(__fmul_rn(m1, sf), __fmul_rn(a.momentum, a.run_std[ch]));
+        }
+    }
+}
+
+int launch_bn_finalize(const BnFwdArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_bn_finalize, dim3(a.c), dim3(256), 0, s, a);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// z = w * ((y - mean) / std) + b   (batch_normalization.py:43, 76)
+__global__ void __launch_bounds__(256) k_bn_apply(const float* __restrict__ y, const int* total_rows,
+                                                  int c, const float* __restrict__ mean,
+                                                  const float* __restrict__ stdv, const float* w,
+                                                  const float* b, float* __restrict__ z) {
+    const long long n = (long long)(*total_rows) * c;
+    const float wv = *w, bv = *b;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int ch = (int)(i % c);
+        const float h = __fdiv_rn(__fsub_rn(y[i], mean[ch]), stdv[ch]);
+        z[i] = __fadd_rn(__fmul_rn(wv, h), bv);
+    }
+}
+
+int launch_bn_apply(const float* y, const int* total_rows, int cap_rows, int c, const float* mean,
+                    const float* std, const float* w, const float* b, float* z, hipStream_t s) {
+    const long long n = (long long)cap_rows * c;
+    int blocks = (int)ceil_div<long long>(n, 256);
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_bn_apply, dim3(blocks), dim3(256), 0, s, y, total_rows, c, mean, std, w, b, z);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// ---------------------------------------------------------------- BN backward
+int bn_bwd_tiles(int cap_rows) { return ceil_div(cap_rows, 64); }
+
+// Per 64-row tile and channel: {sum g, sum g h, sum dz h, sum dz}, g = w dz, h = (y - mean) / std.
+__global__ void __launch_bounds__(256) k_bn_bwd_part(BnBwdArgs a) {
+    const int tile = blockIdx.x;
+    const int total = *a.total_rows;
+    const int r0 = tile * 64;
+    if (r0 >= total) return;
+    const int r1 = min(total, r0 + 64);
+    const float wv = *a.w;
+    for (int ch = threadIdx.x; ch < a.c; ch += blockDim.x) {
+        const float mu = a.mean[ch], sd = a.std[ch];
+        float s1 = 0.f, s2 = 0.f, t1 = 0.f, t2 = 0.f;
+        for (int r = r0; r < r1; ++r) {
+            const long long i = (long long)r * a.c + ch;
+            const float dz = a.dz[i];
+            const float h = __fdiv_rn(__fsub_rn(a.y[i], mu), sd);
+            const float g = wv * dz;
+            s1 += g;
+            s2 = fmaf(g, h, s2);
+            t1 = fmaf(dz, h, t1);
+            t2 += dz;
+        }
+        float* p = a.part + ((long long)tile * a.c + ch) * 4;
+        p[0] = s1;
+        p[1] = s2;
+        p[2] = t1;
+        p[3] = t2;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_bn_bwd_fin(BnBwdArgs a) {
+    __shared__ double red[4];
+    const int ch = blockIdx.x;
+    const int tiles = ceil_div(*a.total_rows, 64);
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
+        const float* p = a.part + ((long long)t * a.c + ch) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += (double)p[j];
+    }
+    double tot[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tot[j] = block_sum_d(v[j], red);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a.sums[ch * 4 + j] = (float)tot[j];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
+    const int total = *a.total_rows;
+    const long long n = (long long)total * a.c;
+    const float wv = *a.w;
+    const float inv_n = total > 0 ? 1.0f / (float)total : 0.f;
+    if (blockIdx.x == 0) {
+        __shared__ double red[4];
+        double t1 = 0.0, t2 = 0.0;
+        for (int ch = threadIdx.x; ch < a.c; ch += blockDim.x) {
+            t1 += (double)a.sums[ch * 4 + 2];
+            t2 += (double)a.sums[ch * 4 + 3];
+        }
+        const double T1 = block_sum_d(t1, red);
+        const double T2 = block_sum_d(t2, red);
+        if (threadIdx.x == 0) {
+            *a.dw = (float)T1;
+            *a.db = (float)T2;
+        }
+    }
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int ch = (int)(i % a.c);
+        const float sd = a.std[ch];
+        const float yv = a.y[i];
+        const float g = wv * a.dz[i];
+        float d;
+        if (a.training) {
+            const float h = __fdiv_rn(__fsub_rn(yv, a.mean[ch]), sd);
+            const float m1 = a.sums[ch * 4 + 0] * inv_n;
+            const float m2 = a.sums[ch * 4 + 1] * inv_n;
+            d = (g - m1 - h * m2) / sd;
+        } else {
+            d = g / sd;
+        }
+        if (ch >= a.relu_from && !(yv > 0.f)) d = 0.f;
+        a.dy[i] = d;
+    }
+}
+
+int launch_bn_backward(const BnBwdArgs& a, hipStream_t s) {
+    const int tiles = bn_bwd_tiles(a.cap_rows);
+    if (tiles > 0) hipLaunchKernelGGL(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
+    HGNN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(a.c), dim3(256), 0, s, a);
+    HGNN_LAUNCH_CHECK();
+    const long long n = (long long)a.cap_rows * a.c;
+    int blocks = (int)ceil_div<long long>(n, 256);
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(blocks), dim3(256), 0, s, a);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// ---------------------------------------------------------------- readout
+// y[b, o] = sum_{n < N_b} sum_k A[n, k] fcw[o, k] + Nmax * fcb[o]
+// The reference sums fc(x1) over all Nmax padded positions; padded positions
+// have x1 = 0, so each contributes exactly fc.bias (layers_mnb.py:92, 386).
+__global__ void __launch_bounds__(256) k_readout_fwd(const float* __restrict__ A, int k,
+                                                     const int* __restrict__ node_off, int nmax,
+                                                     const float* __restrict__ fcw,
+                                                     const float* __restrict__ fcb, int dim_out,
+                                                     float* __restrict__ colsum,
+                                                     float* __restrict__ out) {
+    __shared__ double red[4];
+    const int b = blockIdx.x;
+    const int r0 = node_off[b], r1 = node_off[b + 1];
+    for (int o = 0; o < dim_out; ++o) {
+        double part = 0.0;
+        for (int kk = threadIdx.x; kk < k; kk += blockDim.x) {
+            float cs = 0.f;
+            if (o == 0) {
+                for (int r = r0; r < r1; ++r) cs += A[(long long)r * k + kk];
+                colsum[(long long)b * k + kk] = cs;
+            } else {
+                cs = colsum[(long long)b * k + kk];
+            }
+            part += (double)cs * (double)fcw[(long long)o * k + kk];
+        }
+        const double t = block_sum_d(part, red);
+        if (threadIdx.x == 0) out[b * dim_out + o] = (float)(t + (double)nmax * (double)fcb[o]);
+    }
+}
+
+int launch_readout_fwd(const float* a, int k, const int* node_off, int bs, int nmax, const float* fcw,
+                       const float* fcb, int dim_out, float* colsum, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_readout_fwd, dim3(bs), dim3(256), 0, s, a, k, node_off, nmax, fcw, fcb, dim_out,
+                       colsum, out);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// dA[r, k] = sum_o dout[b(r), o] fcw[o, k]
+__global__ void __launch_bounds__(256) k_readout_bwd_da(const float* __restrict__ dout,
+                                                        const int* __restrict__ node_off,
+                                                        const float* __restrict__ fcw, int dim_out,
+                                                        int k, float* __restrict__ da) {
+    const int b = blockIdx.x;
+    const int r0 = node_off[b], r1 = node_off[b + 1];
+    for (int kk = threadIdx.x; kk < k; kk += blockDim.x) {
+        float v = 0.f;
+        for (int o = 0; o < dim_out; ++o) v = fmaf(dout[b * dim_out + o], fcw[(long long)o * k + kk], v);
+        for (int r = r0; r < r1; ++r) da[(long long)r * k + kk] = v;
+    }
+}
+
+int launch_readout_bwd_da(const float* dout, const int* node_off, int bs, int cap_rows, const int* total_rows,
+                          const float* fcw, int dim_out, int k, float* da, hipStream_t s) {
+    (void)cap_rows;
+    (void)total_rows;
+    hipLaunchKernelGGL(k_readout_bwd_da, dim3(bs), dim3(256), 0, s, dout, node_off, fcw, dim_out, k, da);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// dfcw[o, k] = sum_b dout[b, o] colsum[b, k];  dfcb[o] = Nmax sum_b dout[b, o]
+__global__ void __launch_bounds__(256) k_readout_bwd_params(const float* __restrict__ dout,
+                                                            const float* __restrict__ colsum, int bs,
+                                                            int nmax, int dim_out, int k,
+                                                            float* __restrict__ dfcw,
+                                                            float* __restrict__ dfcb) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < dim_out * k) {
+        const int o = idx / k, kk = idx % k;
+        double s = 0.0;
+        for (int b = 0; b < bs; ++b) s += (double)dout[b * dim_out + o] * (double)colsum[(long long)b * k + kk];
+        dfcw[idx] = (float)s;
+    }
+    if (idx < dim_out) {
+        double s = 0.0;
+        for (int b = 0; b < bs; ++b) s += (double)dout[b * dim_out + idx];
+        dfcb[idx] = (float)(s * (double)nmax);
+    }
+}
+
+int launch_readout_bwd_params(const float* dout, const float* colsum, int bs, int nmax, int dim_out, int k,
+                              float* dfcw, float* dfcb, hipStream_t s) {
+    const int n = dim_out * k > dim_out ? dim_out * k : dim_out;
+    hipLaunchKernelGGL(k_readout_bwd_params, dim3(ceil_div(n, 256)), dim3(256), 0, s, dout, colsum, bs, nmax,
+                       dim_out, k, dfcw, dfcb);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // namespace hgnn

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/hgnn_amd.h"
+
 #define HGNN_WAVE 64
 
 #define HGNN_HOST_CHECK(expr)                                       \

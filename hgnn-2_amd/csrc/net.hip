@@ -1,0 +1,678 @@
+// Network executor: GNN_lg / GNN_simple forward and backward as one enqueue.
+//
+// The reference runs every layer as Python-level torch ops with per-graph
+// Python loops (models/gnns/model_mnb.py:166-174, 232-237; layers_mnb.py).
+// Here the network is a fixed "program" of half-layers derived from the
+// config: each half = aggregate (agg_fwd) -> fused Conv1d pair GEMM with
+// bias/ReLU/BN-partials epilogue -> BN finalize -> BN apply.  The last layer is
+// aggregate -> segmented readout.  Backward walks the program in reverse.  All
+// activations live in one caller-provided workspace laid out here, so a
+// forward+backward is a fixed sequence of launches with no allocation and no
+// host synchronisation (graph-capturable).
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/hgnn_amd.h"
+#include "kernels.h"
+
+namespace hgnn {
+namespace {
+
+constexpr size_t ALIGN = 256;
+
+struct Feat {
+    bool edge;
+    int c;
+    size_t z = 0, y = 0, grad = 0;
+    bool has_y = false;
+};
+
+struct Half {
+    bool edge;
+    int gin, pin;
+    int cg, cp, k;
+    int out, bn;
+    int pw_lin, pb_lin, pw_relu, pb_relu, pbn_w, pbn_b;
+    int relu_from;
+    size_t a = 0, part = 0, mean = 0, stdv = 0;
+};
+
+struct Program {
+    int cap_n = 0, cap_e = 0, jt = 0, d = 0, c2 = 0;
+    int n_params = 0, n_bn = 0;
+    std::vector<Feat> feats;
+    std::vector<Half> halves;
+    int last_gin = -1, last_pin = -1, k_last = 0, p_fcw = 0, p_fcb = 0;
+    size_t a_last = 0, colsum = 0;
+    size_t node_off = 0, edge_off = 0, totals = 0, err = 0;
+    size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
+    int entry_stride_w = 4;
+    size_t dy = 0, da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0;
+    size_t bytes = 0;
+};
+
+struct Bump {
+    size_t top = 0;
+    size_t take(size_t n) {
+        const size_t o = top;
+        top += (n + ALIGN - 1) / ALIGN * ALIGN;
+        return o;
+    }
+};
+
+bool valid_config(const hgnn_net_config* c) {
+    if (!c) return false;
+    if (c->kind != 0 && c->kind != 1) return false;
+    if (c->bs <= 0 || c->nmax <= 0 || c->f_in <= 0 || c->d <= 0 || c->n_layers < 2) return false;
+    if (c->dim_out <= 0) return false;
+    if (c->kind == 1 && (c->emax < 0 || c->order < 1 || c->order > 3)) return false;
+    if (c->j_tot < 3 || c->j_tot > 5) return false;
+    if (2 * c->d > 512) return false;
+    const long long capn = (long long)c->bs * c->nmax;
+    const long long cape = (long long)c->bs * (c->kind == 1 ? c->emax : 0);
+    if (capn * c->nmax > (1ll << 31) - 1) return false;
+    if (cape * (c->emax > c->nmax ? c->emax : c->nmax) > (1ll << 31) - 1) return false;
+    return true;
+}
+
+Program build_program(const hgnn_net_config* c) {
+    Program P;
+    const bool lg = c->kind == 1;
+    P.cap_n = c->bs * c->nmax;
+    P.cap_e = lg ? c->bs * c->emax : 0;
+    P.jt = c->j_tot;
+    P.d = c->d;
+    P.c2 = 2 * c->d;
+    P.entry_stride_w = c->j_tot <= 3 ? 4 : 8;
+    const int L = c->n_layers;
+    P.n_params = (lg ? 12 : 6) * (L - 1) + 2;
+    P.n_bn = (lg ? 2 : 1) * (L - 1);
+
+    auto add_feat = [&](bool edge, int ch) {
+        Feat f;
+        f.edge = edge;
+        f.c = ch;
+        P.feats.push_back(f);
+        return (int)P.feats.size() - 1;
+    };
+    add_feat(false, c->f_in);
+    if (lg) add_feat(true, 1);
+    int in_n = 0, in_e = lg ? 1 : -1;
+    for (int l = 0; l < L - 1; ++l) {
+        if (lg) {
+            const int pb = 12 * l;
+            const int out_n = add_feat(false, P.c2);
+            const int out_e = add_feat(true, P.c2);
+            P.feats[out_n].has_y = P.feats[out_e].has_y = true;
+            Half hn{}, he{};
+            hn.edge = false;
+            hn.gin = in_n;
+            hn.cg = P.feats[in_n].c;
+            hn.out = out_n;
+            hn.bn = 2 * l;
+            hn.pw_relu = pb + 0;
+            hn.pb_relu = pb + 1;
+            hn.pw_lin = pb + 2;
+            hn.pb_lin = pb + 3;
+            hn.pbn_w = pb + 4;
+            hn.pbn_b = pb + 5;
+            hn.relu_from = c->d;
+            he.edge = true;
+            he.gin = in_e;
+            he.cg = P.feats[in_e].c;
+            he.out = out_e;
+            he.bn = 2 * l + 1;
+            he.pw_relu = pb + 6;
+            he.pb_relu = pb + 7;
+            he.pw_lin = pb + 8;
+            he.pb_lin = pb + 9;
+            he.pbn_w = pb + 10;
+            he.pbn_b = pb + 11;
+            he.relu_from = c->d;
+            if (c->order == 1) {  // node first; edge half reads the BN'd node output
+                hn.pin = in_e;
+                he.pin = out_n;
+            } else if (c->order == 2) {  // edge first; node half reads the BN'd edge output
+                he.pin = in_n;
+                hn.pin = out_e;
+            } else {  // independent halves
+                hn.pin = in_e;
+                he.pin = in_n;
+            }
+            hn.cp = P.feats[hn.pin].c;
+            he.cp = P.feats[he.pin].c;
+            hn.k = P.jt * hn.cg + 2 * hn.cp;
+            he.k = P.jt * he.cg + 2 * he.cp;
+            if (c->order == 2) {
+                P.halves.push_back(he);
+                P.halves.push_back(hn);
+            } else {
+                P.halves.push_back(hn);
+                P.halves.push_back(he);
+            }
+            in_n = out_n;
+            in_e = out_e;
+        } else {
+            const int pb = 6 * l;
+            const int out_n = add_feat(false, P.c2);
+            P.feats[out_n].has_y = true;
+            Half h{};
+            h.edge = false;
+            h.gin = in_n;
+            h.cg = P.feats[in_n].c;
+            h.pin = -1;
+            h.cp = 0;
+            h.k = P.jt * h.cg;
+            h.out = out_n;
+            h.bn = l;
+            // layer_simple: cat(relu(cv2(x)), relu(cv1(x))) -> both halves ReLU (layers_mnb.py:59-65)
+            h.pw_lin = pb + 2;
+            h.pb_lin = pb + 3;
+            h.pw_relu = pb + 0;
+            h.pb_relu = pb + 1;
+            h.pbn_w = pb + 4;
+            h.pbn_b = pb + 5;
+            h.relu_from = 0;
+            P.halves.push_back(h);
+            in_n = out_n;
+        }
+    }
+    P.last_gin = in_n;
+    P.last_pin = lg ? in_e : -1;
+    P.k_last = P.jt * P.feats[in_n].c + (lg ? 2 * P.feats[in_e].c : 0);
+    P.p_fcw = P.n_params - 2;
+    P.p_fcb = P.n_params - 1;
+
+    // ---- workspace layout
+    Bump B;
+    P.node_off = B.take(sizeof(int) * (c->bs + 1));
+    P.edge_off = B.take(sizeof(int) * (c->bs + 1));
+    P.totals = B.take(sizeof(int) * 4);
+    P.err = B.take(sizeof(uint32_t) * 4);
+    const int nmax = c->nmax, emax = lg ? c->emax : 0;
+    const size_t sw = P.entry_stride_w * sizeof(float);
+    P.rows[S_W] = B.take(sizeof(RowInfo) * P.cap_n);
+    P.ent[S_W] = B.take((size_t)P.cap_n * nmax * sw);
+    P.rows[S_WT] = B.take(sizeof(RowInfo) * P.cap_n);
+    P.ent[S_WT] = B.take((size_t)P.cap_n * nmax * sw);
+    if (lg) {
+        P.rows[S_WL] = B.take(sizeof(RowInfo) * P.cap_e);
+        P.ent[S_WL] = B.take((size_t)P.cap_e * emax * sw);
+        P.rows[S_WLT] = B.take(sizeof(RowInfo) * P.cap_e);
+        P.ent[S_WLT] = B.take((size_t)P.cap_e * emax * sw);
+        P.rows[S_PN] = B.take(sizeof(RowInfo) * P.cap_n);
+        P.ent[S_PN] = B.take((size_t)P.cap_n * emax * 16);
+        P.rows[S_PE] = B.take(sizeof(RowInfo) * P.cap_e);
+        P.ent[S_PE] = B.take((size_t)P.cap_e * nmax * 16);
+    }
+    for (auto& f : P.feats) {
+        const size_t cap = f.edge ? P.cap_e : P.cap_n;
+        f.z = B.take(cap * f.c * sizeof(float));
+        if (f.has_y) f.y = B.take(cap * f.c * sizeof(float));
+        f.grad = B.take(cap * f.c * sizeof(float));
+    }
+    size_t max_da = 0, max_slab = 0;
+    int max_cap = 0;
+    for (auto& h : P.halves) {
+        const int cap = h.edge ? P.cap_e : P.cap_n;
+        h.a = B.take((size_t)cap * h.k * sizeof(float));
+        h.part = B.take((size_t)gemm_fwd_tiles_m(cap) * P.c2 * 3 * sizeof(float));
+        h.mean = B.take(P.c2 * sizeof(float));
+        h.stdv = B.take(P.c2 * sizeof(float));
+        max_da = std::max(max_da, (size_t)cap * h.k);
+        max_slab = std::max(max_slab, gemm_dw_slab_floats(cap, P.c2, h.k));
+        max_cap = std::max(max_cap, cap);
+    }
+    P.a_last = B.take((size_t)P.cap_n * P.k_last * sizeof(float));
+    P.colsum = B.take((size_t)c->bs * P.k_last * sizeof(float));
+    max_da = std::max(max_da, (size_t)P.cap_n * P.k_last);
+    P.dy = B.take((size_t)max_cap * P.c2 * sizeof(float));
+    P.da = B.take(max_da * sizeof(float));
+    P.slabs = B.take(max_slab * sizeof(float));
+    P.bnb_part = B.take((size_t)bn_bwd_tiles(max_cap) * P.c2 * 4 * sizeof(float));
+    P.bnb_sums = B.take((size_t)P.c2 * 4 * sizeof(float));
+    P.bytes = B.top;
+    return P;
+}
+
+template <typename T>
+T* at(void* ws, size_t off) {
+    return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
+}
+
+BatchMeta meta_of(const Program& P, void* ws) {
+    BatchMeta m;
+    m.node_off = at<int>(ws, P.node_off);
+    m.edge_off = at<int>(ws, P.edge_off);
+    m.totals = at<int>(ws, P.totals);
+    m.err = at<uint32_t>(ws, P.err);
+    return m;
+}
+
+StructView view(const Program& P, void* ws, int kind) {
+    StructView v;
+    v.rows = at<RowInfo>(ws, P.rows[kind]);
+    v.entries = at<float>(ws, P.ent[kind]);
+    v.stride = (kind == S_PN || kind == S_PE) ? 4 : P.entry_stride_w;
+    return v;
+}
+
+#define TRY(x)                  \
+    do {                        \
+        int _r = (x);           \
+        if (_r) return _r;      \
+    } while (0)
+
+// Optional per-kernel-class event timer (bench.py times the dominant kernel
+// inside its timed region with it).  Disabled (nullptr) on the normal path.
+struct Timer {
+    std::vector<hipEvent_t> ev;   // pairs: start, stop
+    std::vector<int> cls;
+    int used = 0;
+    unsigned mask = 0;
+};
+
+#define TL(k, x)                                                                        \
+    do {                                                                                \
+        const bool _t = tm && (tm->mask & (1u << (k))) && tm->used < (int)tm->cls.size(); \
+        if (_t) HGNN_HOST_CHECK(hipEventRecord(tm->ev[2 * tm->used], s));                \
+        int _r = (x);                                                                   \
+        if (_r) return _r;                                                              \
+        if (_t) {                                                                       \
+            HGNN_HOST_CHECK(hipEventRecord(tm->ev[2 * tm->used + 1], s));                \
+            tm->cls[tm->used++] = (k);                                                  \
+        }                                                                               \
+    } while (0)
+
+int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float* const* prm,
+                float* const* run, void* ws, float* out, hipStream_t s, Timer* tm) {
+    const Program P = build_program(c);
+    const bool lg = c->kind == 1;
+    BatchMeta m = meta_of(P, ws);
+    HGNN_HOST_CHECK(hipMemsetAsync(m.err, 0, sizeof(uint32_t), s));
+    TL(HGNN_K_STRUCT, launch_plan(in->d_N_batch, lg ? in->d_E_batch : nullptr, c->bs, c->nmax, lg ? c->emax : 0, m, s));
+
+    ExtractArgs ex{};
+    ex.W = in->d_W;
+    ex.WL = in->d_WL;
+    ex.Pm = in->d_Pm;
+    ex.Pd = in->d_Pd;
+    ex.mask = in->d_mask;
+    ex.mask_lg = in->d_mask_lg;
+    ex.bs = c->bs;
+    ex.nmax = c->nmax;
+    ex.emax = lg ? c->emax : 0;
+    ex.jtot = c->j_tot;
+    ex.meta = m;
+    for (int k = 0; k < S_COUNT; ++k) {
+        ex.rows[k] = at<RowInfo>(ws, P.rows[k]);
+        ex.entries[k] = at<float>(ws, P.ent[k]);
+    }
+    ex.entry_stride_w = P.entry_stride_w;
+    ex.validate = 1;
+    ex.dual = lg ? 1 : 0;
+    TL(HGNN_K_STRUCT, launch_extract(ex, s));
+    TL(HGNN_K_STRUCT, launch_pack_nodes(in->d_X, c->bs, c->f_in, c->nmax, m, at<float>(ws, P.feats[0].z), s));
+    if (lg) TL(HGNN_K_STRUCT, launch_pack_edges(in->d_XL, c->bs, c->emax, m, at<float>(ws, P.feats[1].z), s));
+
+    const int* tot_n = m.totals;
+    const int* tot_e = m.totals + 1;
+    for (const Half& h : P.halves) {
+        const int cap = h.edge ? P.cap_e : P.cap_n;
+        const int* tot = h.edge ? tot_e : tot_n;
+        AggFwdArgs ag{};
+        ag.total_rows = tot;
+        ag.cap_rows = cap;
+        ag.g = view(P, ws, h.edge ? S_WL : S_W);
+        ag.xg = at<float>(ws, P.feats[h.gin].z);
+        ag.cg = h.cg;
+        ag.jtot = P.jt;
+        if (h.pin >= 0) {
+            ag.p = view(P, ws, h.edge ? S_PE : S_PN);
+            ag.xp = at<float>(ws, P.feats[h.pin].z);
+            ag.cp = h.cp;
+        }
+        ag.out = at<float>(ws, h.a);
+        ag.ldo = h.k;
+        TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
+
+        GemmFwdArgs gf{};
+        gf.a = at<float>(ws, h.a);
+        gf.lda = h.k;
+        gf.m_valid = tot;
+        gf.m_cap = cap;
+        gf.k = h.k;
+        gf.w0 = prm[h.pw_lin];
+        gf.w1 = prm[h.pw_relu];
+        gf.b0 = prm[h.pb_lin];
+        gf.b1 = prm[h.pb_relu];
+        gf.n = P.c2;
+        gf.split = P.d;
+        gf.relu_from = h.relu_from;
+        gf.y = at<float>(ws, P.feats[h.out].y);
+        gf.ldy = P.c2;
+        gf.bn_part = c->training ? at<float>(ws, h.part) : nullptr;
+        TL(HGNN_K_GEMM_FWD, launch_gemm_fwd(gf, s));
+
+        BnFwdArgs bf{};
+        bf.part = at<float>(ws, h.part);
+        bf.tiles = gemm_fwd_tiles_m(cap);
+        bf.c = P.c2;
+        bf.count = tot;
+        bf.w = prm[h.pbn_w];
+        bf.b = prm[h.pbn_b];
+        bf.mean = at<float>(ws, h.mean);
+        bf.std = at<float>(ws, h.stdv);
+        bf.run_mean = run ? run[2 * h.bn] : nullptr;
+        bf.run_std = run ? run[2 * h.bn + 1] : nullptr;
+        bf.training = c->training;
+        bf.momentum = 0.1f;
+        if (!c->training && !run) return HGNN_ERR_ARG;
+        TL(HGNN_K_BN_FWD, launch_bn_finalize(bf, s));
+        TL(HGNN_K_BN_FWD, launch_bn_apply(at<float>(ws, P.feats[h.out].y), tot, cap, P.c2, bf.mean, bf.std, bf.w, bf.b,
+                            at<float>(ws, P.feats[h.out].z), s));
+    }
+
+    AggFwdArgs ag{};
+    ag.total_rows = tot_n;
+    ag.cap_rows = P.cap_n;
+    ag.g = view(P, ws, S_W);
+    ag.xg = at<float>(ws, P.feats[P.last_gin].z);
+    ag.cg = P.feats[P.last_gin].c;
+    ag.jtot = P.jt;
+    if (P.last_pin >= 0) {
+        ag.p = view(P, ws, S_PN);
+        ag.xp = at<float>(ws, P.feats[P.last_pin].z);
+        ag.cp = P.feats[P.last_pin].c;
+    }
+    ag.out = at<float>(ws, P.a_last);
+    ag.ldo = P.k_last;
+    TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
+    TL(HGNN_K_READOUT, launch_readout_fwd(at<float>(ws, P.a_last), P.k_last, m.node_off, c->bs, c->nmax, prm[P.p_fcw],
+                           prm[P.p_fcb], c->dim_out, at<float>(ws, P.colsum), out, s));
+    return 0;
+}
+
+int net_backward(const hgnn_net_config* c, const float* const* prm, void* ws, const float* dout,
+                 float* const* grads, float* dX, hipStream_t s, Timer* tm) {
+    const Program P = build_program(c);
+    BatchMeta m = meta_of(P, ws);
+    const int* tot_n = m.totals;
+    const int* tot_e = m.totals + 1;
+    std::vector<char> init(P.feats.size(), 0);
+    auto needs_grad = [&](int f) {
+        if (f < 0) return false;
+        if (f == 0) return c->need_dx != 0;
+        if (c->kind == 1 && f == 1) return false;  // XL never requires grad (scripts/train_mnb.py:56-66)
+        return true;
+    };
+
+    // readout
+    TL(HGNN_K_READOUT, launch_readout_bwd_params(dout, at<float>(ws, P.colsum), c->bs, c->nmax, c->dim_out, P.k_last,
+                                  grads[P.p_fcw], grads[P.p_fcb], s));
+    if (needs_grad(P.last_gin) || needs_grad(P.last_pin)) {
+        float* da = at<float>(ws, P.da);
+        TL(HGNN_K_READOUT, launch_readout_bwd_da(dout, m.node_off, c->bs, P.cap_n, tot_n, prm[P.p_fcw], c->dim_out, P.k_last,
+                                  da, s));
+        const int cg = P.feats[P.last_gin].c;
+        if (needs_grad(P.last_gin)) {
+            AggBwdArgs ab{};
+            ab.total_rows = tot_n;
+            ab.cap_rows = P.cap_n;
+            ab.g = view(P, ws, S_WT);
+            ab.ing = da;
+            ab.ldg = P.k_last;
+            ab.gofs = 0;
+            ab.jtot = P.jt;
+            ab.c = cg;
+            ab.out = at<float>(ws, P.feats[P.last_gin].grad);
+            ab.ldo = cg;
+            ab.accumulate = init[P.last_gin];
+            TL(HGNN_K_AGG_BWD, launch_agg_bwd(ab, s));
+            init[P.last_gin] = 1;
+        }
+        if (needs_grad(P.last_pin)) {
+            const int cp = P.feats[P.last_pin].c;
+            AggBwdArgs ab{};
+            ab.total_rows = tot_e;
+            ab.cap_rows = P.cap_e;
+            ab.p = view(P, ws, S_PE);
+            ab.inp = da;
+            ab.ldp = P.k_last;
+            ab.pofs_m = P.jt * cg;
+            ab.pofs_d = P.jt * cg + cp;
+            ab.jtot = P.jt;
+            ab.c = cp;
+            ab.out = at<float>(ws, P.feats[P.last_pin].grad);
+            ab.ldo = cp;
+            ab.accumulate = init[P.last_pin];
+            TL(HGNN_K_AGG_BWD, launch_agg_bwd(ab, s));
+            init[P.last_pin] = 1;
+        }
+    }
+
+    for (int hi = (int)P.halves.size() - 1; hi >= 0; --hi) {
+        const Half& h = P.halves[hi];
+        const int cap = h.edge ? P.cap_e : P.cap_n;
+        const int* tot = h.edge ? tot_e : tot_n;
+        if (!init[h.out]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[h.out].grad), 0,
+                                                          (size_t)cap * P.c2 * sizeof(float), s));
+        BnBwdArgs bb{};
+        bb.y = at<float>(ws, P.feats[h.out].y);
+        bb.dz = at<float>(ws, P.feats[h.out].grad);
+        bb.total_rows = tot;
+        bb.cap_rows = cap;
+        bb.c = P.c2;
+        bb.mean = at<float>(ws, h.mean);
+        bb.std = at<float>(ws, h.stdv);
+        bb.w = prm[h.pbn_w];
+        bb.relu_from = h.relu_from;
+        bb.training = c->training;
+        bb.part = at<float>(ws, P.bnb_part);
+        bb.sums = at<float>(ws, P.bnb_sums);
+        bb.dy = at<float>(ws, P.dy);
+        bb.dw = grads[h.pbn_w];
+        bb.db = grads[h.pbn_b];
+        TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s));
+
+        GemmDwArgs gw{};
+        gw.dy = at<float>(ws, P.dy);
+        gw.lddy = P.c2;
+        gw.a = at<float>(ws, h.a);
+        gw.lda = h.k;
+        gw.r_valid = tot;
+        gw.r_cap = cap;
+        gw.o = P.c2;
+        gw.k = h.k;
+        gw.split = P.d;
+        gw.slabs = at<float>(ws, P.slabs);
+        gw.dw0 = grads[h.pw_lin];
+        gw.dw1 = grads[h.pw_relu];
+        gw.db0 = grads[h.pb_lin];
+        gw.db1 = grads[h.pb_relu];
+        TL(HGNN_K_GEMM_DW, launch_gemm_dw(gw, s));
+
+        const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
+        if (!ng && !np) continue;
+        float* da = at<float>(ws, P.da);
+        GemmDaArgs gd{};
+        gd.dy = at<float>(ws, P.dy);
+        gd.lddy = P.c2;
+        gd.m_valid = tot;
+        gd.m_cap = cap;
+        gd.o = P.c2;
+        gd.w0 = prm[h.pw_lin];
+        gd.w1 = prm[h.pw_relu];
+        gd.split = P.d;
+        gd.k = h.k;
+        gd.da = da;
+        gd.ldda = h.k;
+        TL(HGNN_K_GEMM_DA, launch_gemm_da(gd, s));
+        if (ng) {
+            AggBwdArgs ab{};
+            ab.total_rows = tot;
+            ab.cap_rows = cap;
+            ab.g = view(P, ws, h.edge ? S_WLT : S_WT);
+            ab.ing = da;
+            ab.ldg = h.k;
+            ab.gofs = 0;
+            ab.jtot = P.jt;
+            ab.c = h.cg;
+            ab.out = at<float>(ws, P.feats[h.gin].grad);
+            ab.ldo = h.cg;
+            ab.accumulate = init[h.gin];
+            TL(HGNN_K_AGG_BWD, launch_agg_bwd(ab, s));
+            init[h.gin] = 1;
+        }
+        if (np) {
+            const bool other_edge = !h.edge;
+            AggBwdArgs ab{};
+            ab.total_rows = other_edge ? tot_e : tot_n;
+            ab.cap_rows = other_edge ? P.cap_e : P.cap_n;
+            ab.p = view(P, ws, h.edge ? S_PN : S_PE);
+            ab.inp = da;
+            ab.ldp = h.k;
+            ab.pofs_m = P.jt * h.cg;
+            ab.pofs_d = P.jt * h.cg + h.cp;
+            ab.jtot = P.jt;
+            ab.c = h.cp;
+            ab.out = at<float>(ws, P.feats[h.pin].grad);
+            ab.ldo = h.cp;
+            ab.accumulate = init[h.pin];
+            TL(HGNN_K_AGG_BWD, launch_agg_bwd(ab, s));
+            init[h.pin] = 1;
+        }
+    }
+    if (c->need_dx) {
+        if (!dX) return HGNN_ERR_ARG;
+        if (!init[0]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[0].grad), 0,
+                                                     (size_t)P.cap_n * c->f_in * sizeof(float), s));
+        TL(HGNN_K_STRUCT, launch_unpack_nodes(at<float>(ws, P.feats[0].grad), c->bs, c->f_in, c->nmax, m, dX, s));
+    }
+    return 0;
+}
+
+}  // namespace
+}  // namespace hgnn
+
+using namespace hgnn;
+
+extern "C" {
+
+int hgnn_abi_version(void) { return HGNN_ABI_VERSION; }
+
+const char* hgnn_status_string(int status) {
+    switch (status) {
+        case HGNN_OK: return "ok";
+        case HGNN_ERR_ARG: return "invalid argument";
+        case HGNN_ERR_UNSUPPORTED: return "unsupported configuration";
+        case HGNN_ERR_HIP: return "HIP runtime error";
+        default: return "unknown status";
+    }
+}
+
+int hgnn_net_param_count(const hgnn_net_config* cfg) {
+    if (!valid_config(cfg)) return -1;
+    return (cfg->kind == 1 ? 12 : 6) * (cfg->n_layers - 1) + 2;
+}
+
+int hgnn_net_bn_count(const hgnn_net_config* cfg) {
+    if (!valid_config(cfg)) return -1;
+    return (cfg->kind == 1 ? 2 : 1) * (cfg->n_layers - 1);
+}
+
+size_t hgnn_net_workspace_bytes(const hgnn_net_config* cfg) {
+    if (!valid_config(cfg)) return 0;
+    return build_program(cfg).bytes;
+}
+
+uint32_t* hgnn_net_error_word(const hgnn_net_config* cfg, void* workspace) {
+    if (!valid_config(cfg) || !workspace) return nullptr;
+    return at<uint32_t>(workspace, build_program(cfg).err);
+}
+
+int hgnn_net_forward(const hgnn_net_config* cfg, const hgnn_net_inputs* in, const float* const* params,
+                     float* const* bn_running, void* workspace, float* d_out, void* stream) {
+    if (!valid_config(cfg) || !in || !params || !workspace || !d_out) return HGNN_ERR_ARG;
+    if (!in->d_X || !in->d_W || !in->d_N_batch || !in->d_mask) return HGNN_ERR_ARG;
+    if (cfg->kind == 1 && (!in->d_XL || !in->d_WL || !in->d_Pm || !in->d_Pd || !in->d_E_batch || !in->d_mask_lg))
+        return HGNN_ERR_ARG;
+    return net_forward(cfg, in, params, bn_running, workspace, d_out, static_cast<hipStream_t>(stream), nullptr);
+}
+
+int hgnn_net_backward(const hgnn_net_config* cfg, const hgnn_net_inputs* in, const float* const* params,
+                      void* workspace, const float* d_dout, float* const* grads, float* d_dX, float* d_dW,
+                      void* stream) {
+    (void)in;
+    if (!valid_config(cfg) || !params || !workspace || !d_dout || !grads) return HGNN_ERR_ARG;
+    if (cfg->need_dw) {
+        (void)d_dW;
+        return HGNN_ERR_UNSUPPORTED;
+    }
+    return net_backward(cfg, params, workspace, d_dout, grads, d_dX, static_cast<hipStream_t>(stream), nullptr);
+}
+
+void* hgnn_timer_create(int max_launches, unsigned class_mask) {
+    if (max_launches <= 0) return nullptr;
+    Timer* t = new Timer();
+    t->ev.resize(2 * (size_t)max_launches);
+    t->cls.resize(max_launches);
+    t->mask = class_mask;
+    for (auto& e : t->ev) {
+        if (hipEventCreate(&e) != hipSuccess) {
+            delete t;
+            return nullptr;
+        }
+    }
+    return t;
+}
+
+void hgnn_timer_reset(void* timer) {
+    if (timer) static_cast<Timer*>(timer)->used = 0;
+}
+
+int hgnn_timer_elapsed(void* timer, int kernel_class, double* total_ms, int* launches) {
+    if (!timer || !total_ms || !launches) return HGNN_ERR_ARG;
+    Timer* t = static_cast<Timer*>(timer);
+    double tot = 0.0;
+    int n = 0;
+    for (int i = 0; i < t->used; ++i) {
+        if (t->cls[i] != kernel_class) continue;
+        float ms = 0.f;
+        if (hipEventSynchronize(t->ev[2 * i + 1]) != hipSuccess) return HGNN_ERR_HIP;
+        if (hipEventElapsedTime(&ms, t->ev[2 * i], t->ev[2 * i + 1]) != hipSuccess) return HGNN_ERR_HIP;
+        tot += ms;
+        ++n;
+    }
+    *total_ms = tot;
+    *launches = n;
+    return HGNN_OK;
+}
+
+void hgnn_timer_destroy(void* timer) {
+    if (!timer) return;
+    Timer* t = static_cast<Timer*>(timer);
+    for (auto& e : t->ev) (void)hipEventDestroy(e);
+    delete t;
+}
+
+int hgnn_net_forward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* in, const float* const* params,
+                           float* const* bn_running, void* workspace, float* d_out, void* stream, void* timer) {
+    if (!valid_config(cfg) || !in || !params || !workspace || !d_out) return HGNN_ERR_ARG;
+    return net_forward(cfg, in, params, bn_running, workspace, d_out, static_cast<hipStream_t>(stream),
+                       static_cast<Timer*>(timer));
+}
+
+int hgnn_net_backward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* in, const float* const* params,
+                            void* workspace, const float* d_dout, float* const* grads, float* d_dX, float* d_dW,
+                            void* stream, void* timer) {
+    (void)in;
+    (void)d_dW;
+    if (!valid_config(cfg) || !params || !workspace || !d_dout || !grads) return HGNN_ERR_ARG;
+    if (cfg->need_dw) return HGNN_ERR_UNSUPPORTED;
+    return net_backward(cfg, params, workspace, d_dout, grads, d_dX, static_cast<hipStream_t>(stream),
+                        static_cast<Timer*>(timer));
+}
+
+}  // extern "C"

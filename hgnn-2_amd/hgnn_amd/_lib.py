@@ -1,0 +1,116 @@
+"""ctypes binding of include/hgnn_amd.h (the C ABI of the gfx950 hot path).
+
+The shared library is built in-tree (``make -C hgnn-2_amd`` or
+``__graft_entry__.build()``) next to this file.  torch is imported first so
+that the HIP runtime torch already loaded (same soname, libamdhip64.so.7) is
+the one the library binds to: one runtime per process.
+
+There is no fallback: if the library is missing, every product entry point
+raises.
+"""
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before ours)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhgnn_amd.so")
+
+HGNN_OK = 0
+STATUS = {0: "ok", 1: "invalid argument", 2: "unsupported configuration", 3: "HIP runtime error"}
+DEVERR = {
+    0x1: "operator entry outside a graph's real block (padding must be zero)",
+    0x2: "mask[:, :, 0] disagrees with N_batch / E_batch",
+    0x4: "N_batch > Nmax, E_batch > Emax or a negative count",
+    0x8: "CCN adjacency without a self loop (chi_ii undefined, functions/utils_ccn.py:137-140)",
+    0x10: "CCN vertex degree above the compiled bound",
+}
+
+
+class NetConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "kind", "order", "bs", "nmax", "emax", "f_in", "d", "n_layers", "j_tot", "dim_out",
+        "training", "need_dx", "need_dw", "reserved")]
+
+
+class NetInputs(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "d_X", "d_XL", "d_W", "d_WL", "d_Pm", "d_Pd", "d_N_batch", "d_E_batch", "d_mask", "d_mask_lg")]
+
+
+_lib = None
+
+_VP = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+
+SIGNATURES = {
+    "hgnn_abi_version": ([], _I),
+    "hgnn_status_string": ([_I], ctypes.c_char_p),
+    "hgnn_net_param_count": ([ctypes.POINTER(NetConfig)], _I),
+    "hgnn_net_bn_count": ([ctypes.POINTER(NetConfig)], _I),
+    "hgnn_net_workspace_bytes": ([ctypes.POINTER(NetConfig)], ctypes.c_size_t),
+    "hgnn_net_error_word": ([ctypes.POINTER(NetConfig), _VP], _VP),
+    "hgnn_net_forward": ([ctypes.POINTER(NetConfig), ctypes.POINTER(NetInputs), _VP, _VP, _VP, _VP, _VP], _I),
+    "hgnn_net_backward": ([ctypes.POINTER(NetConfig), ctypes.POINTER(NetInputs), _VP, _VP, _VP, _VP, _VP, _VP,
+                           _VP], _I),
+    "hgnn_graph_oper_forward": ([_VP, _VP, _VP, _I, _I, _I, _I, _VP], _I),
+    "hgnn_graph_oper_backward": ([_VP, _VP, _VP, _VP, _VP, _I, _I, _I, _I, _VP], _I),
+    "hgnn_p_multi_forward": ([_VP, _L, _L, _L, _VP, _VP, _I, _I, _I, _I, _VP], _I),
+    "hgnn_p_multi_backward": ([_VP, _L, _L, _L, _VP, _VP, _VP, _VP, _I, _I, _I, _I, _VP], _I),
+    "hgnn_bn_forward": ([_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _I, _VP], _I),
+    "hgnn_bn_backward": ([_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _I, _VP], _I),
+    "hgnn_timer_create": ([_I, ctypes.c_uint], _VP),
+    "hgnn_timer_reset": ([_VP], None),
+    "hgnn_timer_elapsed": ([_VP, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)], _I),
+    "hgnn_timer_destroy": ([_VP], None),
+    "hgnn_net_forward_timed": ([ctypes.POINTER(NetConfig), ctypes.POINTER(NetInputs), _VP, _VP, _VP, _VP, _VP,
+                                _VP], _I),
+    "hgnn_net_backward_timed": ([ctypes.POINTER(NetConfig), ctypes.POINTER(NetInputs), _VP, _VP, _VP, _VP, _VP,
+                                 _VP, _VP, _VP], _I),
+    "hgnn_conv1x1_workspace_bytes": ([_I, _I, _I, _I], ctypes.c_size_t),
+    "hgnn_conv1x1_forward": ([_VP, _VP, _VP, _VP, _I, _I, _I, _I, _I, _VP, _VP], _I),
+    "hgnn_conv1x1_backward": ([_VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _I, _VP, _VP], _I),
+}
+
+
+def lib():
+    """Load (once) and return the shared library; raise if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"hgnn_amd: native library not found at {LIB_PATH}; build it with "
+                "`make -C hgnn-2_amd` (or __graft_entry__.build()). There is no CPU fallback.")
+        h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = h
+    return _lib
+
+
+def check(status, what):
+    if status != HGNN_OK:
+        raise RuntimeError(f"hgnn_amd: {what} failed: {STATUS.get(status, status)}")
+
+
+def deverr_message(bits):
+    msgs = [m for b, m in DEVERR.items() if bits & b]
+    return "; ".join(msgs) if msgs else f"device error bits {bits:#x}"
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def ptr_array(tensors):
+    arr = (ctypes.c_void_p * len(tensors))()
+    for i, t in enumerate(tensors):
+        arr[i] = None if t is None else t.data_ptr()
+    return arr
+
+
+def stream_handle(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,280 @@
+"""Autograd binding of the network executor (hgnn_net_forward / _backward).
+
+One torch.autograd.Function runs a whole GNN_lg / GNN_simple forward as a
+single enqueue of HIP kernels (include/hgnn_amd.h, hgnn-2_amd/csrc/net.hip) and
+its backward as another, so `loss.backward()` in the reference's training
+loop (scripts/train_mnb.py:90) works unchanged.
+
+Input validation that needs the batch content (padding of the dense
+operators, mask vs N_batch) runs on the device and sets an error word; the
+host checks it without stalling the stream: at the next forward, at
+`check_errors()`, or immediately when HGNN_STRICT=1.
+"""
+
+import ctypes
+import os
+
+import torch
+
+from . import _lib as L
+
+_pending = []
+_timer = None
+
+
+class KernelTimer:
+    """HIP-event timer around every launch of the selected kernel classes (HGNN_K_*)."""
+
+    def __init__(self, max_launches, classes):
+        mask = 0
+        for c in classes:
+            mask |= 1 << c
+        self.handle = L.lib().hgnn_timer_create(max_launches, mask)
+        if not self.handle:
+            raise RuntimeError("hgnn_amd: could not create the kernel timer")
+
+    def reset(self):
+        L.lib().hgnn_timer_reset(self.handle)
+
+    def elapsed(self, kcls):
+        ms = ctypes.c_double()
+        n = ctypes.c_int()
+        L.check(L.lib().hgnn_timer_elapsed(self.handle, kcls, ctypes.byref(ms), ctypes.byref(n)), "timer")
+        return ms.value, n.value
+
+    def close(self):
+        if self.handle:
+            L.lib().hgnn_timer_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        global _timer
+        _timer = self
+        return self
+
+    def __exit__(self, *exc):
+        global _timer
+        _timer = None
+
+
+def strict():
+    return os.environ.get("HGNN_STRICT", "0") == "1"
+
+
+def _raise_bits(bits):
+    raise RuntimeError("hgnn_amd: invalid input batch: " + L.deverr_message(bits))
+
+
+def check_errors(block=True):
+    """Raise if any enqueued forward found an invalid input batch."""
+    keep = []
+    bad = 0
+    for ev, err in _pending:
+        if block or ev.query():
+            bad |= int(err.item())
+        else:
+            keep.append((ev, err))
+    _pending[:] = keep
+    if bad:
+        _pending.clear()
+        _raise_bits(bad)
+
+
+def _watch_error_word(cfg, ws):
+    base = ws.data_ptr()
+    addr = L.lib().hgnn_net_error_word(ctypes.byref(cfg), ctypes.c_void_p(base))
+    off = int(addr) - base
+    err = ws[off:off + 4].view(torch.int32).clone()
+    if strict():
+        v = int(err.item())
+        if v:
+            _raise_bits(v)
+        return
+    ev = torch.cuda.Event()
+    ev.record()
+    _pending.append((ev, err))
+
+
+def _require_cuda(tensors, what):
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                f"hgnn_amd: {what} runs on the GPU only; got a CPU tensor (move the batch with .cuda(), "
+                "as scripts/train_mnb.py:60 does)")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"hgnn_amd: {what}: tensors on different devices ({dev} vs {t.device})")
+    return dev
+
+
+def _f32(t):
+    if t is None:
+        return None
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"hgnn_amd: expected float32 tensors, got {t.dtype}")
+    return t.contiguous()
+
+
+def _i64(t):
+    return t.to(torch.int64).contiguous()
+
+
+class NetSpec:
+    """Static description of a network call (model hyper-parameters + mode)."""
+
+    def __init__(self, kind, order, d, n_layers, dim_out, params, running, training):
+        self.kind = kind
+        self.order = order
+        self.d = d
+        self.n_layers = n_layers
+        self.dim_out = dim_out
+        self.params = params
+        self.running = running
+        self.training = training
+
+
+def expected_k(kind, order, f_in, d, n_layers, jt):
+    """Input widths (K) of every Conv1d, in ABI parameter order (mirrors net.hip build_program)."""
+    ks = []
+    c2 = 2 * d
+    cn, ce = f_in, 1
+    for _ in range(n_layers - 1):
+        if kind == 1:
+            if order == 1:
+                kn, ke = jt * cn + 2 * ce, jt * ce + 2 * c2
+            elif order == 2:
+                kn, ke = jt * cn + 2 * c2, jt * ce + 2 * cn
+            else:
+                kn, ke = jt * cn + 2 * ce, jt * ce + 2 * cn
+            ks.append((kn, ke))
+            cn, ce = c2, c2
+        else:
+            ks.append((jt * cn,))
+            cn = c2
+    k_last = jt * cn + (2 * ce if kind == 1 else 0)
+    return ks, k_last
+
+
+class _NetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec, tensors, X, W, *params):
+        XL, WL, Pm, Pd, Nb, Eb, mask, mask_lg = tensors
+        dev = X.device
+        lg = spec.kind == 1
+        cfg = L.NetConfig()
+        cfg.kind = spec.kind
+        cfg.order = spec.order
+        cfg.bs = X.shape[0]
+        cfg.nmax = X.shape[2]
+        cfg.emax = XL.shape[2] if lg else 0
+        cfg.f_in = X.shape[1]
+        cfg.d = spec.d
+        cfg.n_layers = spec.n_layers
+        cfg.j_tot = W.shape[3]
+        cfg.dim_out = spec.dim_out
+        cfg.training = 1 if spec.training else 0
+        lib = L.lib()
+        nbytes = lib.hgnn_net_workspace_bytes(ctypes.byref(cfg))
+        if nbytes == 0:
+            raise RuntimeError("hgnn_amd: unsupported network configuration "
+                               f"(bs={cfg.bs}, Nmax={cfg.nmax}, Emax={cfg.emax}, J+2={cfg.j_tot}, d={cfg.d})")
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        out = torch.empty(cfg.bs, cfg.dim_out, dtype=torch.float32, device=dev)
+        inp = L.NetInputs()
+        inp.d_X = X.data_ptr()
+        inp.d_W = W.data_ptr()
+        inp.d_N_batch = Nb.data_ptr()
+        inp.d_mask = mask.data_ptr()
+        if lg:
+            inp.d_XL = XL.data_ptr()
+            inp.d_WL = WL.data_ptr()
+            inp.d_Pm = Pm.data_ptr()
+            inp.d_Pd = Pd.data_ptr()
+            inp.d_E_batch = Eb.data_ptr()
+            inp.d_mask_lg = mask_lg.data_ptr()
+        run = L.ptr_array(spec.running)
+        args = (ctypes.byref(cfg), ctypes.byref(inp), L.ptr_array(params), run, ctypes.c_void_p(ws.data_ptr()),
+                ctypes.c_void_p(out.data_ptr()), L.stream_handle(dev))
+        if _timer is not None:
+            st = lib.hgnn_net_forward_timed(*args, ctypes.c_void_p(_timer.handle))
+        else:
+            st = lib.hgnn_net_forward(*args)
+        L.check(st, "network forward")
+        _watch_error_word(cfg, ws)
+        ctx.cfg = cfg
+        ctx.ws = ws
+        ctx.inp = inp
+        ctx.keep = (X, W, XL, WL, Pm, Pd, Nb, Eb, mask, mask_lg)
+        ctx.params = params
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        cfg = ctx.cfg
+        X = ctx.keep[0]
+        dout = dout.contiguous().to(torch.float32)
+        grads = [torch.empty_like(p) for p in ctx.params]
+        dX = torch.empty_like(X) if ctx.needs_input_grad[2] else None
+        cfg.need_dx = 1 if dX is not None else 0
+        cfg.need_dw = 0
+        args = (ctypes.byref(cfg), ctypes.byref(ctx.inp), L.ptr_array(ctx.params), ctypes.c_void_p(ctx.ws.data_ptr()),
+                ctypes.c_void_p(dout.data_ptr()), L.ptr_array(grads), L.ptr(dX), None, L.stream_handle(X.device))
+        if _timer is not None:
+            st = L.lib().hgnn_net_backward_timed(*args, ctypes.c_void_p(_timer.handle))
+        else:
+            st = L.lib().hgnn_net_backward(*args)
+        L.check(st, "network backward")
+        return (None, None, dX, None, *grads)
+
+
+def run_net(spec, X, W, N_batch, mask, XL=None, WL=None, Pm=None, Pd=None, E_batch=None, mask_lg=None):
+    """Forward of GNN_simple (kind 0) / GNN_lg (kind 1) through the HIP executor."""
+    check_errors(block=False)
+    lg = spec.kind == 1
+    tensors_in = [X, W, N_batch, mask] + ([XL, WL, Pm, Pd, E_batch, mask_lg] if lg else [])
+    dev = _require_cuda(tensors_in, "GNN forward")
+    X = _f32(X)
+    W = _f32(W)
+    mask = _f32(mask)
+    Nb = _i64(N_batch)
+    bs, f_in, nmax = X.shape
+    if W.dim() != 4 or W.shape[:3] != (bs, nmax, nmax):
+        raise RuntimeError(f"hgnn_amd: W must be (bs, Nmax, Nmax, J+2) = ({bs}, {nmax}, {nmax}, .), got {tuple(W.shape)}")
+    if mask.shape != (bs, nmax, nmax) or Nb.shape != (bs,):
+        raise RuntimeError("hgnn_amd: mask must be (bs, Nmax, Nmax) and N_batch (bs,)")
+    if lg:
+        XL, WL, Pm, Pd, mask_lg = map(_f32, (XL, WL, Pm, Pd, mask_lg))
+        Eb = _i64(E_batch)
+        emax = XL.shape[2]
+        jt = W.shape[3]
+        if XL.shape != (bs, 1, emax):
+            raise RuntimeError(f"hgnn_amd: XL must be (bs, 1, Emax), got {tuple(XL.shape)}")
+        if WL.shape != (bs, emax, emax, jt):
+            raise RuntimeError(f"hgnn_amd: WL must be (bs, Emax, Emax, J+2), got {tuple(WL.shape)}")
+        if Pm.shape != (bs, nmax, emax) or Pd.shape != (bs, nmax, emax):
+            raise RuntimeError("hgnn_amd: Pm/Pd must be (bs, Nmax, Emax)")
+        if mask_lg.shape != (bs, emax, emax) or Eb.shape != (bs,):
+            raise RuntimeError("hgnn_amd: mask_lg must be (bs, Emax, Emax) and E_batch (bs,)")
+    else:
+        Eb = None
+    ks, k_last = expected_k(spec.kind, spec.order, f_in, spec.d, spec.n_layers, W.shape[3])
+    params = list(spec.params)
+    per = 12 if lg else 6
+    for l, kk in enumerate(ks):
+        convs = [(0, kk[0]), (2, kk[0])] + ([(6, kk[1]), (8, kk[1])] if lg else [])
+        for off, k in convs:
+            w = params[l * per + off]
+            if w.shape != (spec.d, k, 1):
+                raise RuntimeError(f"hgnn_amd: layer {l} conv weight {tuple(w.shape)} != ({spec.d}, {k}, 1)")
+    if params[-2].shape != (spec.dim_out, k_last, 1):
+        raise RuntimeError(f"hgnn_amd: fc weight {tuple(params[-2].shape)} != ({spec.dim_out}, {k_last}, 1)")
+    for p in params:
+        if p.device != dev or p.dtype != torch.float32:
+            raise RuntimeError("hgnn_amd: parameters must be float32 on the input device (call model.cuda())")
+    params = [p if p.is_contiguous() else p.contiguous() for p in params]
+    tensors = (XL, WL, Pm, Pd, Nb, Eb, mask, mask_lg)
+    return _NetFn.apply(spec, tensors, X, W, *params)

@@ -1,0 +1,112 @@
+"""Algorithmic work (FLOPs / compulsory HBM bytes) of each kernel class of the executor.
+
+Used by bench.py to turn a measured kernel-class duration into a roofline
+fraction.  Counts follow SURVEY.md §8 d: sizes from the actual batch (real,
+unpadded rows; nnz of the extracted operator lists including the phantom edge
+slots), fp32 = 4 B, index = 4 B; every input row read once, every output row
+written once (gather re-reads served on chip are not algorithmic traffic).
+"""
+
+import torch
+
+from .net import expected_k
+
+PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_FP32_MFMA_TFS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak
+
+K_STRUCT, K_AGG_FWD, K_GEMM_FWD, K_BN_FWD, K_READOUT, K_BN_BWD, K_GEMM_DW, K_GEMM_DA, K_AGG_BWD = range(9)
+NAMES = ["struct", "agg_fwd", "gemm_fwd", "bn_fwd", "readout", "bn_bwd", "gemm_dw", "gemm_da", "agg_bwd"]
+
+
+def batch_counts(W, WL, Pm, Pd, N_batch, E_batch):
+    """Real rows and union-pattern nnz of the operator lists (host, from the dense batch)."""
+    nW = int((W != 0).any(dim=3).sum())
+    nWL = int((WL != 0).any(dim=3).sum())
+    nP = int(((Pm != 0) | (Pd != 0)).sum())
+    return dict(nodes=int(N_batch.sum()), edges=int(E_batch.sum()), nnz_w=nW, nnz_wl=nWL, nnz_p=nP)
+
+
+def lg_halves(order, f_in, d, n_layers, jt):
+    """(edge?, rows key, K, Cg, Cp) per half in program order, mirroring net.hip build_program."""
+    ks, k_last = expected_k(1, order, f_in, d, n_layers, jt)
+    out = []
+    cn, ce = f_in, 1
+    for kn, ke in ks:
+        if order == 1:
+            hs = [(False, kn, cn, ce), (True, ke, ce, 2 * d)]
+        elif order == 2:
+            hs = [(True, ke, ce, cn), (False, kn, cn, 2 * d)]
+        else:
+            hs = [(False, kn, cn, ce), (True, ke, ce, cn)]
+        out += hs
+        cn, ce = 2 * d, 2 * d
+    return out, k_last
+
+
+def class_work(kcls, counts, order, f_in, d, n_layers, jt=3):
+    """(flops, bytes) of one training step for kernel class kcls (sum over its launches)."""
+    halves, k_last = lg_halves(order, f_in, d, n_layers, jt)
+    c2 = 2 * d
+    rows = lambda edge: counts["edges"] if edge else counts["nodes"]  # noqa: E731
+    nnz_g = lambda edge: counts["nnz_wl"] if edge else counts["nnz_w"]  # noqa: E731
+    fl = by = 0.0
+    if kcls == K_GEMM_FWD:
+        for edge, k, cg, cp in halves:
+            r = rows(edge)
+            fl += 2.0 * r * k * c2
+            by += 4.0 * (r * k + r * c2 + c2 * (k + 1))
+    elif kcls == K_GEMM_DA:
+        for edge, k, cg, cp in halves:
+            r = rows(edge)
+            fl += 2.0 * r * c2 * k
+            by += 4.0 * (r * c2 + r * k + c2 * k)
+    elif kcls == K_GEMM_DW:
+        for edge, k, cg, cp in halves:
+            r = rows(edge)
+            fl += 2.0 * r * c2 * (k + 1)
+            by += 4.0 * (r * c2 + r * k + c2 * (k + 1))
+    elif kcls in (K_AGG_FWD, K_AGG_BWD):
+        items = [(e, k, cg, cp) for e, k, cg, cp in halves] + [(False, k_last, c2, c2)]
+        for edge, k, cg, cp in items:
+            r, ro = rows(edge), rows(not edge)
+            s_bytes = 8.0 * (r + r) + 16.0 * (nnz_g(edge) + counts["nnz_p"])
+            by += 4.0 * (r * k + r * cg + ro * cp) + s_bytes
+            fl += 2.0 * (nnz_g(edge) * jt * cg + 2 * counts["nnz_p"] * cp)
+    elif kcls == K_BN_FWD:
+        for edge, k, cg, cp in halves:
+            by += 4.0 * 2 * rows(edge) * c2
+    elif kcls == K_BN_BWD:
+        for edge, k, cg, cp in halves:
+            by += 4.0 * 5 * rows(edge) * c2
+    return fl, by
+
+
+def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, steps, jt=3):
+    """bench.py 'roofline' object for a kernel class measured over `steps` steps."""
+    fl, by = class_work(kcls, counts, order, f_in, d, n_layers, jt)
+    sec = ms_total / 1e3
+    if kcls in (K_GEMM_FWD, K_GEMM_DA, K_GEMM_DW):
+        achieved = fl * steps / sec / 1e12
+        peak, unit, bound = PEAK_FP32_MFMA_TFS, "TFLOP/s", "mfma"
+    else:
+        achieved = by * steps / sec / 1e9
+        peak, unit, bound = PEAK_HBM_GBS, "GB/s", "hbm"
+    per_launch = launches / max(steps, 1)
+    return {
+        "kernel": NAMES[kcls],
+        "bound": bound,
+        "achieved": round(achieved, 3),
+        "peak": peak,
+        "unit": unit,
+        "frac": round(achieved / peak, 4),
+        "traffic": None,
+        "launches_per_step": per_launch,
+        "avg_launch_us": round(ms_total * 1e3 / max(launches, 1), 3),
+        "algorithmic_per_step": {"flops": fl, "bytes": by},
+    }
+
+
+def to_device_counts(batch):
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = batch
+    with torch.no_grad():
+        return batch_counts(W, WL, Pm, Pd, Nb, Eb)

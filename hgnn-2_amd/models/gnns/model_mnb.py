@@ -1,0 +1,106 @@
+"""Drop-in for models/gnns/model_mnb.py of the reference.
+
+GNN_simple (reference lines 19-66) and GNN_lg (69-129) keep the reference's
+constructor signatures, attributes (.dual, .J, .n_features, .n_layers,
+.n_outputs, .order), submodule names (layer0, layer1.., layerlast) and
+parameter shapes, so `scripts/main_gnn_qm9.py` / `scripts/train_mnb.py`
+(which read model.dual and model.J, scripts/train_mnb.py:29-30) and saved
+state_dicts work unchanged.
+
+forward() runs the whole network -- every layer, BN and the readout -- as one
+enqueue of gfx950 kernels (hgnn_amd.net -> hgnn_net_forward) and backward as
+another (hgnn_net_backward).  Running BN statistics are updated in place in
+training mode exactly as the reference rebinds them.
+"""
+
+import torch
+import torch.nn as nn
+
+from hgnn_amd.net import NetSpec, run_net
+from models.layers import layers_mnb
+
+
+def _lg_params(layer):
+    return [layer.cv1.weight, layer.cv1.bias, layer.cv2.weight, layer.cv2.bias, layer.bn1.weight, layer.bn1.bias,
+            layer.cv3.weight, layer.cv3.bias, layer.cv4.weight, layer.cv4.bias, layer.bn2.weight, layer.bn2.bias]
+
+
+def _simple_params(layer):
+    return [layer.cv1.weight, layer.cv1.bias, layer.cv2.weight, layer.cv2.bias, layer.bn1.weight, layer.bn1.bias]
+
+
+class GNN_simple(nn.Module):
+    """Power GNN (Community Detection with Hierarchical GNN); reference lines 19-66."""
+
+    def __init__(self, task, n_features, n_layers, dim_input, dim_output=1, J=1, gru=False):
+        super(GNN_simple, self).__init__()
+        self.dual = False
+        self.J = J
+        self.gru = False
+        self.n_features = n_features
+        self.n_layers = n_layers
+        self.n_outputs = dim_output
+        self.featuremap_in = [dim_input, n_features]
+        self.featuremap_mi = [2 * n_features, n_features]
+        self.featuremap_end = [2 * n_features, dim_output]
+        self.layer0 = layers_mnb.layer_simple(self.featuremap_in, J + 2, gru)
+        for i in range(n_layers - 2):
+            module = layers_mnb.layer_simple(self.featuremap_mi, J + 2, gru)
+            self.add_module('layer{}'.format(i + 1), module)
+        self.layerlast = layers_mnb.layer_last(self.featuremap_end, J + 2)
+
+    def _layers(self):
+        return [self.layer0] + [self._modules['layer{}'.format(i + 1)] for i in range(self.n_layers - 2)]
+
+    def forward(self, state, N_batch, mask):
+        X, W = state
+        params, running = [], []
+        for layer in self._layers():
+            params += _simple_params(layer)
+            running += list(layer.bn1.running_on(X.device))
+        params += [self.layerlast.fc.weight, self.layerlast.fc.bias]
+        spec = NetSpec(kind=0, order=0, d=self.n_features, n_layers=self.n_layers, dim_out=self.n_outputs,
+                       params=params, running=running, training=self.training)
+        return run_net(spec, X, W, N_batch, mask)
+
+
+class GNN_lg(nn.Module):
+    """GNN on the line graph with non-backtracking operator; reference lines 69-129."""
+
+    def __init__(self, task, n_features, n_layers, dim_input, dim_output=1, J=1, order=1):
+        super(GNN_lg, self).__init__()
+        self.dual = True
+        self.J = J
+        self.n_features = n_features
+        self.n_layers = n_layers
+        self.n_outputs = dim_output
+        self.order = order
+        self.featuremap_in = [dim_input, 1, n_features]
+        self.featuremap_mi = [2 * n_features, 2 * n_features, n_features]
+        self.featuremap_end = [2 * n_features, dim_output]
+        if order == 1:
+            cls = layers_mnb.layer_with_lg_1
+        elif order == 2:
+            cls = layers_mnb.layer_with_lg_2
+        else:
+            cls = layers_mnb.layer_with_lg_3
+        self.layer0 = cls(self.featuremap_in, J + 2)
+        for i in range(n_layers - 2):
+            module = cls(self.featuremap_mi, J + 2)
+            self.add_module('layer{}'.format(i + 1), module)
+        self.layerlast = layers_mnb.layer_last_lg(self.featuremap_end, J + 2)
+
+    def _layers(self):
+        return [self.layer0] + [self._modules['layer{}'.format(i + 1)] for i in range(self.n_layers - 2)]
+
+    def forward(self, state, N_batch, mask, E_batch, mask_lg):
+        X, XL, W, WL, Pm, Pd = state
+        params, running = [], []
+        for layer in self._layers():
+            params += _lg_params(layer)
+            running += list(layer.bn1.running_on(X.device)) + list(layer.bn2.running_on(X.device))
+        params += [self.layerlast.fc.weight, self.layerlast.fc.bias]
+        order = self.order if self.order in (1, 2) else 3
+        spec = NetSpec(kind=1, order=order, d=self.n_features, n_layers=self.n_layers, dim_out=self.n_outputs,
+                       params=params, running=running, training=self.training)
+        return run_net(spec, X, W, N_batch, mask, XL, WL, Pm, Pd, E_batch, mask_lg)

@@ -127,6 +127,32 @@ int hgnn_net_backward(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
                       const float* d_dout, float* const* grads,
                       float* d_dX, float* d_dW, void* stream);
 
+/* Kernel classes for the optional launch timer (bench.py measures the
+ * dominant kernel with HIP events on the launching stream, inside its timed
+ * region).  A timer records a start/stop event pair around every launch of a
+ * class in `class_mask` (bit k = class k). */
+#define HGNN_K_STRUCT 0    /* plan, dense->list extraction, pack/unpack */
+#define HGNN_K_AGG_FWD 1   /* aggregation gather (graph_oper + P_multi)  */
+#define HGNN_K_GEMM_FWD 2  /* fused Conv1d pair GEMM + bias/ReLU/BN partials */
+#define HGNN_K_BN_FWD 3    /* BN finalize + apply                         */
+#define HGNN_K_READOUT 4   /* readout forward/backward                    */
+#define HGNN_K_BN_BWD 5
+#define HGNN_K_GEMM_DW 6
+#define HGNN_K_GEMM_DA 7
+#define HGNN_K_AGG_BWD 8
+void* hgnn_timer_create(int max_launches, unsigned class_mask);
+void hgnn_timer_reset(void* timer);
+/* Waits for the recorded events; sums the durations of class `kernel_class`. */
+int hgnn_timer_elapsed(void* timer, int kernel_class, double* total_ms, int* launches);
+void hgnn_timer_destroy(void* timer);
+int hgnn_net_forward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
+                           const float* const* params, float* const* bn_running,
+                           void* workspace, float* d_out, void* stream, void* timer);
+int hgnn_net_backward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
+                            const float* const* params, void* workspace,
+                            const float* d_dout, float* const* grads,
+                            float* d_dX, float* d_dW, void* stream, void* timer);
+
 /* ------------------------------------------------------------------------
  * Layer-level drop-ins on dense padded tensors.
  * ---------------------------------------------------------------------- */
@@ -159,11 +185,24 @@ int hgnn_p_multi_backward(const float* d_P, long sb, long sn, long sm,
 int hgnn_bn_forward(const float* d_X, const int64_t* d_nb, const float* d_mask,
                     const float* d_w, const float* d_b, float* d_mean, float* d_std,
                     float* d_out, int bs, int c, int n, int training, void* stream);
-/* dX (bs, C, N) overwritten; dw, db (scalars) overwritten. */
+/* dX (bs, C, N) overwritten; dw, db (scalars) overwritten; d_scratch: 2 C floats. */
 int hgnn_bn_backward(const float* d_X, const int64_t* d_nb, const float* d_mask,
                      const float* d_w, const float* d_mean, const float* d_std,
                      const float* d_dout, float* d_dX, float* d_dw, float* d_db,
-                     int bs, int c, int n, int training, void* stream);
+                     float* d_scratch, int bs, int c, int n, int training, void* stream);
+
+/* 1x1 Conv1d (torch.nn.Conv1d(cin, cout, 1), used by every layer_* module,
+ * layers_mnb.py:36-37, 81, 172-177, 239-244, 305-310, 371) on the channel-major
+ * layout: y (bs, cout, n) = W (cout, cin) . x (bs, cin, n) + b, then ReLU if relu.
+ * Workspace: hgnn_conv1x1_workspace_bytes(). */
+size_t hgnn_conv1x1_workspace_bytes(int bs, int cin, int cout, int n);
+int hgnn_conv1x1_forward(const float* d_x, const float* d_w, const float* d_b, float* d_y,
+                         int bs, int cin, int cout, int n, int relu, void* workspace, void* stream);
+/* d_dy: gradient wrt the pre-ReLU output.  dW (cout, cin), db (cout) overwritten;
+ * dx (bs, cin, n) overwritten when non-NULL. */
+int hgnn_conv1x1_backward(const float* d_x, const float* d_w, const float* d_dy, float* d_dx,
+                          float* d_dw, float* d_db, int bs, int cin, int cout, int n,
+                          void* workspace, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,200 @@
+"""GPU parity of the network executor (GNN_lg / GNN_simple) against the reference.
+
+Checks against (a) the golden fixtures recorded from /root/reference and (b)
+the oracle (oracle/ref_mnb.py, fp64) at larger batches, plus size-independent
+properties at the benchmark size.  Tolerances (SURVEY.md §8 c):
+  outputs   |d| <= 1e-5 * max(1, max|ref|)  and  |gpu - ref64| <= 2 |ref32 - ref64| + 1e-6
+  gradients |d| <= 1e-4 * max_global|g| + 1e-5 |g|   (global floor: cv2/cv4 bias grads are 0)
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import fixture_util as fu
+from oracle import ref_mnb as R
+
+pytestmark = pytest.mark.gpu
+
+LG_CASES = ["lg_d16_o1", "lg_d16_o2", "lg_d16_o3", "lg_d8_o2_L2", "lg_d16_o2_L3", "lg_d64_o2"]
+
+
+def _batch(graphs, J=1):
+    from functions.batching import prepare_batch
+    from functions.operators import graph_operators
+    data = [[X, A, t, *graph_operators([X, A], J, True)] for X, A, t in graphs]
+    return list(prepare_batch(data, 0, J))
+
+
+def _cuda(b):
+    return [t.cuda() for t in b]
+
+
+def _check_grads(named_grads, ref, prefix="grad."):
+    gmax = max(np.abs(ref[k]).max() for k in ref.files if k.startswith(prefix))
+    n = 0
+    for k in ref.files:
+        if not k.startswith(prefix):
+            continue
+        g = named_grads[k[len(prefix):]]
+        assert g is not None, k
+        g = g.detach().cpu().numpy()
+        err = np.abs(g - ref[k])
+        bound = 1e-4 * gmax + 1e-5 * np.abs(ref[k])
+        assert np.all(err <= bound), (k, float(err.max()), float(gmax))
+        n += 1
+    assert n > 0
+
+
+@pytest.mark.parametrize("name", LG_CASES)
+def test_gnn_lg_matches_reference_fixture(golden, name):
+    from models.gnns.model_mnb import GNN_lg
+    z = golden(name)
+    d, L, order, bs, wseed = [int(v) for v in z["cfg"]]
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _cuda(_batch(fu.unpack_graphs(z)))
+    model = GNN_lg(0, d, L, 5, 1, 1, order).cuda()
+    fu.det_init(model, wseed)
+    model.train()
+    X.requires_grad_(True)
+    out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+    loss = torch.nn.MSELoss()(out, T)
+    loss.backward()
+    torch.cuda.synchronize()
+    o = out.detach().cpu().numpy()
+    ref, ref64 = z["out"], z["out64"]
+    assert np.max(np.abs(o - ref)) <= 1e-5 * max(1.0, np.abs(ref).max())
+    assert np.max(np.abs(o - ref64)) <= 2 * np.max(np.abs(ref - ref64)) + 1e-6
+    assert abs(loss.item() - float(z["loss"])) <= 1e-5 * max(1.0, abs(float(z["loss"])))
+    _check_grads({k: p.grad for k, p in model.named_parameters()}, z)
+    dx = X.grad.cpu().numpy()
+    assert np.max(np.abs(dx - z["dX"])) <= 1e-4 * max(1.0, np.abs(z["dX"]).max()) + 1e-6
+    for l in range(L - 1):
+        layer = model.layer0 if l == 0 else getattr(model, f"layer{l}")
+        for nm in ("bn1", "bn2"):
+            bn = getattr(layer, nm)
+            np.testing.assert_allclose(bn.running_mean.cpu().numpy(), z[f"rmean.layer{l}.{nm}"], rtol=1e-5, atol=1e-5)
+            np.testing.assert_allclose(bn.running_std.cpu().numpy(), z[f"rstd.layer{l}.{nm}"], rtol=1e-5, atol=1e-5)
+    model.eval()
+    with torch.no_grad():
+        oe = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg).cpu().numpy()
+    assert np.max(np.abs(oe - z["out_eval"])) <= 1e-5 * max(1.0, np.abs(z["out_eval"]).max())
+
+
+def test_gnn_simple_matches_reference_fixture(golden):
+    from models.gnns.model_mnb import GNN_simple
+    z = golden("gnn_simple")
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _cuda(_batch(fu.unpack_graphs(z)))
+    model = GNN_simple(0, 2, 20, 5, 1, 1).cuda()
+    fu.det_init(model, 201)
+    X.requires_grad_(True)
+    out = model([X, W], Nb, mask)
+    loss = torch.nn.MSELoss()(out, T)
+    loss.backward()
+    o = out.detach().cpu().numpy()
+    assert np.max(np.abs(o - z["out32"])) <= 1e-5 * max(1.0, np.abs(z["out32"]).max())
+    assert np.max(np.abs(o - z["out64"])) <= 2 * np.max(np.abs(z["out32"] - z["out64"])) + 1e-6
+    _check_grads({k: p.grad for k, p in model.named_parameters()}, z, prefix="grad32.")
+    assert np.max(np.abs(X.grad.cpu().numpy() - z["dX32"])) <= 1e-4 * max(1.0, np.abs(z["dX32"]).max()) + 1e-6
+    model.eval()
+    with torch.no_grad():
+        oe = model([X, W], Nb, mask).cpu().numpy()
+    assert np.max(np.abs(oe - z["out_eval"])) <= 1e-5 * max(1.0, np.abs(z["out_eval"]).max())
+
+
+def _oracle_lg(model, b, L, order, dtype=torch.float64):
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = [t.cpu() for t in b]
+    p = {k: v.detach().cpu().to(dtype).requires_grad_(True) for k, v in model.state_dict().items()}
+    st = R.bn_states(L, 2 * model.n_features, dtype=dtype)
+    Xo = X.to(dtype).requires_grad_(True)
+    out = R.gnn_lg(p, [Xo, XL.to(dtype), W.to(dtype), WL.to(dtype), Pm.to(dtype), Pd.to(dtype)], Nb,
+                   mask.to(dtype), Eb, mask_lg.to(dtype), L, order, st, True)
+    loss = torch.nn.MSELoss()(out, T.to(dtype))
+    loss.backward()
+    return out.detach(), loss.item(), {k: v.grad for k, v in p.items()}, Xo.grad
+
+
+@pytest.mark.parametrize("order", [1, 2, 3])
+def test_gnn_lg_vs_oracle_fp64_bs128(order):
+    """bs=128, d=64, L=5 (config-2 model at a quarter batch) against the fp64 oracle."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_lg
+    graphs = dg.qm9_shape_dataset(128, seed=1)
+    b = _batch(graphs)
+    model = GNN_lg(0, 64, 5, 5, 1, 1, order).cuda()
+    fu.det_init(model, 77 + order)
+    ref_out, ref_loss, ref_g, ref_dx = _oracle_lg(model, b, 5, order)
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _cuda(b)
+    X.requires_grad_(True)
+    out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+    loss = torch.nn.MSELoss()(out, T)
+    loss.backward()
+    o = out.detach().cpu().double()
+    assert torch.max(torch.abs(o - ref_out)).item() <= 2e-5 * max(1.0, ref_out.abs().max().item())
+    gmax = max(g.abs().max().item() for g in ref_g.values())
+    for k, p in model.named_parameters():
+        err = (p.grad.cpu().double() - ref_g[k]).abs()
+        assert torch.all(err <= 1e-4 * gmax + 1e-5 * ref_g[k].abs()), (k, err.max().item(), gmax)
+    err = (X.grad.cpu().double() - ref_dx).abs().max().item()
+    assert err <= 1e-4 * max(1.0, ref_dx.abs().max().item())
+
+
+def test_config2_batch_permutation_equivariance():
+    """bs=512 QM9-shape (the benchmark batch): permuting the graphs permutes the outputs."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_lg
+    graphs = dg.qm9_shape_dataset(512, seed=0)
+    perm = torch.randperm(512, generator=torch.Generator().manual_seed(3)).tolist()
+    model = GNN_lg(0, 64, 5, 5, 1, 1, 2).cuda()
+    fu.det_init(model, 9)
+    outs = []
+    for gs in (graphs, [graphs[i] for i in perm]):
+        X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _cuda(_batch(gs))
+        with torch.no_grad():
+            outs.append(model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg).cpu())
+    a, b = outs
+    assert torch.allclose(a[perm], b, rtol=1e-5, atol=1e-5 * max(1.0, a.abs().max().item()))
+    # determinism: a second identical call is bitwise identical (no atomics in the path)
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _cuda(_batch(graphs))
+    with torch.no_grad():
+        a2 = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg).cpu()
+    assert torch.equal(a, a2)
+
+
+def test_invalid_padding_and_mask_raise():
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_lg
+    graphs = dg.qm9_shape_dataset(8, seed=4)
+    model = GNN_lg(0, 8, 3, 5, 1, 1, 2).cuda()
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _cuda(_batch(graphs))
+    i = int(torch.argmin(Nb))
+    n = int(Nb[i])
+    Wbad = W.clone()
+    Wbad[i, n, 0, 2] = 1.0  # an entry in a padded row
+    with pytest.raises(RuntimeError, match="padding"):
+        model([X, XL, Wbad, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+    mbad = mask.clone()
+    mbad[i, n, 0] = 1.0
+    with pytest.raises(RuntimeError, match="mask"):
+        model([X, XL, W, WL, Pm, Pd], Nb, mbad, Eb, mask_lg)
+    # a valid call still works afterwards
+    model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+
+
+def test_empty_line_graph_and_single_node_graphs():
+    """Graphs with no bonds (M = 0) and tiny graphs mixed into one batch."""
+    from models.gnns.model_mnb import GNN_lg
+    g = [(torch.eye(5)[[0, 1, 2]], torch.zeros(3, 3), torch.zeros(13)),
+         (torch.eye(5)[[3, 4]], torch.tensor([[0.0, 2.0], [2.0, 0.0]]), torch.ones(13))]
+    import hgnn_amd.datagen as dg
+    g += dg.qm9_shape_dataset(6, seed=8)
+    b = _batch(g)
+    model = GNN_lg(0, 16, 4, 5, 1, 1, 2).cuda()
+    fu.det_init(model, 5)
+    ref_out, _, ref_g, _ = _oracle_lg(model, b, 4, 2)
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _cuda(b)
+    out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+    torch.nn.MSELoss()(out, T).backward()
+    assert torch.max(torch.abs(out.detach().cpu().double() - ref_out)).item() <= 2e-5 * max(1.0, ref_out.abs().max().item())
+    gmax = max(v.abs().max().item() for v in ref_g.values())
+    for k, p in model.named_parameters():
+        assert torch.all((p.grad.cpu().double() - ref_g[k]).abs() <= 1e-4 * gmax + 1e-5 * ref_g[k].abs()), k

@@ -1,0 +1,181 @@
+"""Host-side drop-ins (CPU): operator construction, batching, index lists, ABI library surface."""
+
+import ctypes
+import os
+import re
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import fixture_util as fu
+from oracle import ref_mnb as R
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_graph_operators_bit_exact_vs_reference(golden):
+    from functions.operators import graph_operators
+    z = golden("operators")
+    graphs = fu.unpack_graphs(z)
+    for k, ((X, A, _), J) in enumerate(zip(graphs, z["J"])):
+        W, WL, Pm, Pd = graph_operators([X, A], int(J), True)
+        Wonly = graph_operators([X, A], int(J), False)
+        assert torch.equal(W, Wonly)
+        for nm, v in (("W", W), ("WL", WL), ("Pm", Pm), ("Pd", Pd)):
+            ref = z[f"{nm}_{k}"]
+            assert v.shape == ref.shape, (k, nm)
+            assert v.dtype == torch.float32
+            assert np.array_equal(v.numpy(), ref), (k, nm)
+
+
+def test_graph_operators_random_vs_oracle():
+    """Seeded random graphs (weights, self loops, isolated nodes) against the loop restatement."""
+    from functions.operators import graph_operators
+    g = torch.Generator().manual_seed(7)
+    for trial in range(40):
+        n = int(torch.randint(2, 14, (1,), generator=g))
+        A = (torch.rand(n, n, generator=g) < 0.35).float()
+        A = torch.triu(A, 1)
+        wts = torch.tensor([1.0, 1.5, 2.0, 3.0])[torch.randint(0, 4, (n, n), generator=g)]
+        A = A * wts
+        A = A + A.t()
+        if trial % 5 == 0:
+            A[0, 0] = 1.0
+        X = torch.zeros(n, 5)
+        J = 1 + trial % 2
+        got = graph_operators([X, A], J, True)
+        ref = R.graph_operators([X, A], J, True)
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b)
+
+
+def test_graph_operators_faster_than_loops():
+    from functions.operators import graph_operators
+    import hgnn_amd.datagen as dg
+    X, A, _ = dg.sbm_dataset(1, n=50, seed=3)[0]
+    t0 = time.perf_counter()
+    graph_operators([X, A], 1, True)
+    assert time.perf_counter() - t0 < 0.5
+
+
+def test_prepare_batch_bit_exact_vs_reference(golden):
+    from functions.batching import prepare_batch
+    from functions.operators import graph_operators
+    z = golden("batch")
+    data = []
+    for X, A, t in fu.unpack_graphs(z):
+        W, WL, Pm, Pd = graph_operators([X, A], 1, True)
+        data.append([X, A, t, W, WL, Pm, Pd])
+    out = prepare_batch(data, 0, 1)
+    names = ["X", "W", "T", "XL", "WL", "Pm", "Pd", "mask", "mask_lg", "N_batch", "E_batch"]
+    for nm, v in zip(names, out):
+        assert v.dtype == torch.from_numpy(z[nm]).dtype, nm
+        assert np.array_equal(v.numpy(), z[nm]), nm
+
+
+def test_get_batches_index_lists(golden):
+    from functions.batching import get_batches
+    z = golden("batch")
+    flat = list(z["batches_23_5"])
+    sep = flat.index(-1)
+    idx, lens = flat[:sep], flat[sep + 1:]
+    got = get_batches(23, 5, None, False, False)
+    assert [len(b) for b in got] == lens
+    assert [i for b in got for i in b] == idx
+
+
+def test_normalize_data_semantics():
+    from functions.utils import normalize_data, RunningAverage
+    x = torch.tensor([1.0, 2.0, 3.0])
+    assert torch.equal(normalize_data(x, 1.0, 1e-6), x - 1.0)  # std < 1e-5: mean only (Q14)
+    assert torch.allclose(normalize_data(x, 2.0, 2.0), (x - 2.0) / 2.0)
+    r = RunningAverage()
+    r.update(4.0)
+    r.update(2.0)
+    assert r.val == pytest.approx(0.9 * 2.0 + 0.1 * 4.0)
+
+
+# ----------------------------------------------------------------------------- C ABI surface
+def _header_functions():
+    src = open(os.path.join(REPO, "include", "hgnn_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hgnn_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from hgnn_amd import _lib
+    lib = _lib.lib()
+    names = _header_functions()
+    assert len(names) >= 10
+    for nm in names:
+        assert hasattr(lib, nm), nm
+    assert lib.hgnn_abi_version() == 1
+    assert set(names) <= set(_lib.SIGNATURES), set(names) - set(_lib.SIGNATURES)
+
+
+def _cfg(**kw):
+    from hgnn_amd import _lib
+    c = _lib.NetConfig()
+    base = dict(kind=1, order=2, bs=512, nmax=29, emax=70, f_in=5, d=64, n_layers=5, j_tot=3, dim_out=1, training=1)
+    base.update(kw)
+    for k, v in base.items():
+        setattr(c, k, v)
+    return c
+
+
+def test_workspace_and_counts_host_only():
+    from hgnn_amd import _lib
+    lib = _lib.lib()
+    c = _cfg()
+    assert lib.hgnn_net_param_count(ctypes.byref(c)) == 12 * 4 + 2
+    assert lib.hgnn_net_bn_count(ctypes.byref(c)) == 8
+    ws = lib.hgnn_net_workspace_bytes(ctypes.byref(c))
+    assert 100e6 < ws < 4e9
+    s = _cfg(kind=0, emax=0, n_layers=20, d=2)
+    assert lib.hgnn_net_param_count(ctypes.byref(s)) == 6 * 19 + 2
+    assert lib.hgnn_net_workspace_bytes(ctypes.byref(s)) > 0
+    for bad in (dict(j_tot=9), dict(n_layers=1), dict(order=4), dict(bs=0), dict(d=300)):
+        assert lib.hgnn_net_workspace_bytes(ctypes.byref(_cfg(**bad))) == 0
+        assert lib.hgnn_net_param_count(ctypes.byref(_cfg(**bad))) == -1
+
+
+def test_expected_k_matches_reference_shapes():
+    from hgnn_amd.net import expected_k
+    from models.gnns.model_mnb import GNN_lg, GNN_simple
+    for order in (1, 2, 3):
+        m = GNN_lg(0, 16, 4, 5, 1, 1, order)
+        ks, kl = expected_k(1, order, 5, 16, 4, 3)
+        for l, (kn, ke) in enumerate(ks):
+            layer = m._layers()[l]
+            assert layer.cv1.weight.shape == (16, kn, 1)
+            assert layer.cv3.weight.shape == (16, ke, 1)
+        assert m.layerlast.fc.weight.shape == (1, kl, 1)
+    m = GNN_simple(0, 2, 5, 5, 1, 1)
+    ks, kl = expected_k(0, 0, 5, 2, 5, 3)
+    assert m.layer0.cv1.weight.shape == (2, ks[0][0], 1)
+    assert m.layerlast.fc.weight.shape == (1, kl, 1)
+
+
+def test_state_dict_matches_reference_layout(golden):
+    """Same parameter names and shapes as the reference (fixture grads are keyed by them)."""
+    from models.gnns.model_mnb import GNN_lg
+    z = golden("lg_d64_o2")
+    m = GNN_lg(0, 64, 5, 5, 1, 1, 2)
+    names = {k[5:]: z[k].shape for k in z.files if k.startswith("grad.")}
+    sd = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    assert sd == {k: tuple(v) for k, v in names.items()}
+
+
+def test_gpu_ops_refuse_cpu_tensors():
+    from models.gnns.model_mnb import GNN_lg
+    from functions.operators import graph_operators
+    from functions.batching import prepare_batch
+    import hgnn_amd.datagen as dg
+    graphs = dg.qm9_shape_dataset(4, seed=5)
+    data = [[X, A, t, *graph_operators([X, A], 1, True)] for X, A, t in graphs]
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = prepare_batch(data, 0, 1)
+    m = GNN_lg(0, 8, 3, 5, 1, 1, 2)
+    with pytest.raises(RuntimeError, match="GPU"):
+        m([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)

@@ -1,0 +1,109 @@
+"""Pin the oracle (oracle/ref_mnb.py) to the reference's golden fixtures (CPU only)."""
+
+import numpy as np
+import pytest
+import torch
+
+import fixture_util as fu
+from oracle import ref_mnb as R
+
+
+def _op_graphs(z):
+    return fu.unpack_graphs(z), z["J"]
+
+
+def test_oracle_graph_operators_bit_exact(golden):
+    z = golden("operators")
+    graphs, js = _op_graphs(z)
+    for k, ((X, A, _), J) in enumerate(zip(graphs, js)):
+        if A.shape[0] > 30:  # the O(M^2) loop restatement is for small graphs only
+            continue
+        W, WL, Pm, Pd = R.graph_operators([X, A], int(J), True)
+        for nm, v in (("W", W), ("WL", WL), ("Pm", Pm), ("Pd", Pd)):
+            ref = z[f"{nm}_{k}"]
+            assert v.shape == ref.shape, (k, nm)
+            assert np.array_equal(v.numpy(), ref), (k, nm)
+
+
+def test_oracle_prepare_batch_bit_exact(golden):
+    z = golden("batch")
+    graphs = fu.unpack_graphs(z)
+    data = []
+    for X, A, t in graphs:
+        W, WL, Pm, Pd = R.graph_operators([X, A], 1, True)
+        data.append([X, A, t, W, WL, Pm, Pd])
+    out = R.prepare_batch(data, 0, 1)
+    names = ["X", "W", "T", "XL", "WL", "Pm", "Pd", "mask", "mask_lg", "N_batch", "E_batch"]
+    for nm, v in zip(names, out):
+        assert np.array_equal(v.numpy(), z[nm]), nm
+
+
+def lg_inputs(z, J=1, dtype=torch.float32, builder=None):
+    from functions.operators import graph_operators as prod_ops
+    from functions.batching import prepare_batch as prod_batch
+    graphs = fu.unpack_graphs(z)
+    build = builder or prod_ops
+    data = []
+    for X, A, t in graphs:
+        W, WL, Pm, Pd = build([X, A], J, True)
+        data.append([X, A, t, W, WL, Pm, Pd])
+    b = list(prod_batch(data, 0, J))
+    for i in range(9):
+        b[i] = b[i].to(dtype)
+    return b
+
+
+def oracle_params(model_cls_args, seed, dtype=torch.float32, kind="lg"):
+    from models.gnns.model_mnb import GNN_lg, GNN_simple
+    m = GNN_lg(*model_cls_args) if kind == "lg" else GNN_simple(*model_cls_args)
+    fu.det_init(m, seed)
+    return {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in m.state_dict().items()}
+
+
+LG_CASES = ["lg_d16_o1", "lg_d16_o2", "lg_d16_o3", "lg_d8_o2_L2", "lg_d16_o2_L3", "lg_d64_o2"]
+
+
+@pytest.mark.parametrize("name", LG_CASES)
+def test_oracle_gnn_lg_matches_reference(golden, name):
+    z = golden(name)
+    d, L, order, bs, wseed = [int(v) for v in z["cfg"]]
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = lg_inputs(z)
+    p = oracle_params((0, d, L, 5, 1, 1, order), wseed)
+    st = R.bn_states(L, 2 * d)
+    X.requires_grad_(True)
+    W.requires_grad_(True)
+    out = R.gnn_lg(p, [X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg, L, order, st, True)
+    loss = torch.nn.MSELoss()(out, T)
+    loss.backward()
+    ref = z["out"]
+    assert np.max(np.abs(out.detach().numpy() - ref)) <= 1e-5 * max(1.0, np.abs(ref).max())
+    gmax = max(np.abs(z[k]).max() for k in z.files if k.startswith("grad."))
+    for k in z.files:
+        if k.startswith("grad."):
+            g = p[k[5:]].grad.numpy()
+            assert np.all(np.abs(g - z[k]) <= 1e-4 * gmax + 1e-5 * np.abs(z[k])), k
+    dxg = X.grad.numpy()
+    assert np.max(np.abs(dxg - z["dX"])) <= 1e-4 * max(1.0, np.abs(z["dX"]).max())
+    assert np.max(np.abs(W.grad.numpy() - z["dW"])) <= 1e-4 * max(1.0, np.abs(z["dW"]).max())
+    for l in range(L - 1):
+        for nm in ("bn1", "bn2"):
+            s = st[f"layer{l}.{nm}"]
+            np.testing.assert_allclose(s["running_mean"].numpy(), z[f"rmean.layer{l}.{nm}"], rtol=1e-5, atol=1e-5)
+            np.testing.assert_allclose(s["running_std"].numpy(), z[f"rstd.layer{l}.{nm}"], rtol=1e-5, atol=1e-5)
+
+
+def test_oracle_gnn_simple_matches_reference(golden):
+    z = golden("gnn_simple")
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = lg_inputs(z)
+    p = oracle_params((0, 2, 20, 5, 1, 1), 201, kind="simple")
+    st = R.bn_states(20, 4, kind="simple")
+    X.requires_grad_(True)
+    out = R.gnn_simple(p, [X, W], Nb, mask, 20, st, True)
+    loss = torch.nn.MSELoss()(out, T)
+    loss.backward()
+    assert np.max(np.abs(out.detach().numpy() - z["out32"])) <= 1e-5 * max(1.0, np.abs(z["out32"]).max())
+    gmax = max(np.abs(z[k]).max() for k in z.files if k.startswith("grad32."))
+    for k in z.files:
+        if k.startswith("grad32."):
+            g = p[k[7:]].grad.numpy()
+            assert np.all(np.abs(g - z[k]) <= 1e-4 * gmax + 1e-5 * np.abs(z[k])), k
