@@ -220,14 +220,16 @@ __global__ void __launch_bounds__(256) k_readout_fwd(const float* __restrict__ A
     for (int o = 0; o < dim_out; ++o) {
         double part = 0.0;
         for (int kk = threadIdx.x; kk < k; kk += blockDim.x) {
-            float cs = 0.f;
+            double cs = 0.0;
             if (o == 0) {
-                for (int r = r0; r < r1; ++r) cs += A[(long long)r * k + kk];
-                colsum[(long long)b * k + kk] = cs;
+                // fp64 column sum: the reference sums per-position dot products with
+                // torch.sum (pairwise), a plain fp32 running sum would be less accurate
+                for (int r = r0; r < r1; ++r) cs += (double)A[(long long)r * k + kk];
+                colsum[(long long)b * k + kk] = (float)cs;
             } else {
-                cs = colsum[(long long)b * k + kk];
+                cs = (double)colsum[(long long)b * k + kk];
             }
-            part += (double)cs * (double)fcw[(long long)o * k + kk];
+            part += cs * (double)fcw[(long long)o * k + kk];
         }
         const double t = block_sum_d(part, red);
         if (threadIdx.x == 0) out[b * dim_out + o] = (float)(t + (double)nmax * (double)fcb[o]);
@@ -266,16 +268,41 @@ int launch_readout_bwd_da(const float* dout, const int* node_off, int bs, int ca
 }
 
 // dfcw[o, k] = sum_b dout[b, o] colsum[b, k];  dfcb[o] = Nmax sum_b dout[b, o]
+// Stage 1: block (k-chunk of 64, graph chunk) -> fp64 partials; stage 2 sums the chunks in order.
+constexpr int RB_CHUNKS = 16;
+
+__global__ void __launch_bounds__(256) k_readout_bwd_part(const float* __restrict__ dout,
+                                                          const float* __restrict__ colsum, int bs,
+                                                          int dim_out, int k, double* __restrict__ part) {
+    __shared__ double red[4][64];
+    const int kk = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int g = threadIdx.x >> 6;
+    const int per = ceil_div(bs, RB_CHUNKS);
+    const int b0 = blockIdx.y * per, b1 = min(bs, b0 + per);
+    for (int o = 0; o < dim_out; ++o) {
+        double s = 0.0;
+        if (kk < k)
+            for (int b = b0 + g; b < b1; b += 4)
+                s += (double)dout[b * dim_out + o] * (double)colsum[(long long)b * k + kk];
+        red[g][threadIdx.x & 63] = s;
+        __syncthreads();
+        if (g == 0 && kk < k) {
+            const int t = threadIdx.x & 63;
+            part[((long long)blockIdx.y * dim_out + o) * k + kk] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void __launch_bounds__(256) k_readout_bwd_params(const float* __restrict__ dout,
-                                                            const float* __restrict__ colsum, int bs,
+                                                            const double* __restrict__ part, int bs,
                                                             int nmax, int dim_out, int k,
                                                             float* __restrict__ dfcw,
                                                             float* __restrict__ dfcb) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx < dim_out * k) {
-        const int o = idx / k, kk = idx % k;
         double s = 0.0;
-        for (int b = 0; b < bs; ++b) s += (double)dout[b * dim_out + o] * (double)colsum[(long long)b * k + kk];
+        for (int c = 0; c < RB_CHUNKS; ++c) s += part[(long long)c * dim_out * k + idx];
         dfcw[idx] = (float)s;
     }
     if (idx < dim_out) {
@@ -285,10 +312,16 @@ __global__ void __launch_bounds__(256) k_readout_bwd_params(const float* __restr
     }
 }
 
+size_t readout_bwd_scratch_bytes(int dim_out, int k) { return sizeof(double) * RB_CHUNKS * dim_out * (size_t)k; }
+
 int launch_readout_bwd_params(const float* dout, const float* colsum, int bs, int nmax, int dim_out, int k,
-                              float* dfcw, float* dfcb, hipStream_t s) {
+                              float* dfcw, float* dfcb, void* scratch, hipStream_t s) {
+    double* part = static_cast<double*>(scratch);
+    hipLaunchKernelGGL(k_readout_bwd_part, dim3(ceil_div(k, 64), RB_CHUNKS), dim3(256), 0, s, dout, colsum, bs,
+                       dim_out, k, part);
+    HGNN_LAUNCH_CHECK();
     const int n = dim_out * k > dim_out ? dim_out * k : dim_out;
-    hipLaunchKernelGGL(k_readout_bwd_params, dim3(ceil_div(n, 256)), dim3(256), 0, s, dout, colsum, bs, nmax,
+    hipLaunchKernelGGL(k_readout_bwd_params, dim3(ceil_div(n, 256)), dim3(256), 0, s, dout, part, bs, nmax,
                        dim_out, k, dfcw, dfcb);
     HGNN_LAUNCH_CHECK();
     return 0;

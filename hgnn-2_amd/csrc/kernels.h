@@ -183,6 +183,27 @@ struct BnBwdArgs {
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s);
 int bn_bwd_tiles(int cap_rows);
 
+// ---------------------------------------------------------------- dense dW of the operators
+struct DwDenseArgs {
+    const float* dA;       // node-half aggregate gradient [rows][lda]; G block = cols [0, jt*f)
+    int lda;
+    int f, jt;
+    const float* xp;       // packed layer input [rows][f]  (unless xdense)
+    const float* xdense;   // dense (bs, f, nmax) layer input (layer 0), or null
+    const float* pmean;    // BN stats of the producer of xp (padded value), or null -> 0
+    const float* pstd;
+    const float* pw;
+    const float* pb;
+    const float* dout;     // readout: dG at padded rows = dout[b] . fcw[:, k] ; null otherwise
+    const float* fcw;
+    int dim_out, kfc;
+    const int* node_off;
+    int bs, nmax;
+    float* dW;             // (bs, nmax, nmax, jt)
+    int accumulate;
+};
+int launch_dw_dense(const DwDenseArgs& a, hipStream_t s);
+
 // ---------------------------------------------------------------- readout
 int launch_readout_fwd(const float* a, int k, const int* node_off, int bs, int nmax,
                        const float* fcw, const float* fcb, int dim_out,
@@ -191,6 +212,7 @@ int launch_readout_bwd_da(const float* dout, const int* node_off, int bs, int ca
                           const int* total_rows, const float* fcw, int dim_out, int k,
                           float* da, hipStream_t s);
 int launch_readout_bwd_params(const float* dout, const float* colsum, int bs, int nmax,
-                              int dim_out, int k, float* dfcw, float* dfcb, hipStream_t s);
+                              int dim_out, int k, float* dfcw, float* dfcb, void* scratch, hipStream_t s);
+size_t readout_bwd_scratch_bytes(int dim_out, int k);
 
 }  // namespace hgnn

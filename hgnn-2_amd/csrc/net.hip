@@ -48,7 +48,7 @@ struct Program {
     size_t node_off = 0, edge_off = 0, totals = 0, err = 0;
     size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
     int entry_stride_w = 4;
-    size_t dy = 0, da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0;
+    size_t dy = 0, da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0;
     size_t bytes = 0;
 };
 
@@ -232,6 +232,7 @@ Program build_program(const hgnn_net_config* c) {
     P.slabs = B.take(max_slab * sizeof(float));
     P.bnb_part = B.take((size_t)bn_bwd_tiles(max_cap) * P.c2 * 4 * sizeof(float));
     P.bnb_sums = B.take((size_t)P.c2 * 4 * sizeof(float));
+    P.rb_scratch = B.take(readout_bwd_scratch_bytes(c->dim_out, P.k_last));
     P.bytes = B.top;
     return P;
 }
@@ -394,8 +395,8 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
     return 0;
 }
 
-int net_backward(const hgnn_net_config* c, const float* const* prm, void* ws, const float* dout,
-                 float* const* grads, float* dX, hipStream_t s, Timer* tm) {
+int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float* const* prm, void* ws,
+                 const float* dout, float* const* grads, float* dX, float* dW, hipStream_t s, Timer* tm) {
     const Program P = build_program(c);
     BatchMeta m = meta_of(P, ws);
     const int* tot_n = m.totals;
@@ -407,14 +408,49 @@ int net_backward(const hgnn_net_config* c, const float* const* prm, void* ws, co
         if (c->kind == 1 && f == 1) return false;  // XL never requires grad (scripts/train_mnb.py:56-66)
         return true;
     };
+    const bool need_dw = c->need_dw != 0;
+    if (need_dw && (!dW || !in || !in->d_X)) return HGNN_ERR_ARG;
+    // dense dW contribution of one graph_oper(W, X_l): G block of dA (node rows) x X_l
+    auto dw_dense = [&](int gin, const float* da, int lda, bool readout, int accumulate) -> int {
+        DwDenseArgs a{};
+        a.dA = da;
+        a.lda = lda;
+        a.f = P.feats[gin].c;
+        a.jt = P.jt;
+        if (gin == 0) {
+            a.xdense = in->d_X;
+        } else {
+            a.xp = at<float>(ws, P.feats[gin].z);
+            for (const Half& hp : P.halves) {
+                if (hp.out != gin) continue;
+                a.pmean = at<float>(ws, hp.mean);
+                a.pstd = at<float>(ws, hp.stdv);
+                a.pw = prm[hp.pbn_w];
+                a.pb = prm[hp.pbn_b];
+            }
+        }
+        if (readout) {
+            a.dout = dout;
+            a.fcw = prm[P.p_fcw];
+            a.dim_out = c->dim_out;
+            a.kfc = P.k_last;
+        }
+        a.node_off = m.node_off;
+        a.bs = c->bs;
+        a.nmax = c->nmax;
+        a.dW = dW;
+        a.accumulate = accumulate;
+        return launch_dw_dense(a, s);
+    };
 
     // readout
     TL(HGNN_K_READOUT, launch_readout_bwd_params(dout, at<float>(ws, P.colsum), c->bs, c->nmax, c->dim_out, P.k_last,
-                                  grads[P.p_fcw], grads[P.p_fcb], s));
-    if (needs_grad(P.last_gin) || needs_grad(P.last_pin)) {
+                                  grads[P.p_fcw], grads[P.p_fcb], at<void>(ws, P.rb_scratch), s));
+    if (needs_grad(P.last_gin) || needs_grad(P.last_pin) || need_dw) {
         float* da = at<float>(ws, P.da);
         TL(HGNN_K_READOUT, launch_readout_bwd_da(dout, m.node_off, c->bs, P.cap_n, tot_n, prm[P.p_fcw], c->dim_out, P.k_last,
                                   da, s));
+        if (need_dw) TL(HGNN_K_DW_DENSE, dw_dense(P.last_gin, da, P.k_last, true, 0));
         const int cg = P.feats[P.last_gin].c;
         if (needs_grad(P.last_gin)) {
             AggBwdArgs ab{};
@@ -494,7 +530,8 @@ int net_backward(const hgnn_net_config* c, const float* const* prm, void* ws, co
         TL(HGNN_K_GEMM_DW, launch_gemm_dw(gw, s));
 
         const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
-        if (!ng && !np) continue;
+        const bool ndw = need_dw && !h.edge;
+        if (!ng && !np && !ndw) continue;
         float* da = at<float>(ws, P.da);
         GemmDaArgs gd{};
         gd.dy = at<float>(ws, P.dy);
@@ -509,6 +546,7 @@ int net_backward(const hgnn_net_config* c, const float* const* prm, void* ws, co
         gd.da = da;
         gd.ldda = h.k;
         TL(HGNN_K_GEMM_DA, launch_gemm_da(gd, s));
+        if (ndw) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, da, h.k, false, 1));
         if (ng) {
             AggBwdArgs ab{};
             ab.total_rows = tot;
@@ -604,13 +642,9 @@ int hgnn_net_forward(const hgnn_net_config* cfg, const hgnn_net_inputs* in, cons
 int hgnn_net_backward(const hgnn_net_config* cfg, const hgnn_net_inputs* in, const float* const* params,
                       void* workspace, const float* d_dout, float* const* grads, float* d_dX, float* d_dW,
                       void* stream) {
-    (void)in;
     if (!valid_config(cfg) || !params || !workspace || !d_dout || !grads) return HGNN_ERR_ARG;
-    if (cfg->need_dw) {
-        (void)d_dW;
-        return HGNN_ERR_UNSUPPORTED;
-    }
-    return net_backward(cfg, params, workspace, d_dout, grads, d_dX, static_cast<hipStream_t>(stream), nullptr);
+    return net_backward(cfg, in, params, workspace, d_dout, grads, d_dX, d_dW, static_cast<hipStream_t>(stream),
+                        nullptr);
 }
 
 void* hgnn_timer_create(int max_launches, unsigned class_mask) {
@@ -667,11 +701,8 @@ int hgnn_net_forward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* in
 int hgnn_net_backward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* in, const float* const* params,
                             void* workspace, const float* d_dout, float* const* grads, float* d_dX, float* d_dW,
                             void* stream, void* timer) {
-    (void)in;
-    (void)d_dW;
     if (!valid_config(cfg) || !params || !workspace || !d_dout || !grads) return HGNN_ERR_ARG;
-    if (cfg->need_dw) return HGNN_ERR_UNSUPPORTED;
-    return net_backward(cfg, params, workspace, d_dout, grads, d_dX, static_cast<hipStream_t>(stream),
+    return net_backward(cfg, in, params, workspace, d_dout, grads, d_dX, d_dW, static_cast<hipStream_t>(stream),
                         static_cast<Timer*>(timer));
 }
 

@@ -219,16 +219,17 @@ class _NetFn(torch.autograd.Function):
         dout = dout.contiguous().to(torch.float32)
         grads = [torch.empty_like(p) for p in ctx.params]
         dX = torch.empty_like(X) if ctx.needs_input_grad[2] else None
+        dW = torch.empty_like(ctx.keep[1]) if ctx.needs_input_grad[3] else None
         cfg.need_dx = 1 if dX is not None else 0
-        cfg.need_dw = 0
+        cfg.need_dw = 1 if dW is not None else 0
         args = (ctypes.byref(cfg), ctypes.byref(ctx.inp), L.ptr_array(ctx.params), ctypes.c_void_p(ctx.ws.data_ptr()),
-                ctypes.c_void_p(dout.data_ptr()), L.ptr_array(grads), L.ptr(dX), None, L.stream_handle(X.device))
+                ctypes.c_void_p(dout.data_ptr()), L.ptr_array(grads), L.ptr(dX), L.ptr(dW), L.stream_handle(X.device))
         if _timer is not None:
             st = L.lib().hgnn_net_backward_timed(*args, ctypes.c_void_p(_timer.handle))
         else:
             st = L.lib().hgnn_net_backward(*args)
         L.check(st, "network backward")
-        return (None, None, dX, None, *grads)
+        return (None, None, dX, dW, *grads)
 
 
 def run_net(spec, X, W, N_batch, mask, XL=None, WL=None, Pm=None, Pd=None, E_batch=None, mask_lg=None):

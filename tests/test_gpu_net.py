@@ -56,10 +56,13 @@ def test_gnn_lg_matches_reference_fixture(golden, name):
     fu.det_init(model, wseed)
     model.train()
     X.requires_grad_(True)
+    W.requires_grad_(True)  # as scripts/train_mnb.py:56-57: the reference materialises W.grad
     out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
     loss = torch.nn.MSELoss()(out, T)
     loss.backward()
     torch.cuda.synchronize()
+    dw = W.grad.cpu().numpy()
+    assert np.max(np.abs(dw - z["dW"])) <= 1e-4 * max(1.0, np.abs(z["dW"]).max()) + 1e-6
     o = out.detach().cpu().numpy()
     ref, ref64 = z["out"], z["out64"]
     assert np.max(np.abs(o - ref)) <= 1e-5 * max(1.0, np.abs(ref).max())
