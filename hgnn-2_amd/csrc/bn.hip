@@ -169,23 +169,49 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
             *a.db = (float)T2;
         }
     }
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (long long)gridDim.x * blockDim.x) {
-        const int ch = (int)(i % a.c);
-        const float sd = a.std[ch];
-        const float yv = a.y[i];
-        const float g = wv * a.dz[i];
-        float d;
-        if (a.training) {
-            const float h = __fdiv_rn(__fsub_rn(yv, a.mean[ch]), sd);
+    (void)n;
+    // one 64-row tile per block; per-channel column sums of dY -> dbpart (the conv bias grads)
+    __shared__ float red[256];
+    const int r0 = blockIdx.x * 64;
+    if (r0 >= total) return;
+    const int r1 = min(total, r0 + 64);
+    const int cw = a.c < 256 ? a.c : 256;
+    const int rgn = 256 / cw;
+    const int tch = threadIdx.x % cw, rg = threadIdx.x / cw;
+    for (int ch0 = 0; ch0 < a.c; ch0 += cw) {
+        const int ch = ch0 + tch;
+        float cs = 0.f;
+        if (rg < rgn && ch < a.c) {
+            const float sd = a.std[ch];
+            const float mu = a.mean[ch];
             const float m1 = a.sums[ch * 4 + 0] * inv_n;
             const float m2 = a.sums[ch * 4 + 1] * inv_n;
-            d = (g - m1 - h * m2) / sd;
-        } else {
-            d = g / sd;
+            for (int r = r0 + rg; r < r1; r += rgn) {
+                const long long i = (long long)r * a.c + ch;
+                const float yv = a.y[i];
+                const float g = wv * a.dz[i];
+                float d;
+                if (a.training) {
+                    const float h = __fdiv_rn(__fsub_rn(yv, mu), sd);
+                    d = (g - m1 - h * m2) / sd;
+                } else {
+                    d = g / sd;
+                }
+                if (ch >= a.relu_from && !(yv > 0.f)) d = 0.f;
+                a.dy[i] = d;
+                cs += d;
+            }
         }
-        if (ch >= a.relu_from && !(yv > 0.f)) d = 0.f;
-        a.dy[i] = d;
+        if (a.dbpart) {
+            red[threadIdx.x] = cs;
+            __syncthreads();
+            if (rg == 0 && ch < a.c) {
+                float t = 0.f;
+                for (int q = 0; q < rgn; ++q) t += red[q * cw + tch];
+                a.dbpart[(long long)blockIdx.x * a.c + ch] = t;
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -195,11 +221,7 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s) {
     HGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_bn_bwd_fin, dim3(a.c), dim3(256), 0, s, a);
     HGNN_LAUNCH_CHECK();
-    const long long n = (long long)a.cap_rows * a.c;
-    int blocks = (int)ceil_div<long long>(n, 256);
-    if (blocks > 4096) blocks = 4096;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -143,6 +143,35 @@ struct GemmDwArgs {
 int launch_gemm_dw(const GemmDwArgs& g, hipStream_t s);
 size_t gemm_dw_slab_floats(int r_cap, int o, int k);
 
+// ---------------------------------------------------------------- GEMM v2 (gemm2.hip)
+struct RepackItem {
+    const float* wl;   // linear conv weight (d, K)
+    const float* wr;   // ReLU conv weight (d, K)
+    const float* bl;
+    const float* br;
+    float* wt;         // out: [K][2d]
+    float* wc;         // out: [2d][kp]
+    float* bc;         // out: [2d]
+    int k, kp;
+};
+constexpr int REPACK_MAX = 24;
+struct RepackTable {
+    RepackItem it[REPACK_MAX];
+    int n, d;
+};
+int launch_repack(const RepackTable& t, hipStream_t s);
+int launch_gemm2_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const float* wt, int n,
+                     const float* bias, int relu_from, float* y, int ldy, float* bn_part, hipStream_t s);
+int launch_gemm2_da(const float* dy, int lddy, const int* m_valid, int m_cap, int o, const float* w0,
+                    const float* w1, int split, int ldw, int k, float* da, int ldda, hipStream_t s);
+int launch_gemm2_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o,
+                    int k, int kchunk, float* slabs, hipStream_t s);
+// slabs -> dW (split rows) ; bias grads from the BN-backward per-tile column sums of dY
+int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int k, int split, float* dw0,
+                      float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s);
+int dw2_kchunk(int r_cap, int o, int k);
+size_t dw2_slab_floats(int r_cap, int o, int k);
+
 // ---------------------------------------------------------------- BN
 struct BnFwdArgs {
     const float* part;     // [tiles][c][3]
@@ -179,6 +208,7 @@ struct BnBwdArgs {
     float* dy;             // out [rows][c]
     float* dw;             // scalar out
     float* db;             // scalar out
+    float* dbpart;         // optional out: per-64-row-tile column sums of dy [tiles][c]
 };
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s);
 int bn_bwd_tiles(int cap_rows);

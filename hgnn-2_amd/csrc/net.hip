@@ -35,7 +35,9 @@ struct Half {
     int out, bn;
     int pw_lin, pb_lin, pw_relu, pb_relu, pbn_w, pbn_b;
     int relu_from;
+    int kp;  // row stride of the aggregate / dA buffers (k rounded up to 4 for GEMM v2)
     size_t a = 0, part = 0, mean = 0, stdv = 0;
+    size_t wt = 0, wc = 0, bc = 0;  // GEMM v2 repacked weights
 };
 
 struct Program {
@@ -48,7 +50,8 @@ struct Program {
     size_t node_off = 0, edge_off = 0, totals = 0, err = 0;
     size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
     int entry_stride_w = 4;
-    size_t dy = 0, da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0;
+    size_t dy = 0, da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0;
+    bool v2 = false;  // GEMM v2 path (2d % 4 == 0); gemm.hip otherwise
     size_t bytes = 0;
 };
 
@@ -214,16 +217,24 @@ Program build_program(const hgnn_net_config* c) {
     }
     size_t max_da = 0, max_slab = 0;
     int max_cap = 0;
+    P.v2 = (P.c2 % 4) == 0;
     for (auto& h : P.halves) {
         const int cap = h.edge ? P.cap_e : P.cap_n;
-        h.a = B.take((size_t)cap * h.k * sizeof(float));
+        h.kp = P.v2 ? (h.k + 3) / 4 * 4 : h.k;
+        h.a = B.take((size_t)cap * h.kp * sizeof(float));
         h.part = B.take((size_t)gemm_fwd_tiles_m(cap) * P.c2 * 3 * sizeof(float));
         h.mean = B.take(P.c2 * sizeof(float));
         h.stdv = B.take(P.c2 * sizeof(float));
-        max_da = std::max(max_da, (size_t)cap * h.k);
-        max_slab = std::max(max_slab, gemm_dw_slab_floats(cap, P.c2, h.k));
+        if (P.v2) {
+            h.wt = B.take((size_t)h.k * P.c2 * sizeof(float));
+            h.wc = B.take((size_t)P.c2 * h.kp * sizeof(float));
+            h.bc = B.take((size_t)P.c2 * sizeof(float));
+        }
+        max_da = std::max(max_da, (size_t)cap * h.kp);
+        max_slab = std::max(max_slab, P.v2 ? dw2_slab_floats(cap, P.c2, h.k) : gemm_dw_slab_floats(cap, P.c2, h.k));
         max_cap = std::max(max_cap, cap);
     }
+    P.dbpart = B.take((size_t)bn_bwd_tiles(max_cap > 0 ? max_cap : 1) * P.c2 * sizeof(float));
     P.a_last = B.take((size_t)P.cap_n * P.k_last * sizeof(float));
     P.colsum = B.take((size_t)c->bs * P.k_last * sizeof(float));
     max_da = std::max(max_da, (size_t)P.cap_n * P.k_last);
@@ -319,6 +330,28 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
 
     const int* tot_n = m.totals;
     const int* tot_e = m.totals + 1;
+    if (P.v2) {
+        // repack the Conv1d pairs of every half: Wcat^T (forward B) and padded Wcat (dA B)
+        RepackTable rt{};
+        rt.d = P.d;
+        for (size_t hi = 0; hi < P.halves.size(); ++hi) {
+            const Half& h = P.halves[hi];
+            RepackItem& it = rt.it[rt.n++];
+            it.wl = prm[h.pw_lin];
+            it.wr = prm[h.pw_relu];
+            it.bl = prm[h.pb_lin];
+            it.br = prm[h.pb_relu];
+            it.wt = at<float>(ws, h.wt);
+            it.wc = at<float>(ws, h.wc);
+            it.bc = at<float>(ws, h.bc);
+            it.k = h.k;
+            it.kp = h.kp;
+            if (rt.n == REPACK_MAX || hi + 1 == P.halves.size()) {
+                TL(HGNN_K_STRUCT, launch_repack(rt, s));
+                rt.n = 0;
+            }
+        }
+    }
     for (const Half& h : P.halves) {
         const int cap = h.edge ? P.cap_e : P.cap_n;
         const int* tot = h.edge ? tot_e : tot_n;
@@ -335,9 +368,14 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
             ag.cp = h.cp;
         }
         ag.out = at<float>(ws, h.a);
-        ag.ldo = h.k;
+        ag.ldo = h.kp;
         TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
 
+        if (P.v2) {
+            TL(HGNN_K_GEMM_FWD, launch_gemm2_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.k, at<float>(ws, h.wt), P.c2,
+                                                 at<float>(ws, h.bc), h.relu_from, at<float>(ws, P.feats[h.out].y),
+                                                 P.c2, c->training ? at<float>(ws, h.part) : nullptr, s));
+        } else {
         GemmFwdArgs gf{};
         gf.a = at<float>(ws, h.a);
         gf.lda = h.k;
@@ -355,6 +393,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
         gf.ldy = P.c2;
         gf.bn_part = c->training ? at<float>(ws, h.part) : nullptr;
         TL(HGNN_K_GEMM_FWD, launch_gemm_fwd(gf, s));
+        }
 
         BnFwdArgs bf{};
         bf.part = at<float>(ws, h.part);
@@ -510,8 +549,17 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         bb.dy = at<float>(ws, P.dy);
         bb.dw = grads[h.pbn_w];
         bb.db = grads[h.pbn_b];
+        bb.dbpart = P.v2 ? at<float>(ws, P.dbpart) : nullptr;
         TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s));
 
+        if (P.v2) {
+            const int kc = dw2_kchunk(cap, P.c2, h.k);
+            TL(HGNN_K_GEMM_DW, launch_gemm2_dw(at<float>(ws, P.dy), P.c2, at<float>(ws, h.a), h.kp, tot, cap, P.c2,
+                                               h.k, kc, at<float>(ws, P.slabs), s));
+            TL(HGNN_K_GEMM_DW, launch_dw_reduce2(at<float>(ws, P.slabs), tot, kc, P.c2, h.k, P.d, grads[h.pw_lin],
+                                                 grads[h.pw_relu], at<float>(ws, P.dbpart), grads[h.pb_lin],
+                                                 grads[h.pb_relu], s));
+        } else {
         GemmDwArgs gw{};
         gw.dy = at<float>(ws, P.dy);
         gw.lddy = P.c2;
@@ -528,11 +576,16 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         gw.db0 = grads[h.pb_lin];
         gw.db1 = grads[h.pb_relu];
         TL(HGNN_K_GEMM_DW, launch_gemm_dw(gw, s));
+        }
 
         const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
         const bool ndw = need_dw && !h.edge;
         if (!ng && !np && !ndw) continue;
         float* da = at<float>(ws, P.da);
+        if (P.v2) {
+            TL(HGNN_K_GEMM_DA, launch_gemm2_da(at<float>(ws, P.dy), P.c2, tot, cap, P.c2, at<float>(ws, h.wc),
+                                               at<float>(ws, h.wc), 1 << 30, h.kp, h.k, da, h.kp, s));
+        } else {
         GemmDaArgs gd{};
         gd.dy = at<float>(ws, P.dy);
         gd.lddy = P.c2;
@@ -546,14 +599,15 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         gd.da = da;
         gd.ldda = h.k;
         TL(HGNN_K_GEMM_DA, launch_gemm_da(gd, s));
-        if (ndw) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, da, h.k, false, 1));
+        }
+        if (ndw) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, da, h.kp, false, 1));
         if (ng) {
             AggBwdArgs ab{};
             ab.total_rows = tot;
             ab.cap_rows = cap;
             ab.g = view(P, ws, h.edge ? S_WLT : S_WT);
             ab.ing = da;
-            ab.ldg = h.k;
+            ab.ldg = h.kp;
             ab.gofs = 0;
             ab.jtot = P.jt;
             ab.c = h.cg;
@@ -570,7 +624,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
             ab.cap_rows = other_edge ? P.cap_e : P.cap_n;
             ab.p = view(P, ws, h.edge ? S_PN : S_PE);
             ab.inp = da;
-            ab.ldp = h.k;
+            ab.ldp = h.kp;
             ab.pofs_m = P.jt * h.cg;
             ab.pofs_d = P.jt * h.cg + h.cp;
             ab.jtot = P.jt;
