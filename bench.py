@@ -103,6 +103,8 @@ def main():
     X.requires_grad_(True)
     W.requires_grad_(True)
     crit = torch.nn.MSELoss()
+    from hgnn_amd.dp import GradAllReduce
+    allreduce = GradAllReduce(params)
 
     def step():
         for p in params:
@@ -111,13 +113,7 @@ def main():
         out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
         loss = crit(out, T)
         loss.backward()
-        if world > 1:
-            grads = [p.grad for p in params]
-            flat = torch._utils._flatten_dense_tensors(grads)
-            dist.all_reduce(flat)
-            flat.div_(world)
-            for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
-                g.copy_(f)
+        allreduce()  # no-op at N = 1
         return loss
 
     for _ in range(args.warmup):

@@ -110,24 +110,61 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part(BnBwdArgs a) {
     if (r0 >= total) return;
     const int r1 = min(total, r0 + 64);
     const float wv = *a.w;
-    for (int ch = threadIdx.x; ch < a.c; ch += blockDim.x) {
-        const float mu = a.mean[ch], sd = a.std[ch];
+    // all 256 threads busy: rgn row groups x cw channels; 4 independent loads in flight per thread
+    __shared__ float red[4][256];
+    const int cw = a.c < 256 ? a.c : 256;
+    const int rgn = 256 / cw;
+    const int tch = threadIdx.x % cw, rg = threadIdx.x / cw;
+    for (int ch0 = 0; ch0 < a.c; ch0 += cw) {
+        const int ch = ch0 + tch;
         float s1 = 0.f, s2 = 0.f, t1 = 0.f, t2 = 0.f;
-        for (int r = r0; r < r1; ++r) {
-            const long long i = (long long)r * a.c + ch;
-            const float dz = a.dz[i];
-            const float h = __fdiv_rn(__fsub_rn(a.y[i], mu), sd);
-            const float g = wv * dz;
-            s1 += g;
-            s2 = fmaf(g, h, s2);
-            t1 = fmaf(dz, h, t1);
-            t2 += dz;
+        if (rg < rgn && ch < a.c) {
+            const float mu = a.mean[ch], sd = a.std[ch];
+            int r = r0 + rg;
+            for (; r + 3 * rgn < r1; r += 4 * rgn) {
+                float dz[4], yv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const long long i = (long long)(r + u * rgn) * a.c + ch;
+                    dz[u] = a.dz[i];
+                    yv[u] = a.y[i];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float h = __fdiv_rn(__fsub_rn(yv[u], mu), sd);
+                    const float g = wv * dz[u];
+                    s1 += g;
+                    s2 = fmaf(g, h, s2);
+                    t1 = fmaf(dz[u], h, t1);
+                    t2 += dz[u];
+                }
+            }
+            for (; r < r1; r += rgn) {
+                const long long i = (long long)r * a.c + ch;
+                const float dz = a.dz[i];
+                const float h = __fdiv_rn(__fsub_rn(a.y[i], mu), sd);
+                const float g = wv * dz;
+                s1 += g;
+                s2 = fmaf(g, h, s2);
+                t1 = fmaf(dz, h, t1);
+                t2 += dz;
+            }
         }
-        float* p = a.part + ((long long)tile * a.c + ch) * 4;
-        p[0] = s1;
-        p[1] = s2;
-        p[2] = t1;
-        p[3] = t2;
+        red[0][threadIdx.x] = s1;
+        red[1][threadIdx.x] = s2;
+        red[2][threadIdx.x] = t1;
+        red[3][threadIdx.x] = t2;
+        __syncthreads();
+        if (rg == 0 && ch < a.c) {
+            float* p = a.part + ((long long)tile * a.c + ch) * 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float t = 0.f;
+                for (int q = 0; q < rgn; ++q) t += red[j][q * cw + tch];
+                p[j] = t;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -186,10 +223,8 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
             const float mu = a.mean[ch];
             const float m1 = a.sums[ch * 4 + 0] * inv_n;
             const float m2 = a.sums[ch * 4 + 1] * inv_n;
-            for (int r = r0 + rg; r < r1; r += rgn) {
-                const long long i = (long long)r * a.c + ch;
-                const float yv = a.y[i];
-                const float g = wv * a.dz[i];
+            auto one = [&](float yv, float dzv) {
+                const float g = wv * dzv;
                 float d;
                 if (a.training) {
                     const float h = __fdiv_rn(__fsub_rn(yv, mu), sd);
@@ -198,6 +233,27 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
                     d = g / sd;
                 }
                 if (ch >= a.relu_from && !(yv > 0.f)) d = 0.f;
+                return d;
+            };
+            int r = r0 + rg;
+            for (; r + 3 * rgn < r1; r += 4 * rgn) {
+                float yv[4], dzv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const long long i = (long long)(r + u * rgn) * a.c + ch;
+                    yv[u] = a.y[i];
+                    dzv[u] = a.dz[i];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float d = one(yv[u], dzv[u]);
+                    a.dy[(long long)(r + u * rgn) * a.c + ch] = d;
+                    cs += d;
+                }
+            }
+            for (; r < r1; r += rgn) {
+                const long long i = (long long)r * a.c + ch;
+                const float d = one(a.y[i], a.dz[i]);
                 a.dy[i] = d;
                 cs += d;
             }
@@ -313,6 +369,16 @@ __global__ void __launch_bounds__(256) k_readout_bwd_part(const float* __restric
             part[((long long)blockIdx.y * dim_out + o) * k + kk] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
         }
         __syncthreads();
+        if (blockIdx.x == 0) {  // this chunk's sum of dout (bias gradient partial)
+            double sb = 0.0;
+            for (int b = b0 + (int)threadIdx.x; b < b1; b += 256) sb += (double)dout[b * dim_out + o];
+            red[g][threadIdx.x & 63] = wave_sum_d(sb);
+            __syncthreads();
+            if (threadIdx.x == 0)
+                part[(long long)RB_CHUNKS * dim_out * k + blockIdx.y * dim_out + o] =
+                    red[0][0] + red[1][0] + red[2][0] + red[3][0];
+            __syncthreads();
+        }
     }
 }
 
@@ -329,12 +395,16 @@ __global__ void __launch_bounds__(256) k_readout_bwd_params(const float* __restr
     }
     if (idx < dim_out) {
         double s = 0.0;
-        for (int b = 0; b < bs; ++b) s += (double)dout[b * dim_out + idx];
+        for (int c = 0; c < RB_CHUNKS; ++c) s += part[(long long)RB_CHUNKS * dim_out * k + c * dim_out + idx];
         dfcb[idx] = (float)(s * (double)nmax);
     }
+    (void)dout;
+    (void)bs;
 }
 
-size_t readout_bwd_scratch_bytes(int dim_out, int k) { return sizeof(double) * RB_CHUNKS * dim_out * (size_t)k; }
+size_t readout_bwd_scratch_bytes(int dim_out, int k) {
+    return sizeof(double) * RB_CHUNKS * dim_out * ((size_t)k + 1);
+}
 
 int launch_readout_bwd_params(const float* dout, const float* colsum, int bs, int nmax, int dim_out, int k,
                               float* dfcw, float* dfcb, void* scratch, hipStream_t s) {

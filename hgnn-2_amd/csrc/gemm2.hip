@@ -400,26 +400,48 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
     const int rows = *r_valid;
     if (idx < M * N) {
         const int zv = ceil_div(rows, kchunk);
-        float s = 0.f;
-        for (int z = 0; z < zv; ++z) s += slabs[(long long)z * M * N + idx];
+        const long long st = (long long)M * N;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int z = 0;
+        for (; z + 4 <= zv; z += 4) {
+            s0 += slabs[z * st + idx];
+            s1 += slabs[(z + 1) * st + idx];
+            s2 += slabs[(z + 2) * st + idx];
+            s3 += slabs[(z + 3) * st + idx];
+        }
+        for (; z < zv; ++z) s0 += slabs[z * st + idx];
+        const float s = (s0 + s1) + (s2 + s3);
         const int o = idx / N, c = idx % N;
         if (o < split) dw0[(long long)o * N + c] = s;
         else dw1[(long long)(o - split) * N + c] = s;
-    } else if (idx < M * N + M) {
-        const int o = idx - M * N;
-        const int tv = ceil_div(rows, 64);
-        double s = 0.0;
-        for (int t = 0; t < tv; ++t) s += (double)dbpart[(long long)t * M + o];
-        if (o < split) db0[o] = (float)s;
-        else db1[o - split] = (float)s;
+    }
+}
+
+// bias gradient: one block per output channel sums the per-tile column sums of dY
+__global__ void __launch_bounds__(256) k_db_reduce(const int* r_valid, int M, int split,
+                                                   const float* __restrict__ dbpart, float* db0, float* db1) {
+    __shared__ double red[4];
+    const int o = blockIdx.x;
+    const int tv = ceil_div(*r_valid, 64);
+    double s = 0.0;
+    for (int t = threadIdx.x; t < tv; t += 256) s += (double)dbpart[(long long)t * M + o];
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double t = red[0] + red[1] + red[2] + red[3];
+        if (o < split) db0[o] = (float)t;
+        else db1[o - split] = (float)t;
     }
 }
 
 int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int k, int split, float* dw0,
                       float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s) {
-    const int total = o * k + o;
+    const int total = o * k;
     hipLaunchKernelGGL(k_dw_reduce2, dim3(ceil_div(total, 256)), dim3(256), 0, s, slabs, r_valid, kchunk, o, k,
                        split, dw0, dw1, dbpart, db0, db1);
+    HGNN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_db_reduce, dim3(o), dim3(256), 0, s, r_valid, o, split, dbpart, db0, db1);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -1,0 +1,85 @@
+"""World-size-2 data-parallel gradient all-reduce over gloo (CPU).
+
+Each rank computes the oracle's gradients for its own shard of graphs (the
+model math is the reference's, oracle/ref_mnb.py), the shared GradAllReduce
+(hgnn_amd/dp.py, the exact code bench.py runs over RCCL) averages them, and
+rank 0 checks the result against the average of both shards' gradients
+computed in one process: "2 reference batches, gradients averaged"
+(SURVEY.md §8 e semantics caveat).
+"""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard_grads(rank, d=8, L=3):
+    import sys
+    for p in (REPO, os.path.join(REPO, "hgnn-2_amd"), os.path.join(REPO, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import fixture_util as fu
+    import hgnn_amd.datagen as dg
+    from functions.batching import prepare_batch
+    from functions.operators import graph_operators
+    from models.gnns.model_mnb import GNN_lg
+    from oracle import ref_mnb as R
+    graphs = dg.qm9_shape_dataset(6, seed=500 + rank)
+    data = [[X, A, t, *graph_operators([X, A], 1, True)] for X, A, t in graphs]
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = prepare_batch(data, 0, 1)
+    m = GNN_lg(0, d, L, 5, 1, 1, 2)
+    fu.det_init(m, 42)
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    st = R.bn_states(L, 2 * d)
+    out = R.gnn_lg(p, [X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg, L, 2, st, True)
+    torch.nn.MSELoss()(out, T).backward()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "hgnn-2_amd"))
+    from hgnn_amd.dp import GradAllReduce
+    p = _shard_grads(rank)
+    params = [p[k] for k in sorted(p)]
+    GradAllReduce(params)()
+    if rank == 0:  # numpy copies: pickled by value, no shared-memory handle outliving the worker
+        q.put({k: p[k].grad.detach().numpy().copy() for k in sorted(p)})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_grad_allreduce_matches_shard_average():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    got = q.get(timeout=300)
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    g0 = _shard_grads(0)
+    g1 = _shard_grads(1)
+    for k, v in got.items():
+        v = torch.from_numpy(v)
+        ref = (g0[k].grad + g1[k].grad) / 2
+        assert torch.allclose(v, ref, rtol=1e-6, atol=1e-7), k
