@@ -1,0 +1,1052 @@
+// Covariant compositional networks (CCN_1D / CCN_2D) on gfx950.
+//
+// Reference: models/compnets/model_ccn.py (CCN_1D 18-64, CCN_2D 68-105) over
+// functions/utils_ccn.py (receptive fields and chi matrices 66-145, base
+// features 148-222, promotions 225-278, updates 281-324) and
+// functions/contraction.py (collapse6to3, 106-121).
+//
+// Index construction (bit-exact with the reference's int semantics):
+//   nbr_i = ascending nonzero(adj[i])  (utils_ccn.py:195-199), d_i = |nbr_i| (incl. self loop)
+//   pos[i][a][x] = index of nbr_i[x] in nbr_{j_a} or -1, j_a = nbr_i[a]  == the chi_{i j_a}
+//   matrices (utils_ccn.py:66-106) as position maps.
+// CCN-1D layer, node i (n = d_i):  T[a][x] = F_{j_a}[pos(x)] ;  row[x] = sum_a T, col[a] = sum_x T;
+//   F'_i[x] = relu(W [row[x] | col[x]] + b)                        (utils_ccn.py:303-324)
+// CCN-2D layer: T[a][b][z] = F_{j_a}[pos(b)][pos(z)] (chi F chi^T), H = T (x) chi_ii = T (x) I, and
+//   the 18 contractions of collapse6to3 reduce to (re-derived in DESIGN.md):
+//     q0 = n Sc, q1 = q1[x], q2 = n Sa, q3 = q3[x], q4 = d_xy tot, q5 = Sc, q6..14 = n Sc,
+//     q15 = T[x][y][y], q16 = T[y][x][y], q17 = d_xy sum_k T[k][k][k]
+//   with Sc[a][b] = sum_z T, Sa[b][z] = sum_a T, q1[a] = sum_bz T, q3[b] = sum_az T.
+//   O(n^3 C) per node instead of the reference's materialised n^5 C tensor.
+// Backward is a gather over the transposed position maps (no atomics): node j collects,
+// for every neighbour i, the gradient of the entries of T_i that read F_j.
+#include <vector>
+
+#include "kernels.h"
+
+namespace hgnn {
+namespace {
+
+constexpr int CCN_MAXD = 64;  // degree bound (one wave per receptive field row)
+
+struct CcnPlanView {
+    const int* node_off;   // (bs + 1)
+    const int* deg;        // per node
+    const int* nbr;        // per node: slot of nmax global node ids
+    const int* selfpos;    // index of i in nbr_i
+    const int* graph;      // node -> graph
+    const int* off1;       // exclusive prefix of deg      (row offsets of 1D features)
+    const int* off2;       // exclusive prefix of deg^2    (row offsets of 2D features, pos maps)
+    const int* pos;        // [sum deg^2] position maps
+    int nmax;
+};
+
+// ------------------------------------------------------------------ plan
+__global__ void __launch_bounds__(256) k_ccn_nbrs(const float* __restrict__ adj, int nmax, const int* node_off,
+                                                  int* deg, int* nbr, int* selfpos, int* graph, uint32_t* err) {
+    const int b = blockIdx.x;
+    const int n0 = node_off[b];
+    const int nb = node_off[b + 1] - n0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const float* A = adj + (long long)b * nmax * nmax;
+    for (int r = wv; r < nb; r += 4) {
+        const int gi = n0 + r;
+        int cnt = 0, sp = -1;
+        for (int c0 = 0; c0 < nb; c0 += 64) {
+            const int c = c0 + lane;
+            const bool nz = c < nb && A[(long long)r * nmax + c] > 0.f;   // utils_ccn.py:195 (A > 0)
+            // the gather-form backward walks N(j) for the readers of F_j: needs a symmetric pattern
+            if (c < nb && nz != (A[(long long)c * nmax + r] > 0.f)) atomicOr(err, (uint32_t)ERR_CCN_ASYM);
+            const unsigned long long m = __ballot(nz);
+            const int p = __popcll(m & ((1ull << lane) - 1ull));
+            if (nz) {
+                nbr[(long long)gi * nmax + cnt + p] = n0 + c;
+                if (c == r) sp = cnt + p;
+            }
+            cnt += __popcll(m);
+        }
+        // self position: the lane that saw c == r holds it
+        const unsigned long long hs = __ballot(sp >= 0);
+        if (lane == 0) {
+            deg[gi] = cnt;
+            graph[gi] = b;
+            if (cnt > CCN_MAXD) atomicOr(err, (uint32_t)ERR_CCN_DEGREE);
+        }
+        if (hs == 0ull) {
+            if (lane == 0) {
+                selfpos[gi] = -1;
+                atomicOr(err, (uint32_t)ERR_CCN_SELFLOOP);
+            }
+        } else if (sp >= 0) {
+            selfpos[gi] = sp;
+        }
+    }
+}
+
+// exclusive scans of deg and deg^2 over all nodes (single block); totals[0..1]
+__global__ void __launch_bounds__(256) k_ccn_scan(const int* deg, const int* total_nodes, int* off1, int* off2,
+                                                  int* totals) {
+    __shared__ int s1[256], s2[256], carry[2];
+    const int t = threadIdx.x;
+    const int n = *total_nodes;
+    if (t == 0) carry[0] = carry[1] = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += 256) {
+        const int i = base + t;
+        const int d = i < n ? deg[i] : 0;
+        s1[t] = d;
+        s2[t] = d * d;
+        __syncthreads();
+        for (int o = 1; o < 256; o <<= 1) {
+            const int a1 = t >= o ? s1[t - o] : 0, a2 = t >= o ? s2[t - o] : 0;
+            __syncthreads();
+            s1[t] += a1;
+            s2[t] += a2;
+            __syncthreads();
+        }
+        if (i < n) {
+            off1[i] = carry[0] + s1[t] - d;
+            off2[i] = carry[1] + s2[t] - d * d;
+        }
+        __syncthreads();
+        if (t == 255) {
+            carry[0] += s1[255];
+            carry[1] += s2[255];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        off1[n] = carry[0];
+        off2[n] = carry[1];
+        totals[0] = carry[0];
+        totals[1] = carry[1];
+    }
+}
+
+// pos[off2[i] + a*d_i + x] = index of nbr_i[x] in nbr_{nbr_i[a]} (binary search), or -1
+__global__ void __launch_bounds__(256) k_ccn_pos(CcnPlanView v, const int* total_nodes, int* pos) {
+    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    if (i >= *total_nodes) return;
+    const int n = v.deg[i];
+    if (n > CCN_MAXD) return;
+    const int* ni = v.nbr + (long long)i * v.nmax;
+    const int me = lane < n ? ni[lane] : -1;
+    for (int a = 0; a < n; ++a) {
+        const int j = ni[a];
+        const int dj = v.deg[j];
+        const int* nj = v.nbr + (long long)j * v.nmax;
+        int p = -1;
+        if (lane < n) {
+            int lo = 0, hi = dj - 1;
+            while (lo <= hi) {
+                const int mid = (lo + hi) >> 1;
+                const int val = nj[mid];
+                if (val == me) {
+                    p = mid;
+                    break;
+                }
+                if (val < me) lo = mid + 1;
+                else hi = mid - 1;
+            }
+            pos[v.off2[i] + a * n + lane] = p;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ CCN-1D
+// One wave per node; lane x = receptive-field position.  Level-0 input is X tiled
+// (utils_ccn.py:212-216): F_0[j][p] = X[j].
+__global__ void __launch_bounds__(256) k_ccn1_fwd(CcnPlanView v, const int* total_nodes, const float* __restrict__ fin,
+                                                  int level0, const float* __restrict__ X, int cin,
+                                                  const float* __restrict__ W, const float* __restrict__ bias, int h,
+                                                  float* __restrict__ coll, float* __restrict__ fout) {
+    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    if (i >= *total_nodes) return;
+    const int n = v.deg[i];
+    if (n > CCN_MAXD) return;
+    const int* ni = v.nbr + (long long)i * v.nmax;
+    const int* pi = v.pos + v.off2[i];
+    const long long row = (long long)v.off1[i] + lane;
+    const int k2 = 2 * cin;
+    for (int c = 0; c < cin; ++c) {
+        float rsum = 0.f, mycol = 0.f;
+        for (int a = 0; a < n; ++a) {
+            const int j = ni[a];
+            float t = 0.f;
+            if (lane < n) {
+                const int p = pi[a * n + lane];
+                if (p >= 0) t = level0 ? X[(long long)j * cin + c] : fin[((long long)v.off1[j] + p) * cin + c];
+            }
+            rsum += t;
+            const float cs = wave_sum(t);
+            if (lane == a) mycol = cs;
+        }
+        if (lane < n) {
+            coll[row * k2 + c] = rsum;
+            coll[row * k2 + cin + c] = mycol;
+        }
+    }
+    if (lane < n) {
+        for (int o = 0; o < h; ++o) {
+            float s = bias[o];
+            for (int k = 0; k < k2; ++k) s = fmaf(W[o * k2 + k], coll[row * k2 + k], s);
+            fout[row * h + o] = s < 0.f ? 0.f : s;
+        }
+    }
+}
+
+// dpre = dF * relu'; param partials per node; dcoll = W^T dpre  -> [drow | dcol]
+__global__ void __launch_bounds__(256) k_ccn1_bwd_node(CcnPlanView v, const int* total_nodes,
+                                                       const float* __restrict__ dF, const float* __restrict__ F,
+                                                       const float* __restrict__ coll, int cin,
+                                                       const float* __restrict__ W, int h, float* __restrict__ dcoll,
+                                                       float* __restrict__ ppart) {
+    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    if (i >= *total_nodes) return;
+    const int n = v.deg[i];
+    const int k2 = 2 * cin;
+    const long long row = (long long)v.off1[i] + lane;
+    const bool act = lane < n && n <= CCN_MAXD;
+    float* pp = ppart + (long long)i * (h * k2 + h);
+    for (int o = 0; o < h; ++o) {
+        float dp = 0.f;
+        if (act) dp = F[row * h + o] > 0.f ? dF[row * h + o] : 0.f;
+        for (int k = 0; k < k2; ++k) {
+            const float c = act ? coll[row * k2 + k] : 0.f;
+            const float s = wave_sum(dp * c);
+            if (lane == 0) pp[o * k2 + k] = s;
+        }
+        const float sb = wave_sum(dp);
+        if (lane == 0) pp[h * k2 + o] = sb;
+    }
+    if (act) {
+        for (int k = 0; k < k2; ++k) {
+            float s = 0.f;
+            for (int o = 0; o < h; ++o) {
+                const float dp = F[row * h + o] > 0.f ? dF[row * h + o] : 0.f;
+                s = fmaf(W[o * k2 + k], dp, s);
+            }
+            dcoll[row * k2 + k] = s;
+        }
+    }
+}
+
+// dF_prev[j][u] = sum_{i in N(j)} [q(u) valid] (drow_i[q(u)] + dcol_i[aj]) (+ readout term);
+// level 0: dX[j] = sum_u of it + d_j * dsum0
+__global__ void __launch_bounds__(256) k_ccn1_bwd_gather(CcnPlanView v, const int* total_nodes,
+                                                         const float* __restrict__ dcoll, int cin,
+                                                         const float* __restrict__ dsum, int dsum_ld, int dsum_off,
+                                                         int level0, float* __restrict__ dout) {
+    const int j = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    if (j >= *total_nodes) return;
+    const int n = v.deg[j];
+    if (n > CCN_MAXD) return;
+    const int* nj = v.nbr + (long long)j * v.nmax;
+    const int* pj = v.pos + v.off2[j];
+    const int sj = v.selfpos[j];
+    const int g = v.graph[j];
+    const int k2 = 2 * cin;
+    for (int c = 0; c < cin; ++c) {
+        float acc = 0.f;
+        if (lane < n) {
+            for (int a = 0; a < n; ++a) {
+                const int i = nj[a];
+                const int q = pj[a * n + lane];
+                if (q < 0) continue;
+                const int aj = pj[a * n + sj];
+                const long long ri = v.off1[i];
+                acc += dcoll[(ri + q) * k2 + c] + dcoll[(ri + aj) * k2 + cin + c];
+            }
+        }
+        const float rd = dsum ? dsum[(long long)g * dsum_ld + dsum_off + c] : 0.f;
+        if (level0) {
+            const float s = wave_sum(acc);
+            if (lane == 0) dout[(long long)j * cin + c] = s + (float)n * rd;
+        } else if (lane < n) {
+            dout[((long long)v.off1[j] + lane) * cin + c] = acc + rd;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ CCN-2D
+struct C2Save {
+    float* Sc;   // [sum d^2][C]  Sc[a][b]
+    float* Sa;   // [sum d^2][C]  Sa[b][z]
+    float* D1;   // [sum d^2][C]  T[a][b][b]
+    float* D2;   // [sum d^2][C]  T[a][b][a]
+    float* q1;   // [sum d][C]
+    float* q3;   // [sum d][C]
+    float* tot;  // [nodes][C]
+    float* d3;   // [nodes][C]
+};
+
+// Block per node i; wave w owns rows b = w, w+4, ...; lane z.
+__global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* total_nodes, const float* __restrict__ fin,
+                                                  int level0, const float* __restrict__ X, int cin,
+                                                  const float* __restrict__ W, const float* __restrict__ bias, int h,
+                                                  C2Save sv, float* __restrict__ fout) {
+    __shared__ int sp[CCN_MAXD * CCN_MAXD];
+    __shared__ float sq1[CCN_MAXD], sd3;
+    const int i = blockIdx.x;
+    if (i >= *total_nodes) return;
+    const int n = v.deg[i];
+    if (n > CCN_MAXD) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int* ni = v.nbr + (long long)i * v.nmax;
+    const long long o2 = v.off2[i], o1 = v.off1[i];
+    for (int e = threadIdx.x; e < n * n; e += 256) sp[e] = v.pos[o2 + e];
+    __syncthreads();
+    for (int c = 0; c < cin; ++c) {
+        if (threadIdx.x < CCN_MAXD) sq1[threadIdx.x] = 0.f;
+        if (threadIdx.x == 0) sd3 = 0.f;
+        __syncthreads();
+        for (int b = wv; b < n; b += 4) {
+            float sa = 0.f, q3 = 0.f;
+            for (int a = 0; a < n; ++a) {
+                const int j = ni[a];
+                const int pb = sp[a * n + b];
+                float t = 0.f;
+                if (lane < n && pb >= 0) {
+                    const int pz = sp[a * n + lane];
+                    if (pz >= 0) {
+                        if (level0) {
+                            t = X[(long long)j * cin + c];
+                        } else {
+                            const int dj = v.deg[j];
+                            t = fin[((long long)v.off2[j] + pb * dj + pz) * cin + c];
+                        }
+                    }
+                }
+                sa += t;
+                const float sc = wave_sum(t);
+                if (lane == 0) {
+                    sv.Sc[(o2 + a * n + b) * cin + c] = sc;
+                    atomicAdd(&sq1[a], sc);
+                }
+                if (lane == b) sv.D1[(o2 + a * n + b) * cin + c] = t;
+                if (lane == a) sv.D2[(o2 + a * n + b) * cin + c] = t;
+                if (lane == a && a == b) atomicAdd(&sd3, t);
+            }
+            if (lane < n) sv.Sa[(o2 + b * n + lane) * cin + c] = sa;
+            q3 = wave_sum(sa);
+            if (lane == 0) sv.q3[(o1 + b) * cin + c] = q3;
+        }
+        __syncthreads();
+        if (threadIdx.x < n) sv.q1[(o1 + threadIdx.x) * cin + c] = sq1[threadIdx.x];
+        if (threadIdx.x == 0) {
+            float t = 0.f;
+            for (int a = 0; a < n; ++a) t += sq1[a];
+            sv.tot[(long long)i * cin + c] = t;
+            sv.d3[(long long)i * cin + c] = sd3;
+        }
+        __syncthreads();
+    }
+    // output: out[x][y][o] = relu(sum_q W_q . block_q[x][y] + b)   (W: h x 18 C, block q at cols q*C..)
+    const float nf = (float)n;
+    const int K = 18 * cin;
+    for (int e = threadIdx.x; e < n * n; e += 256) {
+        const int x = e / n, y = e % n;
+        for (int o = 0; o < h; ++o) {
+            const float* w = W + (long long)o * K;
+            float s = bias[o];
+            for (int c = 0; c < cin; ++c) {
+                const float sc = sv.Sc[(o2 + x * n + y) * cin + c];
+                const float sa = sv.Sa[(o2 + x * n + y) * cin + c];
+                float blk[18];
+                blk[0] = nf * sc;
+                blk[1] = sv.q1[(o1 + x) * cin + c];
+                blk[2] = nf * sa;
+                blk[3] = sv.q3[(o1 + x) * cin + c];
+                blk[4] = x == y ? sv.tot[(long long)i * cin + c] : 0.f;
+                blk[5] = sc;
+#pragma unroll
+                for (int q = 6; q < 15; ++q) blk[q] = nf * sc;
+                blk[15] = sv.D1[(o2 + x * n + y) * cin + c];
+                blk[16] = sv.D2[(o2 + y * n + x) * cin + c];
+                blk[17] = x == y ? sv.d3[(long long)i * cin + c] : 0.f;
+#pragma unroll
+                for (int q = 0; q < 18; ++q) s = fmaf(w[q * cin + c], blk[q], s);
+            }
+            fout[(o2 + e) * h + o] = s < 0.f ? 0.f : s;
+        }
+    }
+}
+
+struct C2Grad {
+    float* dSc;  // [sum d^2][C]  (dSc + dq1 folded)
+    float* dSa;  // [sum d^2][C]  (dSa + dq3 + dtot folded)
+    float* dD1;  // [sum d^2][C]
+    float* dD2;  // [sum d^2][C]  indexed [a][b]
+    float* dd3;  // [nodes][C]
+};
+
+// Block per node: dpre = dF * relu'(F); param partials; node-level gradient matrices.
+__global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int* total_nodes,
+                                                       const float* __restrict__ dF, const float* __restrict__ F,
+                                                       C2Save sv, int cin, const float* __restrict__ W, int h,
+                                                       C2Grad gd, float* __restrict__ ppart) {
+    __shared__ float sdq1[CCN_MAXD], sdq3[CCN_MAXD], sdtot, sdd3;
+    __shared__ float red[256];
+    const int i = blockIdx.x;
+    if (i >= *total_nodes) return;
+    const int n = v.deg[i];
+    if (n > CCN_MAXD) return;
+    const long long o2 = v.off2[i], o1 = v.off1[i];
+    const float nf = (float)n;
+    const int K = 18 * cin;
+    float* pp = ppart + (long long)i * (h * K + h);
+    // parameter partials: dW[o][q*C + c] = sum_xy dpre[x][y][o] * block_q[x][y][c]
+    for (int o = 0; o < h; ++o) {
+        for (int c = 0; c < cin; ++c) {
+            float acc[18];
+#pragma unroll
+            for (int q = 0; q < 18; ++q) acc[q] = 0.f;
+            for (int e = threadIdx.x; e < n * n; e += 256) {
+                const int x = e / n, y = e % n;
+                const long long r = o2 + e;
+                const float dp = F[r * h + o] > 0.f ? dF[r * h + o] : 0.f;
+                const float sc = sv.Sc[r * cin + c];
+                acc[0] = fmaf(dp, nf * sc, acc[0]);
+                acc[1] = fmaf(dp, sv.q1[(o1 + x) * cin + c], acc[1]);
+                acc[2] = fmaf(dp, nf * sv.Sa[r * cin + c], acc[2]);
+                acc[3] = fmaf(dp, sv.q3[(o1 + x) * cin + c], acc[3]);
+                if (x == y) {
+                    acc[4] = fmaf(dp, sv.tot[(long long)i * cin + c], acc[4]);
+                    acc[17] = fmaf(dp, sv.d3[(long long)i * cin + c], acc[17]);
+                }
+                acc[5] = fmaf(dp, sc, acc[5]);
+                acc[15] = fmaf(dp, sv.D1[r * cin + c], acc[15]);
+                acc[16] = fmaf(dp, sv.D2[(o2 + y * n + x) * cin + c], acc[16]);
+            }
+#pragma unroll
+            for (int q = 6; q < 15; ++q) acc[q] = acc[0];
+#pragma unroll
+            for (int q = 0; q < 18; ++q) {
+                if (q >= 6 && q < 15) continue;
+                red[threadIdx.x] = acc[q];
+                __syncthreads();
+                for (int s = 128; s > 0; s >>= 1) {
+                    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+                    __syncthreads();
+                }
+                if (threadIdx.x == 0) {
+                    pp[o * K + q * cin + c] = red[0];
+                    if (q == 0)
+                        for (int qq = 6; qq < 15; ++qq) pp[o * K + qq * cin + c] = red[0];
+                }
+                __syncthreads();
+            }
+        }
+        float sb = 0.f;
+        for (int e = threadIdx.x; e < n * n; e += 256) {
+            const long long r = o2 + e;
+            sb += F[r * h + o] > 0.f ? dF[r * h + o] : 0.f;
+        }
+        red[threadIdx.x] = sb;
+        __syncthreads();
+        for (int s = 128; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) pp[h * K + o] = red[0];
+        __syncthreads();
+    }
+    // input-side gradients of the contraction blocks: g_q = W_q^T dpre
+    for (int c = 0; c < cin; ++c) {
+        if (threadIdx.x < CCN_MAXD) sdq1[threadIdx.x] = sdq3[threadIdx.x] = 0.f;
+        if (threadIdx.x == 0) sdtot = sdd3 = 0.f;
+        __syncthreads();
+        for (int e = threadIdx.x; e < n * n; e += 256) {
+            const int x = e / n, y = e % n;
+            const long long r = o2 + e;
+            float g[18];
+#pragma unroll
+            for (int q = 0; q < 18; ++q) g[q] = 0.f;
+            for (int o = 0; o < h; ++o) {
+                const float dp = F[r * h + o] > 0.f ? dF[r * h + o] : 0.f;
+                const float* w = W + (long long)o * K;
+#pragma unroll
+                for (int q = 0; q < 18; ++q) g[q] = fmaf(w[q * cin + c], dp, g[q]);
+            }
+            float gsc = g[0] + g[5];
+            float s9 = 0.f;
+#pragma unroll
+            for (int q = 6; q < 15; ++q) s9 += g[q];
+            gsc = nf * (g[0] + s9) + g[5];
+            gd.dSc[r * cin + c] = gsc;
+            gd.dSa[r * cin + c] = nf * g[2];
+            gd.dD1[r * cin + c] = g[15];
+            gd.dD2[(o2 + y * n + x) * cin + c] = g[16];
+            atomicAdd(&sdq1[x], g[1]);
+            atomicAdd(&sdq3[x], g[3]);
+            if (x == y) {
+                atomicAdd(&sdtot, g[4]);
+                atomicAdd(&sdd3, g[17]);
+            }
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < n * n; e += 256) {
+            const int a = e / n;
+            const long long r = o2 + e;
+            gd.dSc[r * cin + c] += sdq1[a];          // q1[a] = sum_b Sc[a][b]
+            gd.dSa[r * cin + c] += sdq3[a] + sdtot;  // q3[b] = sum_z Sa[b][z]; tot touches every entry
+        }
+        if (threadIdx.x == 0) gd.dd3[(long long)i * cin + c] = sdd3;
+        __syncthreads();
+    }
+}
+
+// Block per node j; thread per (u, v): dF_prev[j][u][v] = sum over neighbours i of the gradient of the
+// entry of T_i that read F_j[u][v] (+ readout); level 0: dX[j] = sum over (u, v) (+ d_j^2 dsum0).
+__global__ void __launch_bounds__(256) k_ccn2_bwd_gather(CcnPlanView v, const int* total_nodes, C2Grad gd, int cin,
+                                                         const float* __restrict__ dsum, int dsum_ld, int dsum_off,
+                                                         int level0, float* __restrict__ dout) {
+    __shared__ int sp[CCN_MAXD * CCN_MAXD];
+    __shared__ float red[256];
+    const int j = blockIdx.x;
+    if (j >= *total_nodes) return;
+    const int n = v.deg[j];
+    if (n > CCN_MAXD) return;
+    const long long o2 = v.off2[j];
+    const int* nj = v.nbr + (long long)j * v.nmax;
+    const int sj = v.selfpos[j];
+    const int g = v.graph[j];
+    for (int e = threadIdx.x; e < n * n; e += 256) sp[e] = v.pos[o2 + e];
+    __syncthreads();
+    for (int c = 0; c < cin; ++c) {
+        const float rd = dsum ? dsum[(long long)g * dsum_ld + dsum_off + c] : 0.f;
+        float part = 0.f;
+        for (int e = threadIdx.x; e < n * n; e += 256) {
+            const int u = e / n, w = e % n;
+            float acc = 0.f;
+            for (int a = 0; a < n; ++a) {
+                const int b = sp[a * n + u], z = sp[a * n + w];
+                if (b < 0 || z < 0) continue;
+                const int i = nj[a];
+                const int aj = sp[a * n + sj];
+                const int di = v.deg[i];
+                const long long oi = v.off2[i];
+                float t = gd.dSc[(oi + aj * di + b) * cin + c] + gd.dSa[(oi + b * di + z) * cin + c];
+                if (z == b) t += gd.dD1[(oi + aj * di + b) * cin + c];
+                if (z == aj) t += gd.dD2[(oi + aj * di + b) * cin + c];
+                if (aj == b && b == z) t += gd.dd3[(long long)i * cin + c];
+                acc += t;
+            }
+            if (level0) part += acc;
+            else dout[(o2 + e) * cin + c] = acc + rd;
+        }
+        if (level0) {
+            red[threadIdx.x] = part;
+            __syncthreads();
+            for (int s = 128; s > 0; s >>= 1) {
+                if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+                __syncthreads();
+            }
+            if (threadIdx.x == 0) dout[(long long)j * cin + c] = red[0] + (float)(n * n) * rd;
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------ readout
+// feat[b] = cat_l (sum over the graph's rows of F_l); level 0: sum_i d_i^order X[i]
+struct ReadoutArgs {
+    CcnPlanView v;
+    int order, L, f, h, n_out, bs;
+    const float* X;
+    const float* F[16];   // levels 1..L (packed)
+    const float* fcw;
+    const float* fcb;
+    float* feat;          // [bs][f + L h]
+    float* out;           // [bs][n_out]
+};
+
+__global__ void __launch_bounds__(256) k_ccn_readout(ReadoutArgs r) {
+    __shared__ double red[4];
+    const int b = blockIdx.x;
+    const int n0 = r.v.node_off[b], n1 = r.v.node_off[b + 1];
+    const int* off = r.order == 1 ? r.v.off1 : r.v.off2;
+    const int nf = r.f + r.L * r.h;
+    float* feat = r.feat + (long long)b * nf;
+    auto bsum = [&](double x) {
+        x = wave_sum_d(x);
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+        __syncthreads();
+        return red[0] + red[1] + red[2] + red[3];
+    };
+    for (int c = 0; c < r.f; ++c) {
+        double s = 0.0;
+        for (int i = n0 + (int)threadIdx.x; i < n1; i += 256) {
+            const double d = r.v.deg[i];
+            s += (r.order == 1 ? d : d * d) * (double)r.X[(long long)i * r.f + c];
+        }
+        const double t = bsum(s);
+        if (threadIdx.x == 0) feat[c] = (float)t;
+    }
+    for (int l = 0; l < r.L; ++l) {
+        const long long r0 = off[n0], r1 = off[n1];
+        for (int c = 0; c < r.h; ++c) {
+            double s = 0.0;
+            for (long long q = r0 + threadIdx.x; q < r1; q += 256) s += (double)r.F[l][q * r.h + c];
+            const double t = bsum(s);
+            if (threadIdx.x == 0) feat[r.f + l * r.h + c] = (float)t;
+        }
+    }
+    __syncthreads();
+    for (int o = 0; o < r.n_out; ++o) {
+        double s = 0.0;
+        for (int k = threadIdx.x; k < nf; k += 256) s += (double)r.fcw[o * nf + k] * (double)feat[k];
+        const double t = bsum(s);
+        if (threadIdx.x == 0) r.out[(long long)b * r.n_out + o] = (float)(t + (double)r.fcb[o]);
+    }
+}
+
+// dsum[b][k] = sum_o dout[b][o] fcw[o][k];  dfcw, dfcb summed over graphs (one block)
+__global__ void __launch_bounds__(256) k_ccn_readout_bwd(const float* __restrict__ dout, const float* __restrict__ feat,
+                                                         const float* __restrict__ fcw, int bs, int n_out, int nf,
+                                                         float* __restrict__ dsum, float* __restrict__ dfcw,
+                                                         float* __restrict__ dfcb) {
+    for (int e = threadIdx.x; e < bs * nf; e += 256) {
+        const int b = e / nf, k = e % nf;
+        float s = 0.f;
+        for (int o = 0; o < n_out; ++o) s = fmaf(dout[b * n_out + o], fcw[o * nf + k], s);
+        dsum[e] = s;
+    }
+    for (int e = threadIdx.x; e < n_out * nf; e += 256) {
+        const int o = e / nf, k = e % nf;
+        double s = 0.0;
+        for (int b = 0; b < bs; ++b) s += (double)dout[b * n_out + o] * (double)feat[(long long)b * nf + k];
+        dfcw[e] = (float)s;
+    }
+    for (int o = threadIdx.x; o < n_out; o += 256) {
+        double s = 0.0;
+        for (int b = 0; b < bs; ++b) s += (double)dout[b * n_out + o];
+        dfcb[o] = (float)s;
+    }
+}
+
+// sum the per-node parameter partials: out[k] = sum_i part[i][k]  (k < kw: weight, then bias)
+__global__ void __launch_bounds__(256) k_ccn_param_reduce(const float* __restrict__ part, const int* total_nodes,
+                                                          int kw, int kb, float* __restrict__ dw, float* __restrict__ db) {
+    __shared__ double red[4];
+    const int k = blockIdx.x;
+    const int n = *total_nodes;
+    const int stride = kw + kb;
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) s += (double)part[(long long)i * stride + k];
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double t = red[0] + red[1] + red[2] + red[3];
+        if (k < kw) dw[k] = (float)t;
+        else db[k - kw] = (float)t;
+    }
+}
+
+// dF[row][c] = dsum[graph][off + c] for every feature row of the node (top level)
+__global__ void k_ccn_bcast(CcnPlanView v, const int* total_nodes, int order, const float* __restrict__ dsum, int ld,
+                            int off, int h, float* __restrict__ dF) {
+    const int i = blockIdx.x;
+    if (i >= *total_nodes) return;
+    const int g = v.graph[i];
+    const long long r0 = order == 1 ? v.off1[i] : v.off2[i];
+    const long long r1 = order == 1 ? v.off1[i + 1] : v.off2[i + 1];
+    for (long long q = r0 * h + threadIdx.x; q < r1 * h; q += blockDim.x) dF[q] = dsum[(long long)g * ld + off + (int)(q % h)];
+}
+
+// X (bs, nmax, f) padded -> packed [nodes][f]; and the inverse for dX (zero padding)
+__global__ void k_ccn_pack_x(const float* __restrict__ X, const int* node_off, int nmax, int f, float* __restrict__ Xp) {
+    const int b = blockIdx.x;
+    const int n0 = node_off[b], nb = node_off[b + 1] - n0;
+    for (int e = threadIdx.x; e < nb * f; e += blockDim.x) Xp[(long long)n0 * f + e] = X[(long long)b * nmax * f + e];
+}
+
+__global__ void k_ccn_unpack_dx(const float* __restrict__ dXp, const int* node_off, int nmax, int f,
+                                float* __restrict__ dX) {
+    const int b = blockIdx.x;
+    const int n0 = node_off[b], nb = node_off[b + 1] - n0;
+    for (int e = threadIdx.x; e < nmax * f; e += blockDim.x)
+        dX[(long long)b * nmax * f + e] = e < nb * f ? dXp[(long long)n0 * f + e] : 0.f;
+}
+
+// collapse6to3 on a general F (C, n, n, n, n, n): out[x][y][q*C + ch]
+// (functions/contraction.py: _c6to2_111 44-61, _c6to2_12 64-85, _c6to2_3 88-103)
+__global__ void k_collapse6to3(const float* __restrict__ F, float* __restrict__ out, int C, int n) {
+    const long long tot = (long long)n * n * 18 * C;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= tot) return;
+    const int ch = (int)(idx % C), q = (int)((idx / C) % 18);
+    const int y = (int)((idx / (18LL * C)) % n), x = (int)(idx / (18LL * C * n));
+    auto G = [&](int a, int b, int c, int d, int e) {
+        return F[(((((long long)ch * n + a) * n + b) * n + c) * n + d) * n + e];
+    };
+    float s = 0.f;
+    if (q == 0) {
+        for (int c = 0; c < n; ++c) for (int d = 0; d < n; ++d) for (int e = 0; e < n; ++e) s += G(x, y, c, d, e);
+    } else if (q == 1) {
+        for (int b = 0; b < n; ++b) for (int c = 0; c < n; ++c) for (int e = 0; e < n; ++e) s += G(x, b, c, y, e);
+    } else if (q == 2) {
+        for (int a = 0; a < n; ++a) for (int d = 0; d < n; ++d) for (int e = 0; e < n; ++e) s += G(a, x, y, d, e);
+    } else if (q == 3) {
+        for (int a = 0; a < n; ++a) for (int c = 0; c < n; ++c) for (int e = 0; e < n; ++e) s += G(a, x, c, y, e);
+    } else if (q == 4) {
+        for (int a = 0; a < n; ++a) for (int b = 0; b < n; ++b) for (int c = 0; c < n; ++c) s += G(a, b, c, x, y);
+    } else if (q == 5) {
+        for (int e = 0; e < n; ++e) for (int c = 0; c < n; ++c) s += G(x, y, c, c, e);
+    } else if (q < 15) {
+        for (int c = 0; c < n; ++c) for (int d = 0; d < n; ++d) s += G(x, y, c, d, d);
+    } else if (q == 15) {
+        for (int b = 0; b < n; ++b) s += G(x, b, b, y, b);
+    } else if (q == 16) {
+        for (int a = 0; a < n; ++a) s += G(a, x, a, y, a);
+    } else {
+        for (int a = 0; a < n; ++a) s += G(a, a, a, x, y);
+    }
+    out[idx] = s;
+}
+
+// adjoint of k_collapse6to3: dF[ch][a][b][c][d][e] from dOut[x][y][q*C + ch]
+__global__ void k_collapse6to3_bwd(const float* __restrict__ dO, float* __restrict__ dF, int C, int n) {
+    const long long tot = (long long)C * n * n * n * n * n;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= tot) return;
+    long long t = idx;
+    const int e = (int)(t % n); t /= n;
+    const int d = (int)(t % n); t /= n;
+    const int c = (int)(t % n); t /= n;
+    const int b = (int)(t % n); t /= n;
+    const int a = (int)(t % n); t /= n;
+    const int ch = (int)t;
+    auto g = [&](int x, int y, int q) { return dO[((long long)x * n + y) * 18 * C + q * C + ch]; };
+    float s = g(a, b, 0) + g(a, d, 1) + g(b, c, 2) + g(b, d, 3) + g(d, e, 4);
+    if (c == d) s += g(a, b, 5);
+    if (d == e)
+        for (int q = 6; q < 15; ++q) s += g(a, b, q);
+    if (b == c && c == e) s += g(a, d, 15);
+    if (a == c && c == e) s += g(b, d, 16);
+    if (a == b && b == c) s += g(d, e, 17);
+    dF[idx] = s;
+}
+
+// ------------------------------------------------------------------ executor
+struct CcnLayout {
+    size_t node_off, deg, nbr, selfpos, graph, off1, off2, totals, err, pos;
+    size_t plan_bytes;
+    // feature workspace (needs sums)
+    std::vector<size_t> F, coll;    // per level 1..L
+    std::vector<C2Save> dummy;
+    size_t sc[16], sa[16], d1[16], d2[16], q1[16], q3[16], tot[16], d3[16];
+    size_t feat, dsum, ppart, dF[2], dcoll, g_sc, g_sa, g_d1, g_d2, g_d3, xp, dxp;
+    size_t bytes;
+};
+
+size_t al(size_t x) { return (x + 255) / 256 * 256; }
+
+bool ccn_ok(const hgnn_ccn_config* c) {
+    return c && (c->order == 1 || c->order == 2) && c->bs > 0 && c->nmax > 0 && c->f_in > 0 && c->hidden > 0 &&
+           c->layers >= 1 && c->layers <= 15 && c->n_out > 0;
+}
+
+CcnLayout ccn_layout(const hgnn_ccn_config* c, long long sum_d, long long sum_d2) {
+    CcnLayout L{};
+    const long long nodes = (long long)c->bs * c->nmax;
+    size_t t = 0;
+    auto take = [&](size_t n) {
+        const size_t o = t;
+        t += al(n);
+        return o;
+    };
+    L.node_off = take(4 * (c->bs + 1));
+    L.deg = take(4 * nodes);
+    L.nbr = take(4 * nodes * c->nmax);
+    L.selfpos = take(4 * nodes);
+    L.graph = take(4 * nodes);
+    L.off1 = take(4 * (nodes + 1));
+    L.off2 = take(4 * (nodes + 1));
+    L.totals = take(16);
+    L.err = take(16);
+    L.pos = take(4 * (size_t)(sum_d2 > 0 ? sum_d2 : 1));
+    L.plan_bytes = t;
+    const long long rows = c->order == 1 ? sum_d : sum_d2;
+    const int Lv = c->layers;
+    const int h = c->hidden, f = c->f_in;
+    L.F.resize(Lv);
+    L.coll.resize(Lv);
+    int cmax = f > h ? f : h;
+    for (int l = 0; l < Lv; ++l) {
+        const int cin = l == 0 ? f : h;
+        L.F[l] = take(4 * (size_t)rows * h);
+        if (c->order == 1) {
+            L.coll[l] = take(4 * (size_t)rows * 2 * cin);
+        } else {
+            L.sc[l] = take(4 * (size_t)sum_d2 * cin);
+            L.sa[l] = take(4 * (size_t)sum_d2 * cin);
+            L.d1[l] = take(4 * (size_t)sum_d2 * cin);
+            L.d2[l] = take(4 * (size_t)sum_d2 * cin);
+            L.q1[l] = take(4 * (size_t)sum_d * cin);
+            L.q3[l] = take(4 * (size_t)sum_d * cin);
+            L.tot[l] = take(4 * (size_t)nodes * cin);
+            L.d3[l] = take(4 * (size_t)nodes * cin);
+        }
+    }
+    const int nf = f + Lv * h;
+    L.feat = take(4 * (size_t)c->bs * nf);
+    L.dsum = take(4 * (size_t)c->bs * nf);
+    const int kmax = (c->order == 1 ? 2 : 18) * cmax;
+    L.ppart = take(4 * (size_t)nodes * (h * kmax + h));
+    L.dF[0] = take(4 * (size_t)rows * cmax);
+    L.dF[1] = take(4 * (size_t)rows * cmax);
+    if (c->order == 1) {
+        L.dcoll = take(4 * (size_t)rows * 2 * cmax);
+    } else {
+        L.g_sc = take(4 * (size_t)sum_d2 * cmax);
+        L.g_sa = take(4 * (size_t)sum_d2 * cmax);
+        L.g_d1 = take(4 * (size_t)sum_d2 * cmax);
+        L.g_d2 = take(4 * (size_t)sum_d2 * cmax);
+        L.g_d3 = take(4 * (size_t)nodes * cmax);
+    }
+    L.xp = take(4 * (size_t)nodes * f);
+    L.dxp = take(4 * (size_t)nodes * f);
+    L.bytes = t;
+    return L;
+}
+
+template <typename T>
+T* P(void* base, size_t off) {
+    return reinterpret_cast<T*>(static_cast<char*>(base) + off);
+}
+
+CcnPlanView plan_view(const hgnn_ccn_config* c, const CcnLayout& L, void* ws) {
+    CcnPlanView v;
+    v.node_off = P<int>(ws, L.node_off);
+    v.deg = P<int>(ws, L.deg);
+    v.nbr = P<int>(ws, L.nbr);
+    v.selfpos = P<int>(ws, L.selfpos);
+    v.graph = P<int>(ws, L.graph);
+    v.off1 = P<int>(ws, L.off1);
+    v.off2 = P<int>(ws, L.off2);
+    v.pos = P<int>(ws, L.pos);
+    v.nmax = c->nmax;
+    return v;
+}
+
+C2Save save_of(const CcnLayout& L, void* ws, int l) {
+    C2Save s;
+    s.Sc = P<float>(ws, L.sc[l]);
+    s.Sa = P<float>(ws, L.sa[l]);
+    s.D1 = P<float>(ws, L.d1[l]);
+    s.D2 = P<float>(ws, L.d2[l]);
+    s.q1 = P<float>(ws, L.q1[l]);
+    s.q3 = P<float>(ws, L.q3[l]);
+    s.tot = P<float>(ws, L.tot[l]);
+    s.d3 = P<float>(ws, L.d3[l]);
+    return s;
+}
+
+}  // namespace
+}  // namespace hgnn
+
+using namespace hgnn;
+
+extern "C" {
+
+int hgnn_collapse6to3(const float* d_F, float* d_out, int c, int n, void* stream) {
+    if (!d_F || !d_out || c <= 0 || n <= 0) return HGNN_ERR_ARG;
+    const long long tot = (long long)n * n * 18 * c;
+    hipLaunchKernelGGL(k_collapse6to3, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_F,
+                       d_out, c, n);
+    HGNN_LAUNCH_CHECK();
+    return HGNN_OK;
+}
+
+int hgnn_collapse6to3_backward(const float* d_dout, float* d_dF, int c, int n, void* stream) {
+    if (!d_dout || !d_dF || c <= 0 || n <= 0) return HGNN_ERR_ARG;
+    const long long tot = (long long)c * n * n * n * n * n;
+    hipLaunchKernelGGL(k_collapse6to3_bwd, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       d_dout, d_dF, c, n);
+    HGNN_LAUNCH_CHECK();
+    return HGNN_OK;
+}
+
+int hgnn_ccn_plan_offsets(const hgnn_ccn_config* cfg, long long max_sum_d2, size_t* offs) {
+    if (!ccn_ok(cfg) || !offs) return HGNN_ERR_ARG;
+    const CcnLayout L = ccn_layout(cfg, 0, max_sum_d2);
+    const size_t o[9] = {L.node_off, L.deg, L.nbr, L.selfpos, L.graph, L.off1, L.off2, L.pos, L.err};
+    for (int i = 0; i < 9; ++i) offs[i] = o[i];
+    return HGNN_OK;
+}
+
+size_t hgnn_ccn_plan_bytes(const hgnn_ccn_config* cfg, long long max_sum_d2) {
+    if (!ccn_ok(cfg)) return 0;
+    return ccn_layout(cfg, 0, max_sum_d2).plan_bytes;
+}
+
+int hgnn_ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t* d_n_batch, void* plan_ws,
+                  long long max_sum_d2, long long* h_sums, void* stream) {
+    if (!ccn_ok(cfg) || !d_adj || !d_n_batch || !plan_ws || !h_sums) return HGNN_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const CcnLayout L = ccn_layout(cfg, 0, max_sum_d2);
+    BatchMeta m;
+    m.node_off = P<int>(plan_ws, L.node_off);
+    m.edge_off = P<int>(plan_ws, L.off1);  // scratch, overwritten by the scan
+    m.totals = P<int>(plan_ws, L.totals);
+    m.err = P<uint32_t>(plan_ws, L.err);
+    HGNN_HOST_CHECK(hipMemsetAsync(m.err, 0, 4, s));
+    int r = launch_plan(d_n_batch, nullptr, cfg->bs, cfg->nmax, 0, m, s);
+    if (r) return r;
+    CcnPlanView v = plan_view(cfg, L, plan_ws);
+    hipLaunchKernelGGL(k_ccn_nbrs, dim3(cfg->bs), dim3(256), 0, s, d_adj, cfg->nmax, v.node_off,
+                       P<int>(plan_ws, L.deg), P<int>(plan_ws, L.nbr), P<int>(plan_ws, L.selfpos),
+                       P<int>(plan_ws, L.graph), m.err);
+    HGNN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ccn_scan, dim3(1), dim3(256), 0, s, P<int>(plan_ws, L.deg), m.totals,
+                       P<int>(plan_ws, L.off1), P<int>(plan_ws, L.off2), m.totals + 2);
+    HGNN_LAUNCH_CHECK();
+    int hbuf[4] = {0, 0, 0, 0};
+    HGNN_HOST_CHECK(hipMemcpyAsync(hbuf, m.totals, 16, hipMemcpyDeviceToHost, s));
+    HGNN_HOST_CHECK(hipStreamSynchronize(s));
+    const long long nodes = hbuf[0];
+    h_sums[0] = hbuf[2];
+    h_sums[1] = hbuf[3];
+    h_sums[2] = nodes;
+    if (h_sums[1] > max_sum_d2) return HGNN_ERR_ARG;  // caller re-plans with a larger bound
+    hipLaunchKernelGGL(k_ccn_pos, dim3((unsigned)((nodes + 3) / 4 > 0 ? (nodes + 3) / 4 : 1)), dim3(256), 0, s, v,
+                       m.totals, P<int>(plan_ws, L.pos));
+    HGNN_LAUNCH_CHECK();
+    return HGNN_OK;
+}
+
+uint32_t* hgnn_ccn_error_word(const hgnn_ccn_config* cfg, void* plan_ws, long long max_sum_d2) {
+    if (!ccn_ok(cfg) || !plan_ws) return nullptr;
+    return P<uint32_t>(plan_ws, ccn_layout(cfg, 0, max_sum_d2).err);
+}
+
+size_t hgnn_ccn_workspace_bytes(const hgnn_ccn_config* cfg, const long long* sums) {
+    if (!ccn_ok(cfg) || !sums) return 0;
+    const CcnLayout L = ccn_layout(cfg, sums[0], sums[1]);
+    return L.bytes - L.plan_bytes;
+}
+
+static void* feat_ws(void* ws, const CcnLayout& L) { return static_cast<char*>(ws) - L.plan_bytes; }
+
+int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const float* d_X, const float* const* params,
+                     void* plan_ws, long long max_sum_d2, void* workspace, float* d_out, void* stream) {
+    if (!ccn_ok(cfg) || !sums || !d_X || !params || !plan_ws || !workspace || !d_out) return HGNN_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const CcnLayout Lp = ccn_layout(cfg, 0, max_sum_d2);
+    const CcnLayout L = ccn_layout(cfg, sums[0], sums[1]);
+    CcnPlanView v = plan_view(cfg, Lp, plan_ws);
+    void* W = feat_ws(workspace, L);
+    const int* tot = P<int>(plan_ws, Lp.totals);
+    const int nodes = (int)sums[2];
+    const int h = cfg->hidden, f = cfg->f_in;
+    float* Xp = P<float>(W, L.xp);
+    hipLaunchKernelGGL(k_ccn_pack_x, dim3(cfg->bs), dim3(256), 0, s, d_X, v.node_off, cfg->nmax, f, Xp);
+    HGNN_LAUNCH_CHECK();
+    d_X = Xp;
+    for (int l = 0; l < cfg->layers; ++l) {
+        const int cin = l == 0 ? f : h;
+        const float* fin = l == 0 ? nullptr : P<float>(W, L.F[l - 1]);
+        const float* w = params[2 * l];
+        const float* b = params[2 * l + 1];
+        if (cfg->order == 1) {
+            hipLaunchKernelGGL(k_ccn1_fwd, dim3(nodes > 0 ? (nodes + 3) / 4 : 1), dim3(256), 0, s, v, tot, fin,
+                               l == 0 ? 1 : 0, d_X, cin, w, b, h, P<float>(W, L.coll[l]), P<float>(W, L.F[l]));
+        } else {
+            hipLaunchKernelGGL(k_ccn2_fwd, dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s, v, tot, fin, l == 0 ? 1 : 0,
+                               d_X, cin, w, b, h, save_of(L, W, l), P<float>(W, L.F[l]));
+        }
+        HGNN_LAUNCH_CHECK();
+    }
+    ReadoutArgs ra{};
+    ra.v = v;
+    ra.order = cfg->order;
+    ra.L = cfg->layers;
+    ra.f = f;
+    ra.h = h;
+    ra.n_out = cfg->n_out;
+    ra.bs = cfg->bs;
+    ra.X = d_X;
+    for (int l = 0; l < cfg->layers; ++l) ra.F[l] = P<float>(W, L.F[l]);
+    ra.fcw = params[2 * cfg->layers];
+    ra.fcb = params[2 * cfg->layers + 1];
+    ra.feat = P<float>(W, L.feat);
+    ra.out = d_out;
+    hipLaunchKernelGGL(k_ccn_readout, dim3(cfg->bs), dim3(256), 0, s, ra);
+    HGNN_LAUNCH_CHECK();
+    return HGNN_OK;
+}
+
+int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const float* const* params, void* plan_ws,
+                      long long max_sum_d2, void* workspace, const float* d_dout, float* const* grads, float* d_dX,
+                      void* stream) {
+    if (!ccn_ok(cfg) || !sums || !params || !plan_ws || !workspace || !d_dout || !grads || !d_dX) return HGNN_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const CcnLayout Lp = ccn_layout(cfg, 0, max_sum_d2);
+    const CcnLayout L = ccn_layout(cfg, sums[0], sums[1]);
+    CcnPlanView v = plan_view(cfg, Lp, plan_ws);
+    void* W = feat_ws(workspace, L);
+    const int* tot = P<int>(plan_ws, Lp.totals);
+    const int nodes = (int)sums[2];
+    const int h = cfg->hidden, f = cfg->f_in, Lv = cfg->layers;
+    const int nf = f + Lv * h;
+    float* dsum = P<float>(W, L.dsum);
+    hipLaunchKernelGGL(k_ccn_readout_bwd, dim3(1), dim3(256), 0, s, d_dout, P<float>(W, L.feat), params[2 * Lv],
+                       cfg->bs, cfg->n_out, nf, dsum, grads[2 * Lv], grads[2 * Lv + 1]);
+    HGNN_LAUNCH_CHECK();
+    const unsigned nb4 = nodes > 0 ? (unsigned)(nodes + 3) / 4 : 1u;
+    const unsigned nb1 = nodes > 0 ? (unsigned)nodes : 1u;
+    const long long rows = cfg->order == 1 ? sums[0] : sums[1];
+    // dF of the top level = readout broadcast of its slice of dsum
+    float* dF = P<float>(W, L.dF[0]);
+    float* dFn = P<float>(W, L.dF[1]);
+    hipLaunchKernelGGL(k_ccn_bcast, dim3(nb1), dim3(64), 0, s, v, tot, cfg->order, dsum, nf, f + (Lv - 1) * h, h, dF);
+    HGNN_LAUNCH_CHECK();
+    for (int l = Lv - 1; l >= 0; --l) {
+        const int cin = l == 0 ? f : h;
+        const float* w = params[2 * l];
+        const int K = (cfg->order == 1 ? 2 : 18) * cin;
+        float* ppart = P<float>(W, L.ppart);
+        if (cfg->order == 1) {
+            hipLaunchKernelGGL(k_ccn1_bwd_node, dim3(nb4), dim3(256), 0, s, v, tot, dF, P<float>(W, L.F[l]),
+                               P<float>(W, L.coll[l]), cin, w, h, P<float>(W, L.dcoll), ppart);
+        } else {
+            C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
+                      P<float>(W, L.g_d3)};
+            hipLaunchKernelGGL(k_ccn2_bwd_node, dim3(nb1), dim3(256), 0, s, v, tot, dF, P<float>(W, L.F[l]),
+                               save_of(L, W, l), cin, w, h, gd, ppart);
+        }
+        HGNN_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_ccn_param_reduce, dim3(h * K + h), dim3(256), 0, s, ppart, tot, h * K, h, grads[2 * l],
+                           grads[2 * l + 1]);
+        HGNN_LAUNCH_CHECK();
+        const int lvl0 = l == 0 ? 1 : 0;
+        float* dst = lvl0 ? P<float>(W, L.dxp) : dFn;
+        const int doff = lvl0 ? 0 : f + (l - 1) * h;
+        if (cfg->order == 1) {
+            hipLaunchKernelGGL(k_ccn1_bwd_gather, dim3(nb4), dim3(256), 0, s, v, tot, P<float>(W, L.dcoll), cin, dsum,
+                               nf, doff, lvl0, dst);
+        } else {
+            C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
+                      P<float>(W, L.g_d3)};
+            hipLaunchKernelGGL(k_ccn2_bwd_gather, dim3(nb1), dim3(256), 0, s, v, tot, gd, cin, dsum, nf, doff, lvl0,
+                               dst);
+        }
+        HGNN_LAUNCH_CHECK();
+        float* t = dF;
+        dF = dFn;
+        dFn = t;
+    }
+    (void)rows;
+    hipLaunchKernelGGL(k_ccn_unpack_dx, dim3(cfg->bs), dim3(256), 0, s, P<float>(W, L.dxp), v.node_off, cfg->nmax, f,
+                       d_dX);
+    HGNN_LAUNCH_CHECK();
+    return HGNN_OK;
+}
+
+}  // extern "C"

@@ -38,6 +38,7 @@ enum : uint32_t {
     ERR_SIZES = 1u << 2,         // N_b > Nmax, E_b > Emax or negative count
     ERR_CCN_SELFLOOP = 1u << 3,  // CCN adjacency without self loop (chi_ii absent)
     ERR_CCN_DEGREE = 1u << 4,    // CCN degree above the compiled bound
+    ERR_CCN_ASYM = 1u << 5,      // CCN adjacency pattern not symmetric
 };
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -23,7 +23,8 @@ DEVERR = {
     0x2: "mask[:, :, 0] disagrees with N_batch / E_batch",
     0x4: "N_batch > Nmax, E_batch > Emax or a negative count",
     0x8: "CCN adjacency without a self loop (chi_ii undefined, functions/utils_ccn.py:137-140)",
-    0x10: "CCN vertex degree above the compiled bound",
+    0x10: "CCN vertex degree above the compiled bound (64)",
+    0x20: "CCN adjacency pattern is not symmetric (the batched CCN backward needs A_ij > 0 <=> A_ji > 0)",
 }
 
 
@@ -36,6 +37,10 @@ class NetConfig(ctypes.Structure):
 class NetInputs(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
         "d_X", "d_XL", "d_W", "d_WL", "d_Pm", "d_Pd", "d_N_batch", "d_E_batch", "d_mask", "d_mask_lg")]
+
+
+class CcnConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("order", "bs", "nmax", "f_in", "hidden", "layers", "n_out", "reserved")]
 
 
 _lib = None
@@ -68,6 +73,18 @@ SIGNATURES = {
                                 _VP], _I),
     "hgnn_net_backward_timed": ([ctypes.POINTER(NetConfig), ctypes.POINTER(NetInputs), _VP, _VP, _VP, _VP, _VP,
                                  _VP, _VP, _VP], _I),
+    "hgnn_ccn_plan_bytes": ([ctypes.POINTER(CcnConfig), ctypes.c_longlong], ctypes.c_size_t),
+    "hgnn_ccn_plan": ([ctypes.POINTER(CcnConfig), _VP, _VP, _VP, ctypes.c_longlong,
+                       ctypes.POINTER(ctypes.c_longlong), _VP], _I),
+    "hgnn_ccn_error_word": ([ctypes.POINTER(CcnConfig), _VP, ctypes.c_longlong], _VP),
+    "hgnn_ccn_workspace_bytes": ([ctypes.POINTER(CcnConfig), ctypes.POINTER(ctypes.c_longlong)], ctypes.c_size_t),
+    "hgnn_ccn_forward": ([ctypes.POINTER(CcnConfig), ctypes.POINTER(ctypes.c_longlong), _VP, _VP, _VP,
+                          ctypes.c_longlong, _VP, _VP, _VP], _I),
+    "hgnn_ccn_backward": ([ctypes.POINTER(CcnConfig), ctypes.POINTER(ctypes.c_longlong), _VP, _VP,
+                           ctypes.c_longlong, _VP, _VP, _VP, _VP, _VP], _I),
+    "hgnn_collapse6to3": ([_VP, _VP, _I, _I, _VP], _I),
+    "hgnn_collapse6to3_backward": ([_VP, _VP, _I, _I, _VP], _I),
+    "hgnn_ccn_plan_offsets": ([ctypes.POINTER(CcnConfig), ctypes.c_longlong, ctypes.POINTER(ctypes.c_size_t)], _I),
     "hgnn_conv1x1_workspace_bytes": ([_I, _I, _I, _I], ctypes.c_size_t),
     "hgnn_conv1x1_forward": ([_VP, _VP, _VP, _VP, _I, _I, _I, _I, _I, _VP, _VP], _I),
     "hgnn_conv1x1_backward": ([_VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _I, _VP, _VP], _I),

@@ -1,0 +1,174 @@
+"""Autograd binding of the batched CCN executor (hgnn_ccn_* in include/hgnn_amd.h).
+
+The reference builds every receptive field, chi matrix, promotion and the
+d^5 tensor product per node in Python (functions/utils_ccn.py:66-324,
+functions/contraction.py:106-121) and runs one graph per forward
+(models/compnets/model_ccn.py:41-64, 93-105).  Here a whole padded batch of
+graphs goes through three device phases (csrc/ccn.hip):
+
+  plan      neighbour lists, degrees, prefix offsets and chi position maps
+            (int, bit-exact with _get_chi) -- one small host sync for the
+            ragged totals that size the feature workspace;
+  forward   per level one kernel (promotion + contraction + Linear + ReLU
+            fused; the 2-D contraction uses the closed form of DESIGN.md
+            instead of materialising T (x) I), then the readout;
+  backward  the adjoint of each phase, gather-formulated (no atomics).
+
+X is (bs, nmax, f) zero-padded, adj (bs, nmax, nmax) with the self loops the
+reference's caller adds (scripts/train_ccn.py:36), n_batch (bs,) int64.
+"""
+
+import ctypes
+
+import torch
+
+from . import _lib as L
+from .net import _require_cuda, _f32, _i64, _raise_bits
+
+CCN_MAX_DEGREE = 64  # csrc/ccn.hip CCN_MAXD
+
+
+class CcnSpec:
+    def __init__(self, order, f_in, hidden, layers, n_out):
+        self.order = order
+        self.f_in = f_in
+        self.hidden = hidden
+        self.layers = layers
+        self.n_out = n_out
+
+    def config(self, bs, nmax):
+        return L.CcnConfig(self.order, bs, nmax, self.f_in, self.hidden, self.layers, self.n_out, 0)
+
+    def param_shapes(self):
+        m = 2 if self.order == 1 else 18
+        shapes = []
+        for l in range(self.layers):
+            cin = self.f_in if l == 0 else self.hidden
+            shapes += [(self.hidden, m * cin), (self.hidden,)]
+        shapes += [(self.n_out, self.f_in + self.layers * self.hidden), (self.n_out,)]
+        return shapes
+
+
+def _plan(cfg, adj, n_batch, stream):
+    lib = L.lib()
+    dev = adj.device
+    # upper bound of sum_i d_i^2 from the padded adjacency (exact when padding is zero)
+    deg = (adj > 0).sum(-1)
+    max_d2 = max(int((deg * deg).sum().item()), 1)
+    plan = torch.empty(lib.hgnn_ccn_plan_bytes(ctypes.byref(cfg), max_d2), dtype=torch.uint8, device=dev)
+    sums = (ctypes.c_longlong * 3)()
+    L.check(lib.hgnn_ccn_plan(ctypes.byref(cfg), L.ptr(adj), L.ptr(n_batch), L.ptr(plan), max_d2, sums, stream),
+            "hgnn_ccn_plan")
+    base = plan.data_ptr()
+    off = int(lib.hgnn_ccn_error_word(ctypes.byref(cfg), ctypes.c_void_p(base), max_d2)) - base
+    bits = int(plan[off:off + 4].view(torch.int32).item())
+    if bits:
+        _raise_bits(bits)
+    return plan, max_d2, sums
+
+
+class _CcnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec, X, adj, n_batch, *params):
+        lib = L.lib()
+        bs, nmax, _ = X.shape
+        cfg = spec.config(bs, nmax)
+        s = L.stream_handle(X.device)
+        plan, max_d2, sums = _plan(cfg, adj, n_batch, s)
+        ws = torch.empty(max(lib.hgnn_ccn_workspace_bytes(ctypes.byref(cfg), sums), 1), dtype=torch.uint8,
+                         device=X.device)
+        out = torch.empty(bs, spec.n_out, dtype=torch.float32, device=X.device)
+        pa = L.ptr_array(params)
+        L.check(lib.hgnn_ccn_forward(ctypes.byref(cfg), sums, L.ptr(X), pa, L.ptr(plan), max_d2, L.ptr(ws),
+                                     L.ptr(out), s), "hgnn_ccn_forward")
+        ctx.cfg, ctx.sums, ctx.plan, ctx.ws, ctx.max_d2 = cfg, sums, plan, ws, max_d2
+        ctx.params = params
+        ctx.x_shape = X.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = L.lib()
+        dout = dout.contiguous()
+        dev = dout.device
+        grads = [torch.empty_like(p) for p in ctx.params]
+        dX = torch.empty(ctx.x_shape, dtype=torch.float32, device=dev)
+        L.check(lib.hgnn_ccn_backward(ctypes.byref(ctx.cfg), ctx.sums, L.ptr_array(ctx.params), L.ptr(ctx.plan),
+                                      ctx.max_d2, L.ptr(ctx.ws), L.ptr(dout), L.ptr_array(grads), L.ptr(dX),
+                                      L.stream_handle(dev)), "hgnn_ccn_backward")
+        return (None, dX, None, None, *grads)
+
+
+def run_ccn(spec, params, X, adj, n_batch):
+    """Batched CCN forward: X (bs,nmax,f), adj (bs,nmax,nmax), n_batch (bs,) -> (bs, n_out)."""
+    _require_cuda([X, adj, n_batch, *params], "CCN")
+    if X.dim() != 3 or adj.dim() != 3:
+        raise RuntimeError(f"hgnn_amd: CCN expects X (bs,nmax,f) and adj (bs,nmax,nmax), got {tuple(X.shape)}, "
+                           f"{tuple(adj.shape)}")
+    bs, nmax, f = X.shape
+    if tuple(adj.shape) != (bs, nmax, nmax) or f != spec.f_in or n_batch.numel() != bs:
+        raise RuntimeError(f"hgnn_amd: CCN shape mismatch: X {tuple(X.shape)}, adj {tuple(adj.shape)}, "
+                           f"n_batch {tuple(n_batch.shape)}, input_feats {spec.f_in}")
+    for p, shp in zip(params, spec.param_shapes()):
+        if tuple(p.shape) != shp:
+            raise RuntimeError(f"hgnn_amd: CCN parameter shape {tuple(p.shape)} != {shp}")
+    return _CcnFn.apply(spec, _f32(X), _f32(adj), _i64(n_batch), *[_f32(p) for p in params])
+
+
+def plan_maps(order, X, adj, n_batch):
+    """Index construction only (for tests): per-graph (deg, nbr, pos) as numpy, read back from the device plan."""
+    import numpy as np
+    lib = L.lib()
+    bs, nmax, f = X.shape
+    cfg = L.CcnConfig(order, bs, nmax, f, 1, 1, 1, 0)
+    s = L.stream_handle(X.device)
+    plan, max_d2, sums = _plan(cfg, _f32(adj), _i64(n_batch), s)
+    offs = (ctypes.c_size_t * 9)()
+    L.check(lib.hgnn_ccn_plan_offsets(ctypes.byref(cfg), max_d2, offs), "hgnn_ccn_plan_offsets")
+    torch.cuda.synchronize(X.device)
+    h = plan.cpu().numpy()
+
+    def arr(i, n):
+        return h[offs[i]:offs[i] + 4 * n].view(np.int32)
+
+    nodes = bs * nmax
+    node_off = arr(0, bs + 1)
+    deg = arr(1, nodes)
+    nbr = arr(2, nodes * nmax)
+    off2 = arr(6, nodes + 1)
+    pos = arr(7, int(sums[1]))
+    out = []
+    for b in range(bs):
+        n0, n1 = int(node_off[b]), int(node_off[b + 1])
+        dg = deg[n0:n1].astype(np.int64)
+        nb = np.concatenate([nbr[i * nmax:i * nmax + deg[i]] for i in range(n0, n1)]) if n1 > n0 else np.zeros(0)
+        ps = pos[off2[n0]:off2[n1]].astype(np.int64)
+        out.append((dg, nb.astype(np.int64) - n0, ps))  # plan stores packed node ids
+    return out
+
+
+class _Collapse(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, F):
+        c, n = F.shape[0], F.shape[1]
+        out = torch.empty(n, n, 18 * c, dtype=torch.float32, device=F.device)
+        L.check(L.lib().hgnn_collapse6to3(L.ptr(F), L.ptr(out), c, n, L.stream_handle(F.device)),
+                "hgnn_collapse6to3")
+        ctx.shape = F.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        c, n = ctx.shape[0], ctx.shape[1]
+        dF = torch.empty(ctx.shape, dtype=torch.float32, device=dout.device)
+        L.check(L.lib().hgnn_collapse6to3_backward(L.ptr(dout.contiguous()), L.ptr(dF), c, n,
+                                                   L.stream_handle(dout.device)), "hgnn_collapse6to3_backward")
+        return dF
+
+
+def collapse6to3(F):
+    """F (C, n, n, n, n, n) -> (n, n, 18 C), contraction q at channels [q C, (q+1) C)."""
+    _require_cuda([F], "collapse6to3")
+    if F.dim() != 6 or any(F.shape[i] != F.shape[1] for i in range(1, 6)):
+        raise RuntimeError(f"hgnn_amd: collapse6to3 expects (C, n, n, n, n, n), got {tuple(F.shape)}")
+    return _Collapse.apply(_f32(F))

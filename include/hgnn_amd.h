@@ -50,6 +50,7 @@ extern "C" {
 #define HGNN_DEVERR_SIZES 0x4u        /* N_batch > Nmax, E_batch > Emax, < 0   */
 #define HGNN_DEVERR_CCN_SELFLOOP 0x8u /* CCN adjacency lacks a self loop        */
 #define HGNN_DEVERR_CCN_DEGREE 0x10u  /* CCN degree above the compiled bound    */
+#define HGNN_DEVERR_CCN_ASYM 0x20u    /* CCN adjacency pattern not symmetric    */
 
 int hgnn_abi_version(void);
 const char* hgnn_status_string(int status);
@@ -153,6 +154,56 @@ int hgnn_net_backward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* i
                             const float* const* params, void* workspace,
                             const float* d_dout, float* const* grads,
                             float* d_dX, float* d_dW, void* stream, void* timer);
+
+/* ------------------------------------------------------------------------
+ * Covariant compositional networks: CCN_1D / CCN_2D forward + backward.
+ *
+ * Replaces models/compnets/model_ccn.py:41-64 (CCN_1D.forward) and 93-105
+ * (CCN_2D.forward) with CompnetUtils' receptive fields / chi matrices
+ * (functions/utils_ccn.py:66-222), promotions and updates (225-324) and
+ * collapse6to3 (functions/contraction.py:106-121, evaluated in its O(n^3) closed
+ * form).  A batch of graphs is padded like prepare_batch does for the GNNs:
+ *   X (bs, nmax, f), adj (bs, nmax, nmax) WITH self loops (scripts/train_ccn.py:36),
+ *   n_batch (bs,) int64.
+ * Graphs are independent: output[b] is the reference's net(X_b, adj_b).
+ * Params: w1.weight w1.bias ... wL.weight wL.bias fc.weight fc.bias (nn.Linear).
+ * ---------------------------------------------------------------------- */
+typedef struct hgnn_ccn_config {
+    int32_t order;    /* 1: CCN_1D, 2: CCN_2D                         */
+    int32_t bs, nmax, f_in;
+    int32_t hidden;   /* hidden_size                                   */
+    int32_t layers;   /* number of update layers (<= 15)               */
+    int32_t n_out;    /* n_outputs                                     */
+    int32_t reserved;
+} hgnn_ccn_config;
+
+/* Plan: receptive fields, degrees, offsets and chi position maps (device).  The
+ * one synchronising call of the CCN path: it returns h_sums = {sum d_i,
+ * sum d_i^2, nodes} to size the feature workspace.  Pass the bound
+ * max_sum_d2 used to size plan_ws (e.g. bs * nmax^2); HGNN_ERR_ARG if exceeded. */
+size_t hgnn_ccn_plan_bytes(const hgnn_ccn_config* cfg, long long max_sum_d2);
+int hgnn_ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t* d_n_batch,
+                  void* plan_ws, long long max_sum_d2, long long* h_sums, void* stream);
+uint32_t* hgnn_ccn_error_word(const hgnn_ccn_config* cfg, void* plan_ws, long long max_sum_d2);
+size_t hgnn_ccn_workspace_bytes(const hgnn_ccn_config* cfg, const long long* sums);
+int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const float* d_X,
+                     const float* const* params, void* plan_ws, long long max_sum_d2,
+                     void* workspace, float* d_out, void* stream);
+/* grads overwritten (params order); d_dX (bs, nmax, f) overwritten. */
+int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const float* const* params,
+                      void* plan_ws, long long max_sum_d2, void* workspace, const float* d_dout,
+                      float* const* grads, float* d_dX, void* stream);
+
+/* collapse6to3 (functions/contraction.py:106-121) on a general 6-D tensor
+ * F (C, n, n, n, n, n) -> (n, n, 18 C); the 18 contractions of _c6to2_111 /
+ * _c6to2_12 / _c6to2_3 with their diagonal filters. */
+int hgnn_collapse6to3(const float* d_F, float* d_out, int c, int n, void* stream);
+int hgnn_collapse6to3_backward(const float* d_dout, float* d_dF, int c, int n, void* stream);
+
+/* Byte offsets inside plan_ws of: node_off, deg, nbr (nmax slots per node),
+ * selfpos, graph, off1 (prefix of d), off2 (prefix of d^2), pos (chi position
+ * maps), error word -- for inspection / tests of the index construction. */
+int hgnn_ccn_plan_offsets(const hgnn_ccn_config* cfg, long long max_sum_d2, size_t* offs);
 
 /* ------------------------------------------------------------------------
  * Layer-level drop-ins on dense padded tensors.

@@ -1,0 +1,162 @@
+"""CCN-1D / CCN-2D on the GPU vs the reference's fixtures and the oracle (oracle/ref_ccn.py).
+
+Tolerances (north_star: fp32 within 1e-5 of the reference's CPU forward):
+outputs |gpu - ref| <= 1e-5 max(1, |ref|); gradients within
+1e-4 max|g| + 1e-5 |g| (summation order differs from the reference's
+per-node autograd); index construction bit-exact.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import fixture_util as fu
+from test_oracle import ccn_graphs, ccn_params
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, ref, what, rel=1e-5):
+    got = got.detach().double().cpu()
+    ref = torch.as_tensor(ref).double()
+    err = (got - ref).abs().max().item() if got.numel() else 0.0
+    tol = rel * max(1.0, ref.abs().max().item() if ref.numel() else 0.0)
+    assert err <= tol, f"{what}: max err {err:.3g} > {tol:.3g}"
+
+
+def _grad_close(got, ref, what):
+    got = got.detach().double().cpu()
+    ref = torch.as_tensor(ref).double()
+    tol = 1e-4 * ref.abs().max().item() + 1e-5 * ref.abs() + 1e-7
+    bad = (got - ref).abs() > tol
+    assert not bad.any(), f"{what}: max err {(got - ref).abs().max().item():.3g}"
+
+
+def _pad(graphs, dev):
+    bs = len(graphs)
+    nmax = max(X.shape[0] for X, _, _ in graphs)
+    f = graphs[0][0].shape[1]
+    X = torch.zeros(bs, nmax, f)
+    A = torch.zeros(bs, nmax, nmax)
+    for b, (x, a, _) in enumerate(graphs):
+        n = x.shape[0]
+        X[b, :n] = x
+        A[b, :n, :n] = a
+    nb = torch.tensor([g[0].shape[0] for g in graphs], dtype=torch.int64)
+    return X.to(dev), A.to(dev), nb.to(dev)
+
+
+def test_ccn_plan_maps_bit_exact(golden):
+    from hgnn_amd.ccn import plan_maps
+    z = golden("ccn")
+    graphs = ccn_graphs(z)
+    X, A, nb = _pad(graphs, "cuda")
+    for order in (1, 2):
+        maps = plan_maps(order, X, A, nb)
+        for k, (deg, nbr, pos) in enumerate(maps):
+            assert np.array_equal(deg, z[f"deg_{k}"]), k
+            assert np.array_equal(nbr, z[f"nbr_{k}"]), k
+            assert np.array_equal(pos, z[f"pos_{k}"]), k
+
+
+def test_collapse6to3_matches_reference(golden):
+    from functions.contraction import collapse6to3
+    z = golden("ccn")
+    for d in range(1, 7):
+        T = torch.from_numpy(z[f"c6_T_{d}"])
+        H = (T.permute(3, 0, 1, 2).unsqueeze(4).unsqueeze(5) * torch.eye(d)).contiguous().cuda()
+        _close(collapse6to3(H), z[f"c6_out_{d}"], f"collapse d={d}")
+
+
+def test_collapse6to3_general_and_adjoint():
+    """General F (not T (x) I) vs the oracle's einsum restatement; backward = exact adjoint."""
+    from functions.contraction import collapse6to3
+    from oracle import ref_ccn as RC
+    g = torch.Generator().manual_seed(5)
+    for c, n in ((1, 2), (3, 4), (2, 5)):
+        F = torch.randn(c, n, n, n, n, n, generator=g)
+        Fg = F.cuda().requires_grad_(True)
+        out = collapse6to3(Fg)
+        _close(out, RC.collapse6to3(F.double()), f"general collapse c={c} n={n}")
+        G = torch.randn(out.shape, generator=g)
+        out.backward(G.cuda())
+        lhs = (RC.collapse6to3(F.double()) * G.double()).sum().item()
+        rhs = (F.double() * Fg.grad.double().cpu()).sum().item()
+        assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs)), (c, n, lhs, rhs)
+
+
+@pytest.mark.parametrize("kind", ["1d", "2d"])
+def test_ccn_per_graph_matches_reference(golden, kind):
+    """The drop-in forward(X, adj) + MSE backward, graph by graph, as scripts/train_ccn.py runs it."""
+    z = golden("ccn")
+    for k, (X, adj, t) in enumerate(ccn_graphs(z)):
+        if f"{kind}_out_{k}" not in z:
+            continue
+        net, _ = ccn_params(kind, k)
+        net = net.cuda()
+        Xr = X.cuda().requires_grad_(True)
+        out = net(Xr, adj.cuda())
+        assert out.shape == (1,)
+        loss = torch.nn.MSELoss()(out, t[0].view(1).cuda())
+        loss.backward()
+        _close(out, z[f"{kind}_out_{k}"], f"{kind} out {k}")
+        _close(loss.view(1), np.array([z[f"{kind}_loss_{k}"]]), f"{kind} loss {k}")
+        _grad_close(Xr.grad, z[f"{kind}_dX_{k}"], f"{kind} dX {k}")
+        for n, p in net.named_parameters():
+            _grad_close(p.grad, z[f"{kind}_grad_{k}.{n}"], f"{kind} grad {k} {n}")
+
+
+@pytest.mark.parametrize("order", [1, 2])
+def test_ccn_batched_matches_oracle(order):
+    """A padded batch of QM9-shape + SBM graphs in one call vs the fp64 oracle per graph."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_1D, CCN_2D
+    from oracle import ref_ccn as RC
+    graphs = dg.qm9_shape_dataset(24, seed=71) + dg.sbm_dataset(3, n=20, seed=72)
+    graphs = [(X, A + torch.eye(A.shape[0]), t) for X, A, t in graphs]
+    f = graphs[0][0].shape[1]
+    sbm_f = graphs[-1][0].shape[1]
+    if sbm_f != f:
+        graphs = graphs[:24]
+    net = (CCN_1D if order == 1 else CCN_2D)(f, 2, 3, 3)
+    fu.det_init(net, 77)
+    p64 = {n: v.detach().double().clone().requires_grad_(True) for n, v in net.named_parameters()}
+    net = net.cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    Xr = X.clone().requires_grad_(True)
+    out = net.forward_batch(Xr, A, nb)
+    w = torch.randn(out.shape, generator=torch.Generator().manual_seed(3))
+    (out * w.cuda()).sum().backward()
+    for b, (x, a, _) in enumerate(graphs):
+        xr = x.double().requires_grad_(True)
+        ref = RC.ccn_forward(p64, xr, a.double(), order, 3)
+        _close(out[b], ref, f"order {order} graph {b}")
+        (ref * w[b].double()).sum().backward()
+        n = x.shape[0]
+        _grad_close(Xr.grad[b, :n], xr.grad, f"dX graph {b}")
+        assert Xr.grad[b, n:].abs().max().item() == 0.0 if n < X.shape[1] else True
+    for n, p in net.named_parameters():
+        _grad_close(p.grad, p64[n].grad, f"grad {n}")
+
+
+def test_ccn_batched_equals_per_graph():
+    """Packing is invisible: forward_batch rows equal the single-graph forward."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_2D
+    graphs = [(X, A + torch.eye(A.shape[0]), t) for X, A, t in dg.qm9_shape_dataset(10, seed=81)]
+    net = CCN_2D(5, 1, 2, 2).cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    with torch.no_grad():
+        ob = net.forward_batch(X, A, nb)
+        for b, (x, a, _) in enumerate(graphs):
+            o = net(x.cuda(), a.cuda())
+            _close(o, ob[b].cpu(), f"graph {b}", rel=1e-6)
+
+
+def test_ccn_missing_self_loop_raises():
+    from models.compnets.model_ccn import CCN_1D
+    net = CCN_1D(5, 1, 2, 2).cuda()
+    A = torch.zeros(4, 4)
+    A[0, 1] = A[1, 0] = 1.0
+    with pytest.raises(RuntimeError, match="self loop"):
+        net(torch.randn(4, 5).cuda(), A.cuda())

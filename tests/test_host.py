@@ -179,3 +179,45 @@ def test_gpu_ops_refuse_cpu_tensors():
     m = GNN_lg(0, 8, 3, 5, 1, 1, 2)
     with pytest.raises(RuntimeError, match="GPU"):
         m([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+
+
+def test_compnet_utils_1d_surface_matches_reference(golden):
+    """CompnetUtils (functions/utils_ccn.py drop-in) reproduces the reference's 1-D pipeline and chi matrices."""
+    import fixture_util as fu
+    from functions.utils_ccn import CompnetUtils
+    from test_oracle import ccn_graphs, ccn_params
+    z = golden("ccn")
+    for k, (X, adj, _) in enumerate(ccn_graphs(z)):
+        net, _ = ccn_params("1d", k)
+        u = CompnetUtils(False)
+        F = [u.get_F0_1D(X, adj)]
+        for l in range(2):
+            F.append(u.update_F_1D(F[-1], net._modules[f"w{l + 1}"]))
+        out = net.fc(torch.cat([sum(v.sum(0) for v in f) for f in F], 0))
+        assert torch.allclose(out.detach(), torch.from_numpy(z[f"1d_out_{k}"]), rtol=1e-5, atol=1e-5), k
+        pos = []
+        for i in range(adj.shape[0]):
+            for j in range(adj.shape[0]):
+                if adj[i, j] > 0:
+                    chi = u.chis[i][j]
+                    pos += [int(r.nonzero()[0]) if r.any() else -1 for r in chi]
+        assert np.array_equal(np.array(pos), z[f"pos_{k}"]), k
+        assert fu is not None
+
+
+def test_ccn_state_dict_layout():
+    from models.compnets.model_ccn import CCN_1D, CCN_2D
+    s1 = {k: tuple(v.shape) for k, v in CCN_1D(5, 1, 2, 2).state_dict().items()}
+    s2 = {k: tuple(v.shape) for k, v in CCN_2D(5, 1, 2, 2).state_dict().items()}
+    assert s1 == {"w1.weight": (2, 10), "w1.bias": (2,), "w2.weight": (2, 4), "w2.bias": (2,),
+                  "fc.weight": (1, 9), "fc.bias": (1,)}
+    assert s2 == {"w1.weight": (2, 90), "w1.bias": (2,), "w2.weight": (2, 36), "w2.bias": (2,),
+                  "fc.weight": (1, 9), "fc.bias": (1,)}
+    assert CCN_2D(5, 1, 3, 2).hidden_size == 2
+
+
+def test_ccn_cpu_tensors_raise():
+    from models.compnets.model_ccn import CCN_1D
+    net = CCN_1D(5, 1, 2, 2)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        net(torch.zeros(3, 5), torch.eye(3))

@@ -107,3 +107,60 @@ def test_oracle_gnn_simple_matches_reference(golden):
         if k.startswith("grad32."):
             g = p[k[7:]].grad.numpy()
             assert np.all(np.abs(g - z[k]) <= 1e-4 * gmax + 1e-5 * np.abs(z[k])), k
+
+
+# --------------------------------------------------------------------------- CCN
+def ccn_params(kind, k, dtype=torch.float32):
+    """Fixture weights: det_init(net, 300 + k) on a CCN of the fixtures' shape (5 -> 1, h=2, L=2)."""
+    from models.compnets.model_ccn import CCN_1D, CCN_2D
+    net = (CCN_1D if kind == "1d" else CCN_2D)(5, 1, 2, 2, False)
+    fu.det_init(net, 300 + k)
+    return net, {n: v.detach().to(dtype).clone() for n, v in net.named_parameters()}
+
+
+def ccn_graphs(z):
+    return [(X, A + torch.eye(A.shape[0]), t) for X, A, t in fu.unpack_graphs(z)]
+
+
+def test_oracle_collapse6to3_matches_reference(golden):
+    from oracle import ref_ccn as RC
+    z = golden("ccn")
+    for d in range(1, 7):
+        T = torch.from_numpy(z[f"c6_T_{d}"]).double()
+        H = T.permute(3, 0, 1, 2).unsqueeze(4).unsqueeze(5) * torch.eye(d, dtype=torch.float64)
+        got = RC.collapse6to3(H)
+        ref = torch.from_numpy(z[f"c6_out_{d}"]).double()
+        assert torch.allclose(got, ref, rtol=1e-5, atol=1e-5), d
+
+
+def test_oracle_ccn_receptive_fields_bit_exact(golden):
+    from oracle import ref_ccn as RC
+    z = golden("ccn")
+    for k, (X, adj, _) in enumerate(ccn_graphs(z)):
+        nbrs = RC.receptive_fields(adj)
+        assert np.array_equal(np.array([len(v) for v in nbrs]), z[f"deg_{k}"]), k
+        assert np.array_equal(np.concatenate([np.array(v) for v in nbrs]), z[f"nbr_{k}"]), k
+        pos = [q for i in range(len(nbrs)) for j in nbrs[i] for q in RC.positions(nbrs, i, j)]
+        assert np.array_equal(np.array(pos), z[f"pos_{k}"]), k
+
+
+@pytest.mark.parametrize("kind", ["1d", "2d"])
+def test_oracle_ccn_matches_reference(golden, kind):
+    from oracle import ref_ccn as RC
+    z = golden("ccn")
+    order = 1 if kind == "1d" else 2
+    for k, (X, adj, t) in enumerate(ccn_graphs(z)):
+        if f"{kind}_out_{k}" not in z:
+            continue
+        _, p = ccn_params(kind, k)
+        p = {n: v.requires_grad_(True) for n, v in p.items()}
+        Xr = X.clone().requires_grad_(True)
+        out = RC.ccn_forward(p, Xr, adj, order, 2)
+        loss = torch.nn.MSELoss()(out, t[0].view(1))
+        loss.backward()
+        ref = torch.from_numpy(z[f"{kind}_out_{k}"])
+        assert torch.allclose(out.detach(), ref, rtol=1e-5, atol=1e-5), (k, out, ref)
+        assert torch.allclose(Xr.grad, torch.from_numpy(z[f"{kind}_dX_{k}"]), rtol=1e-4, atol=1e-5), k
+        for n, v in p.items():
+            g = torch.from_numpy(z[f"{kind}_grad_{k}.{n}"])
+            assert torch.allclose(v.grad, g, rtol=1e-4, atol=1e-5 * max(1.0, g.abs().max().item())), (k, n)
