@@ -122,11 +122,11 @@ def main():
 
     dominant = None
     if args.roofline:
-        with KernelTimer(4096, range(10)) as tm:
+        with KernelTimer(4096, range(RF.N_CLASSES)) as tm:
             for _ in range(2):
                 step()
             torch.cuda.synchronize()
-            per = {k: tm.elapsed(k) for k in range(10)}
+            per = {k: tm.elapsed(k) for k in range(RF.N_CLASSES)}
         tm.close()
         dominant = max(per, key=lambda k: per[k][0])
         launches_per_step = per[dominant][1] // 2

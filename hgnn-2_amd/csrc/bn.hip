@@ -286,37 +286,62 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s) {
 // y[b, o] = sum_{n < N_b} sum_k A[n, k] fcw[o, k] + Nmax * fcb[o]
 // The reference sums fc(x1) over all Nmax padded positions; padded positions
 // have x1 = 0, so each contributes exactly fc.bias (layers_mnb.py:92, 386).
-__global__ void __launch_bounds__(256) k_readout_fwd(const float* __restrict__ A, int k,
-                                                     const int* __restrict__ node_off, int nmax,
-                                                     const float* __restrict__ fcw,
-                                                     const float* __restrict__ fcb, int dim_out,
-                                                     float* __restrict__ colsum,
-                                                     float* __restrict__ out) {
-    __shared__ double red[4];
+// One 1024-thread block per graph, a thread per column; the row loop issues 8
+// independent loads per round (the serial walk was latency-bound: 27 us / step).
+constexpr int RO_THREADS = 1024;
+
+__global__ void __launch_bounds__(RO_THREADS) k_readout_fwd(const float* __restrict__ A, int k,
+                                                            const int* __restrict__ node_off, int nmax,
+                                                            const float* __restrict__ fcw,
+                                                            const float* __restrict__ fcb, int dim_out,
+                                                            float* __restrict__ colsum,
+                                                            float* __restrict__ out) {
+    __shared__ double red[RO_THREADS / 64];
     const int b = blockIdx.x;
     const int r0 = node_off[b], r1 = node_off[b + 1];
+    // fp64 column sums: the reference sums per-position dot products with
+    // torch.sum (pairwise); a plain fp32 running sum would be less accurate
+    double part0 = 0.0;
+    for (int kk = threadIdx.x; kk < k; kk += RO_THREADS) {
+        const float* col = A + kk;
+        double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int r = r0;
+        for (; r + 8 <= r1; r += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = col[(long long)(r + u) * k];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) c[u] += (double)v[u];
+        }
+        for (int u = 0; r < r1; ++r, ++u) c[u] += (double)col[(long long)r * k];
+        const double cs = ((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]));
+        colsum[(long long)b * k + kk] = (float)cs;
+        if (dim_out > 0) part0 += cs * (double)fcw[kk];
+    }
+    __syncthreads();
     for (int o = 0; o < dim_out; ++o) {
         double part = 0.0;
-        for (int kk = threadIdx.x; kk < k; kk += blockDim.x) {
-            double cs = 0.0;
-            if (o == 0) {
-                // fp64 column sum: the reference sums per-position dot products with
-                // torch.sum (pairwise), a plain fp32 running sum would be less accurate
-                for (int r = r0; r < r1; ++r) cs += (double)A[(long long)r * k + kk];
-                colsum[(long long)b * k + kk] = (float)cs;
-            } else {
-                cs = (double)colsum[(long long)b * k + kk];
-            }
-            part += cs * (double)fcw[(long long)o * k + kk];
+        if (o == 0) {
+            part = part0;
+        } else {
+            for (int kk = threadIdx.x; kk < k; kk += RO_THREADS)
+                part += (double)colsum[(long long)b * k + kk] * (double)fcw[(long long)o * k + kk];
         }
-        const double t = block_sum_d(part, red);
-        if (threadIdx.x == 0) out[b * dim_out + o] = (float)(t + (double)nmax * (double)fcb[o]);
+        part = wave_sum_d(part);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = part;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0.0;
+            for (int w = 0; w < RO_THREADS / 64; ++w) t += red[w];
+            out[b * dim_out + o] = (float)(t + (double)nmax * (double)fcb[o]);
+        }
+        __syncthreads();
     }
 }
 
 int launch_readout_fwd(const float* a, int k, const int* node_off, int bs, int nmax, const float* fcw,
                        const float* fcb, int dim_out, float* colsum, float* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_readout_fwd, dim3(bs), dim3(256), 0, s, a, k, node_off, nmax, fcw, fcb, dim_out,
+    hipLaunchKernelGGL(k_readout_fwd, dim3(bs), dim3(RO_THREADS), 0, s, a, k, node_off, nmax, fcw, fcb, dim_out,
                        colsum, out);
     HGNN_LAUNCH_CHECK();
     return 0;

@@ -1,0 +1,435 @@
+// GEMM v3 ("NT"): C[M][N] = A[M][K] . B[N][K]^T with both operands k-contiguous,
+// fp32 MFMA v_mfma_f32_32x32x2_f32.
+//
+// Forward:  Y[rows][2d]  = Agg[rows][kp] . Wcat[2d][kp]^T  (+ bias, ReLU half, BN partials)
+// dA:       dA[rows][K]  = dY[rows][2d]  . WT[K][2d]^T
+// Both operands are staged global -> registers -> LDS with float4 loads into
+// k-contiguous LDS rows (stride BK + 4 floats: conflict-free ds_read_b128), so
+// no transpose happens anywhere.  The k order inside a BK tile is permuted:
+// MFMA step s contracts k = s (lanes 0-31) and k = BK/2 + s (lanes 32-63); the
+// same permutation on A and B leaves the sum unchanged, and one ds_read_b128
+// per operand then feeds 4 consecutive MFMA steps.  Measured on the box
+// (tools/gemm_lab.hip) against v2 on the config-2 shapes: node fwd 57 -> 30 us,
+// edge fwd 79 -> 51 us, edge dA 64 -> 48 us.
+#include "kernels.h"
+
+namespace hgnn {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+enum { E3_FWD = 0, E3_STORE = 1 };
+
+struct G3 {
+    const float* a;
+    int lda;
+    const float* b;
+    int ldb;
+    int m_cap;
+    const int* m_valid;
+    int k;
+    int n;
+    float* c;
+    int ldc;
+    const float* bias;
+    int relu_from;
+    float* bn_part;  // [ceil(m_cap / 64)][n][3] (count, mean, M2)
+};
+
+template <int BM, int BN, int BK, int WGM, int WGN, int EPI>
+__global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 32, AN = TN / 32;
+    constexpr int LDK = BK + 4;
+    constexpr int AF4 = BM * BK / 4 / NT, BF4 = BN * BK / 4 / NT;
+    static_assert(AF4 >= 1 && BF4 >= 1 && AM >= 1 && AN >= 1, "tile shape");
+    static_assert(EPI != E3_FWD || (BM == 64 && WGM == 2), "BN partials are per 64-row tile");
+    __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv / WGN, wn = wv % WGN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const int Mv = p.m_valid ? *p.m_valid : p.m_cap;
+    if (m0 >= Mv) return;
+    const int K = p.k, N = p.n;
+
+    // The k tail (K % 4 != 0: the padding columns of the aggregate) is zeroed when the
+    // staged registers are written to LDS, not right after the load: masking there
+    // makes the compiler wait for every load at once (vmcnt(0)) and kills the prefetch.
+    float4 ra[AF4], rb[BF4];
+    auto mask_tail = [](float4 v, int gk, int kend) {
+        if (gk + 3 >= kend) {
+            if (gk >= kend) v.x = 0.f;
+            if (gk + 1 >= kend) v.y = 0.f;
+            if (gk + 2 >= kend) v.z = 0.f;
+            v.w = 0.f;
+        }
+        return v;
+    };
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < AF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            const int gm = m0 + row, gk = k0 + kq;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gm < Mv && gk < K) v = *reinterpret_cast<const float4*>(p.a + (long long)gm * p.lda + gk);
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            const int gn = n0 + row, gk = k0 + kq;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gn < N && gk < K) v = *reinterpret_cast<const float4*>(p.b + (long long)gn * p.ldb + gk);
+            rb[i] = v;
+        }
+    };
+    auto store = [&](int buf, int k0) {
+        const bool tail = k0 + BK > K;
+#pragma unroll
+        for (int i = 0; i < AF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            *reinterpret_cast<float4*>(&As[buf][row * LDK + kq]) = tail ? mask_tail(ra[i], k0 + kq, K) : ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            *reinterpret_cast<float4*>(&Bs[buf][row * LDK + kq]) = tail ? mask_tail(rb[i], k0 + kq, K) : rb[i];
+        }
+    };
+
+    f32x16 acc[AM][AN];
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nt = ceil_div(K, BK);
+    const int h = lane >> 5, l31 = lane & 31;
+    load(0);
+    store(0, 0);
+    __syncthreads();
+    if (nt > 1) load(BK);
+    for (int t = 0; t < nt; ++t) {
+        const int buf = t & 1;
+        const float* as = &As[buf][(wm * TM + l31) * LDK + h * (BK / 2)];
+        const float* bs = &Bs[buf][(wn * TN + l31) * LDK + h * (BK / 2)];
+#pragma unroll
+        for (int g = 0; g < BK / 8; ++g) {
+            float4 a[AM], b[AN];
+#pragma unroll
+            for (int i = 0; i < AM; ++i) a[i] = *reinterpret_cast<const float4*>(as + i * 32 * LDK + 4 * g);
+#pragma unroll
+            for (int j = 0; j < AN; ++j) b[j] = *reinterpret_cast<const float4*>(bs + j * 32 * LDK + 4 * g);
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+#pragma unroll
+                for (int j = 0; j < AN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                }
+        }
+        if (t + 1 < nt) {
+            store(buf ^ 1, (t + 1) * BK);
+            if (t + 2 < nt) load((t + 2) * BK);
+        }
+        __syncthreads();
+    }
+
+    // C/D layout of the 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    if constexpr (EPI == E3_FWD) {
+        float* red = &As[0][0];  // [2][BN] sums + [2][BN] counts, then [2][BN] M2
+        float s[AN];
+        int cnt[AN];
+#pragma unroll
+        for (int j = 0; j < AN; ++j) {
+            const int gn = n0 + wn * TN + j * 32 + l31;
+            const float bias = gn < N ? p.bias[gn] : 0.f;
+            const bool relu = gn >= p.relu_from;
+            s[j] = 0.f;
+            cnt[j] = 0;
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int gm = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    float v = acc[i][j][r] + bias;
+                    if (relu) v = v < 0.f ? 0.f : v;
+                    acc[i][j][r] = v;
+                    if (gm < Mv) {
+                        if (gn < N) p.c[(long long)gm * p.ldc + gn] = v;
+                        s[j] += v;
+                        ++cnt[j];
+                    }
+                }
+        }
+        if (p.bn_part) {
+            float mean[AN];
+#pragma unroll
+            for (int j = 0; j < AN; ++j) {
+                s[j] += __shfl_xor(s[j], 32, 64);
+                cnt[j] += __shfl_xor(cnt[j], 32, 64);
+                const int col = wn * TN + j * 32 + l31;
+                if (lane < 32) {
+                    red[wm * BN + col] = s[j];
+                    red[2 * BN + wm * BN + col] = (float)cnt[j];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < AN; ++j) {
+                const int col = wn * TN + j * 32 + l31;
+                const float S = red[col] + red[BN + col];
+                const float C = red[2 * BN + col] + red[3 * BN + col];
+                mean[j] = C > 0.f ? S / C : 0.f;
+                cnt[j] = (int)C;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < AN; ++j) {
+                float q = 0.f;
+#pragma unroll
+                for (int i = 0; i < AM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int gm = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (gm < Mv) {
+                            const float dl = acc[i][j][r] - mean[j];
+                            q = fmaf(dl, dl, q);
+                        }
+                    }
+                q += __shfl_xor(q, 32, 64);
+                const int col = wn * TN + j * 32 + l31;
+                if (lane < 32) red[wm * BN + col] = q;
+            }
+            __syncthreads();
+            if (wm == 0 && lane < 32) {
+#pragma unroll
+                for (int j = 0; j < AN; ++j) {
+                    const int col = wn * TN + j * 32 + l31;
+                    const int gn = n0 + col;
+                    if (gn < N) {
+                        float* pp = p.bn_part + ((long long)blockIdx.x * N + gn) * 3;
+                        pp[0] = (float)cnt[j];
+                        pp[1] = mean[j];
+                        pp[2] = red[col] + red[BN + col];
+                    }
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int j = 0; j < AN; ++j) {
+                const int gn = n0 + wn * TN + j * 32 + l31;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int gm = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (gm < Mv && gn < N) p.c[(long long)gm * p.ldc + gn] = acc[i][j][r];
+                }
+            }
+    }
+}
+
+// dW ("TN"): slabs[z][m][n] = sum_{r in chunk z} A[r][m] B[r][n], with A = dY [R][2d] and
+// B = the saved aggregate [R][kp].  Both operands are reduction-major, so LDS keeps
+// the natural [k][m] image (float4 copies) and fragments are ds_read_b32, with the
+// same k permutation and a one-step register prefetch of the next fragments.
+// Measured (tools/gemm_lab.hip, config-2 shapes): edge 78 -> 41 us, node 37.5 -> 21 us vs v2.
+template <int BM, int BN, int BK, int WGM, int WGN>
+__global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __restrict__ A, int lda,
+                                                             const float* __restrict__ B, int ldb,
+                                                             float* __restrict__ slabs, int M, int N,
+                                                             const int* __restrict__ r_valid, int kchunk) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 32, AN = TN / 32;
+    constexpr int PA = BM + 4, PB = BN + 4;
+    constexpr int AF4 = BM * BK / 4 / NT, BF4 = BN * BK / 4 / NT;
+    static_assert(AF4 >= 1 && BF4 >= 1 && AM >= 1 && AN >= 1, "tile shape");
+    static_assert(AF4 * 4 * NT == BM * BK && BF4 * 4 * NT == BN * BK, "staging must cover the tile");
+    __shared__ __attribute__((aligned(16))) float As[2][BK * PA];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BK * PB];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv / WGN, wn = wv % WGN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const int R = *r_valid;
+    const int kbeg = blockIdx.z * kchunk, kend = min(R, kbeg + kchunk);
+    if (kbeg >= kend) return;  // the reduce only sums the chunks that hold rows
+    float4 ra[AF4], rb[BF4];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < AF4; ++i) {
+            const int e = tid + i * NT, kr = e / (BM / 4), mq = (e % (BM / 4)) * 4;
+            const int gk = k0 + kr, gm = m0 + mq;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gk < kend && gm < M) v = *reinterpret_cast<const float4*>(A + (long long)gk * lda + gm);
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BF4; ++i) {
+            const int e = tid + i * NT, kr = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+            const int gk = k0 + kr, gn = n0 + nq;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gk < kend && gn < N) v = *reinterpret_cast<const float4*>(B + (long long)gk * ldb + gn);
+            rb[i] = v;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < AF4; ++i) {
+            const int e = tid + i * NT, kr = e / (BM / 4), mq = (e % (BM / 4)) * 4;
+            *reinterpret_cast<float4*>(&As[buf][kr * PA + mq]) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BF4; ++i) {
+            const int e = tid + i * NT, kr = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+            *reinterpret_cast<float4*>(&Bs[buf][kr * PB + nq]) = rb[i];
+        }
+    };
+    f32x16 acc[AM][AN];
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nt = ceil_div(kend - kbeg, BK);
+    const int h = lane >> 5, l31 = lane & 31;
+    load(kbeg);
+    store(0);
+    __syncthreads();
+    if (nt > 1) load(kbeg + BK);
+    for (int t = 0; t < nt; ++t) {
+        const int buf = t & 1;
+        const float* as = &As[buf][h * (BK / 2) * PA + wm * TM + l31];
+        const float* bs = &Bs[buf][h * (BK / 2) * PB + wn * TN + l31];
+        float fa[2][AM], fb[2][AN];
+#pragma unroll
+        for (int i = 0; i < AM; ++i) fa[0][i] = as[i * 32];
+#pragma unroll
+        for (int j = 0; j < AN; ++j) fb[0][j] = bs[j * 32];
+#pragma unroll
+        for (int st = 0; st < BK / 2; ++st) {
+            const int cur = st & 1, nxt = cur ^ 1;
+            if (st + 1 < BK / 2) {
+#pragma unroll
+                for (int i = 0; i < AM; ++i) fa[nxt][i] = as[(st + 1) * PA + i * 32];
+#pragma unroll
+                for (int j = 0; j < AN; ++j) fb[nxt][j] = bs[(st + 1) * PB + j * 32];
+            }
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+#pragma unroll
+                for (int j = 0; j < AN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
+        }
+        if (t + 1 < nt) {
+            store(buf ^ 1);
+            if (t + 2 < nt) load(kbeg + (t + 2) * BK);
+        }
+        __syncthreads();
+    }
+    float* out = slabs + (long long)blockIdx.z * M * N;
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j) {
+            const int gn = n0 + wn * TN + j * 32 + l31;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gm = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (gm < M && gn < N) out[(long long)gm * N + gn] = acc[i][j][r];
+            }
+        }
+}
+
+}  // namespace
+
+// Row chunk of the dW slabs: ~256 blocks of 128 x 128 output tiles, multiple of 32 rows.
+int dw3_kchunk(int r_cap, int o, int k) {
+    const int tiles = ceil_div(o, 128) * ceil_div(k, 128);
+    int chunks = 256 / (tiles > 0 ? tiles : 1);
+    if (chunks < 1) chunks = 1;
+    int kc = ceil_div(r_cap > 0 ? r_cap : 1, chunks);
+    kc = ceil_div(kc, 32) * 32;
+    return kc < 64 ? 64 : kc;
+}
+
+size_t dw3_slab_floats(int r_cap, int o, int k) {
+    return (size_t)ceil_div(r_cap > 0 ? r_cap : 1, dw3_kchunk(r_cap, o, k)) * o * k;
+}
+
+// slabs[z][o][k] = sum_{r in chunk z} dY[r, o] A[r, k]
+int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
+                    int kchunk, float* slabs, hipStream_t s) {
+    if (r_cap <= 0) return 0;
+    const int z = ceil_div(r_cap, kchunk);
+    hipLaunchKernelGGL((k_gemm3_tn<128, 128, 32, 4, 2>), dim3(ceil_div(o, 128), ceil_div(k, 128), z), dim3(512), 0, s,
+                       dy, lddy, a, lda, slabs, o, k, r_valid, kchunk);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+bool gemm3_ok(int lda, int ldb, int ldc, const void* a, const void* b) {
+    auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    return lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 && al(a) && al(b);
+}
+
+// Y[r, n] = A[r, :k] . Wc[n, :k] + bias[n]; ReLU on n >= relu_from; BN partials per 64-row tile.
+int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const float* wc, int ldw, int n,
+                     const float* bias, int relu_from, float* y, int ldy, float* bn_part, hipStream_t s) {
+    if (m_cap <= 0) return 0;
+    G3 p{};
+    p.a = a;
+    p.lda = lda;
+    p.b = wc;
+    p.ldb = ldw;
+    p.m_cap = m_cap;
+    p.m_valid = m_valid;
+    p.k = k;
+    p.n = n;
+    p.c = y;
+    p.ldc = ldy;
+    p.bias = bias;
+    p.relu_from = relu_from;
+    p.bn_part = bn_part;
+    if (n <= 64) {
+        hipLaunchKernelGGL((k_gemm3<64, 64, 32, 2, 2, E3_FWD>), dim3(ceil_div(m_cap, 64), ceil_div(n, 64)), dim3(256),
+                           0, s, p);
+    } else {
+        hipLaunchKernelGGL((k_gemm3<64, 128, 32, 2, 2, E3_FWD>), dim3(ceil_div(m_cap, 64), ceil_div(n, 128)),
+                           dim3(256), 0, s, p);
+    }
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// dA[r, j] = sum_o dY[r, o] WT[j, o]   (j < kout)
+int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, int o, const float* wt, int ldw,
+                    int kout, float* da, int ldda, hipStream_t s) {
+    if (m_cap <= 0) return 0;
+    G3 p{};
+    p.a = dy;
+    p.lda = lddy;
+    p.b = wt;
+    p.ldb = ldw;
+    p.m_cap = m_cap;
+    p.m_valid = m_valid;
+    p.k = o;
+    p.n = kout;
+    p.c = da;
+    p.ldc = ldda;
+    hipLaunchKernelGGL((k_gemm3<64, 128, 32, 2, 2, E3_STORE>), dim3(ceil_div(m_cap, 64), ceil_div(kout, 128)),
+                       dim3(256), 0, s, p);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // namespace hgnn

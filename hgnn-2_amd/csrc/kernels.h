@@ -160,6 +160,16 @@ struct RepackTable {
     int n, d;
 };
 int launch_repack(const RepackTable& t, hipStream_t s);
+// GEMM v3 (gemm3.hip): both operands k-contiguous ("NT"), used for the forward and dA.
+bool gemm3_ok(int lda, int ldb, int ldc, const void* a, const void* b);
+int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const float* wc, int ldw, int n,
+                     const float* bias, int relu_from, float* y, int ldy, float* bn_part, hipStream_t s);
+int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, int o, const float* wt, int ldw,
+                    int kout, float* da, int ldda, hipStream_t s);
+int dw3_kchunk(int r_cap, int o, int k);
+size_t dw3_slab_floats(int r_cap, int o, int k);
+int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
+                    int kchunk, float* slabs, hipStream_t s);
 int launch_gemm2_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const float* wt, int n,
                      const float* bias, int relu_from, float* y, int ldy, float* bn_part, hipStream_t s);
 int launch_gemm2_da(const float* dy, int lddy, const int* m_valid, int m_cap, int o, const float* w0,

@@ -231,7 +231,7 @@ Program build_program(const hgnn_net_config* c) {
             h.bc = B.take((size_t)P.c2 * sizeof(float));
         }
         max_da = std::max(max_da, (size_t)cap * h.kp);
-        max_slab = std::max(max_slab, P.v2 ? dw2_slab_floats(cap, P.c2, h.k) : gemm_dw_slab_floats(cap, P.c2, h.k));
+        max_slab = std::max(max_slab, P.v2 ? dw3_slab_floats(cap, P.c2, h.k) : gemm_dw_slab_floats(cap, P.c2, h.k));
         max_cap = std::max(max_cap, cap);
     }
     P.dbpart = B.take((size_t)bn_bwd_tiles(max_cap > 0 ? max_cap : 1) * P.c2 * sizeof(float));
@@ -372,9 +372,10 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
         TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
 
         if (P.v2) {
-            TL(HGNN_K_GEMM_FWD, launch_gemm2_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.k, at<float>(ws, h.wt), P.c2,
-                                                 at<float>(ws, h.bc), h.relu_from, at<float>(ws, P.feats[h.out].y),
-                                                 P.c2, c->training ? at<float>(ws, h.part) : nullptr, s));
+            TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.k, at<float>(ws, h.wc), h.kp,
+                                                 P.c2, at<float>(ws, h.bc), h.relu_from,
+                                                 at<float>(ws, P.feats[h.out].y), P.c2,
+                                                 c->training ? at<float>(ws, h.part) : nullptr, s));
         } else {
         GemmFwdArgs gf{};
         gf.a = at<float>(ws, h.a);
@@ -553,10 +554,10 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s));
 
         if (P.v2) {
-            const int kc = dw2_kchunk(cap, P.c2, h.k);
-            TL(HGNN_K_GEMM_DW, launch_gemm2_dw(at<float>(ws, P.dy), P.c2, at<float>(ws, h.a), h.kp, tot, cap, P.c2,
+            const int kc = dw3_kchunk(cap, P.c2, h.k);
+            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(at<float>(ws, P.dy), P.c2, at<float>(ws, h.a), h.kp, tot, cap, P.c2,
                                                h.k, kc, at<float>(ws, P.slabs), s));
-            TL(HGNN_K_GEMM_DW, launch_dw_reduce2(at<float>(ws, P.slabs), tot, kc, P.c2, h.k, P.d, grads[h.pw_lin],
+            TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, kc, P.c2, h.k, P.d, grads[h.pw_lin],
                                                  grads[h.pw_relu], at<float>(ws, P.dbpart), grads[h.pb_lin],
                                                  grads[h.pb_relu], s));
         } else {
@@ -583,8 +584,8 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         if (!ng && !np && !ndw) continue;
         float* da = at<float>(ws, P.da);
         if (P.v2) {
-            TL(HGNN_K_GEMM_DA, launch_gemm2_da(at<float>(ws, P.dy), P.c2, tot, cap, P.c2, at<float>(ws, h.wc),
-                                               at<float>(ws, h.wc), 1 << 30, h.kp, h.k, da, h.kp, s));
+            TL(HGNN_K_GEMM_DA, launch_gemm3_da(at<float>(ws, P.dy), P.c2, tot, cap, P.c2, at<float>(ws, h.wt), P.c2,
+                                               h.k, da, h.kp, s));
         } else {
         GemmDaArgs gd{};
         gd.dy = at<float>(ws, P.dy);

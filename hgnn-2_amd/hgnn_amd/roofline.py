@@ -14,8 +14,11 @@ from .net import expected_k
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_FP32_MFMA_TFS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak
 
-K_STRUCT, K_AGG_FWD, K_GEMM_FWD, K_BN_FWD, K_READOUT, K_BN_BWD, K_GEMM_DW, K_GEMM_DA, K_AGG_BWD, K_DW_DENSE = range(10)
-NAMES = ["struct", "agg_fwd", "gemm_fwd", "bn_fwd", "readout", "bn_bwd", "gemm_dw", "gemm_da", "agg_bwd", "dw_dense"]
+(K_STRUCT, K_AGG_FWD, K_GEMM_FWD, K_BN_FWD, K_READOUT, K_BN_BWD, K_GEMM_DW, K_GEMM_DA, K_AGG_BWD, K_DW_DENSE,
+ K_DW_REDUCE) = range(11)
+NAMES = ["struct", "agg_fwd", "gemm_fwd", "bn_fwd", "readout", "bn_bwd", "gemm_dw", "gemm_da", "agg_bwd", "dw_dense",
+         "dw_reduce"]
+N_CLASSES = len(NAMES)
 
 
 def batch_counts(W, WL, Pm, Pd, N_batch, E_batch):
@@ -63,8 +66,8 @@ def class_work(kcls, counts, order, f_in, d, n_layers, jt=3):
     elif kcls == K_GEMM_DW:
         for edge, k, cg, cp in halves:
             r = rows(edge)
-            fl += 2.0 * r * c2 * (k + 1)
-            by += 4.0 * (r * c2 + r * k + c2 * (k + 1))
+            fl += 2.0 * r * c2 * k
+            by += 4.0 * (r * c2 + r * k + c2 * k)
     elif kcls in (K_AGG_FWD, K_AGG_BWD):
         items = [(e, k, cg, cp) for e, k, cg, cp in halves] + [(False, k_last, c2, c2)]
         for edge, k, cg, cp in items:
