@@ -293,8 +293,9 @@ __global__ void __launch_bounds__(256) k_repack(RepackTable t) {
     for (long long e = (long long)blockIdx.y * blockDim.x + threadIdx.x; e < nt + nc + c2;
          e += (long long)gridDim.y * blockDim.x) {
         if (e < nt) {
-            const int k = (int)(e / c2), n = (int)(e % c2);
-            it.wt[e] = n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k];
+            // coalesced reads along k, scattered 4-byte writes (the L2 merges them)
+            const int n = (int)(e / K), k = (int)(e % K);
+            it.wt[(long long)k * c2 + n] = n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k];
         } else if (e < nt + nc) {
             const long long f = e - nt;
             const int n = (int)(f / kp), k = (int)(f % kp);
@@ -310,7 +311,7 @@ __global__ void __launch_bounds__(256) k_repack(RepackTable t) {
 
 int launch_repack(const RepackTable& t, hipStream_t s) {
     if (t.n <= 0) return 0;
-    hipLaunchKernelGGL(k_repack, dim3(t.n, 16), dim3(256), 0, s, t);
+    hipLaunchKernelGGL(k_repack, dim3(t.n, 96), dim3(256), 0, s, t);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

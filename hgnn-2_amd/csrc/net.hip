@@ -50,7 +50,7 @@ struct Program {
     size_t node_off = 0, edge_off = 0, totals = 0, err = 0;
     size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
     int entry_stride_w = 4;
-    size_t dy = 0, da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0;
+    size_t dy = 0, dy2 = 0, da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0, dbpart2 = 0;
     bool v2 = false;  // GEMM v2 path (2d % 4 == 0); gemm.hip otherwise
     size_t bytes = 0;
 };
@@ -235,10 +235,12 @@ Program build_program(const hgnn_net_config* c) {
         max_cap = std::max(max_cap, cap);
     }
     P.dbpart = B.take((size_t)bn_bwd_tiles(max_cap > 0 ? max_cap : 1) * P.c2 * sizeof(float));
+    P.dbpart2 = B.take((size_t)bn_bwd_tiles(max_cap > 0 ? max_cap : 1) * P.c2 * sizeof(float));
     P.a_last = B.take((size_t)P.cap_n * P.k_last * sizeof(float));
     P.colsum = B.take((size_t)c->bs * P.k_last * sizeof(float));
     max_da = std::max(max_da, (size_t)P.cap_n * P.k_last);
     P.dy = B.take((size_t)max_cap * P.c2 * sizeof(float));
+    P.dy2 = B.take((size_t)max_cap * P.c2 * sizeof(float));
     P.da = B.take(max_da * sizeof(float));
     P.slabs = B.take(max_slab * sizeof(float));
     P.bnb_part = B.take((size_t)bn_bwd_tiles(max_cap) * P.c2 * 4 * sizeof(float));
@@ -435,6 +437,42 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
     return 0;
 }
 
+// Side stream of the backward: the weight-gradient GEMM of a half (and its slab
+// reduction) only feeds the parameter grads, so it runs beside the dA -> dense dW
+// -> aggregation-backward chain of the same half.  Fork after the half's BN
+// backward, join before the next half's BN backward overwrites dY / the bias
+// partials, and once more at the end.  One non-blocking stream and a few events
+// per host thread and device, created on first use.
+struct SideStream {
+    int dev = -1;
+    hipStream_t s = nullptr;
+    hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
+};
+
+static int side_stream(SideStream** out) {
+    thread_local SideStream ss;
+    int dev = 0;
+    HGNN_HOST_CHECK(hipGetDevice(&dev));
+    if (ss.dev != dev) {
+        if (ss.s) {
+            (void)hipStreamDestroy(ss.s);
+            for (int i = 0; i < 2; ++i) {
+                (void)hipEventDestroy(ss.fork[i]);
+                (void)hipEventDestroy(ss.join[i]);
+            }
+        }
+        ss = SideStream{};
+        HGNN_HOST_CHECK(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) {
+            HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming));
+            HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming));
+        }
+        ss.dev = dev;
+    }
+    *out = &ss;
+    return 0;
+}
+
 int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float* const* prm, void* ws,
                  const float* dout, float* const* grads, float* dX, float* dW, hipStream_t s, Timer* tm) {
     const Program P = build_program(c);
@@ -528,10 +566,40 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         }
     }
 
-    for (int hi = (int)P.halves.size() - 1; hi >= 0; --hi) {
+    SideStream* side = nullptr;
+    if (P.v2) TRY(side_stream(&side));
+    // dY and the bias partials alternate between two buffers, so the side stream's
+    // dW of half i may still read its pair while the main stream runs half i+1.
+    bool pending[2] = {false, false};
+    int parity = 0;
+    auto fork_dw = [&](const Half& h, int cap, const int* tot, float* dyb, float* dbp) -> int {
+        const int kc = dw3_kchunk(cap, P.c2, h.k);
+        HGNN_HOST_CHECK(hipEventRecord(side->fork[parity], s));
+        HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, side->fork[parity], 0));
+        hipStream_t main_s = s;
+        s = side->s;  // TL records its timer events on the stream the kernel runs on
+        int r = 0;
+        do {
+            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(dyb, P.c2, at<float>(ws, h.a), h.kp, tot, cap, P.c2, h.k, kc,
+                                               at<float>(ws, P.slabs), s));
+            TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, kc, P.c2, h.k, P.d, grads[h.pw_lin],
+                                                   grads[h.pw_relu], dbp, grads[h.pb_lin], grads[h.pb_relu], s));
+            r = hipEventRecord(side->join[parity], s) == hipSuccess ? 0 : HGNN_ERR_HIP;
+        } while (0);
+        s = main_s;
+        pending[parity] = true;
+        return r;
+    };
+    for (int hi = (int)P.halves.size() - 1; hi >= 0; --hi, parity ^= 1) {
         const Half& h = P.halves[hi];
         const int cap = h.edge ? P.cap_e : P.cap_n;
         const int* tot = h.edge ? tot_e : tot_n;
+        float* dyb = at<float>(ws, parity ? P.dy2 : P.dy);
+        float* dbp = at<float>(ws, parity ? P.dbpart2 : P.dbpart);
+        if (pending[parity]) {  // the dW two halves back still reads this dY / bias-partial pair
+            HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[parity], 0));
+            pending[parity] = false;
+        }
         if (!init[h.out]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[h.out].grad), 0,
                                                           (size_t)cap * P.c2 * sizeof(float), s));
         BnBwdArgs bb{};
@@ -547,59 +615,58 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         bb.training = c->training;
         bb.part = at<float>(ws, P.bnb_part);
         bb.sums = at<float>(ws, P.bnb_sums);
-        bb.dy = at<float>(ws, P.dy);
+        bb.dy = dyb;
         bb.dw = grads[h.pbn_w];
         bb.db = grads[h.pbn_b];
-        bb.dbpart = P.v2 ? at<float>(ws, P.dbpart) : nullptr;
+        bb.dbpart = P.v2 ? dbp : nullptr;
         TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s));
 
-        if (P.v2) {
-            const int kc = dw3_kchunk(cap, P.c2, h.k);
-            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(at<float>(ws, P.dy), P.c2, at<float>(ws, h.a), h.kp, tot, cap, P.c2,
-                                               h.k, kc, at<float>(ws, P.slabs), s));
-            TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, kc, P.c2, h.k, P.d, grads[h.pw_lin],
-                                                 grads[h.pw_relu], at<float>(ws, P.dbpart), grads[h.pb_lin],
-                                                 grads[h.pb_relu], s));
-        } else {
-        GemmDwArgs gw{};
-        gw.dy = at<float>(ws, P.dy);
-        gw.lddy = P.c2;
-        gw.a = at<float>(ws, h.a);
-        gw.lda = h.k;
-        gw.r_valid = tot;
-        gw.r_cap = cap;
-        gw.o = P.c2;
-        gw.k = h.k;
-        gw.split = P.d;
-        gw.slabs = at<float>(ws, P.slabs);
-        gw.dw0 = grads[h.pw_lin];
-        gw.dw1 = grads[h.pw_relu];
-        gw.db0 = grads[h.pb_lin];
-        gw.db1 = grads[h.pb_relu];
-        TL(HGNN_K_GEMM_DW, launch_gemm_dw(gw, s));
+        if (!P.v2) {
+            GemmDwArgs gw{};
+            gw.dy = dyb;
+            gw.lddy = P.c2;
+            gw.a = at<float>(ws, h.a);
+            gw.lda = h.k;
+            gw.r_valid = tot;
+            gw.r_cap = cap;
+            gw.o = P.c2;
+            gw.k = h.k;
+            gw.split = P.d;
+            gw.slabs = at<float>(ws, P.slabs);
+            gw.dw0 = grads[h.pw_lin];
+            gw.dw1 = grads[h.pw_relu];
+            gw.db0 = grads[h.pb_lin];
+            gw.db1 = grads[h.pb_relu];
+            TL(HGNN_K_GEMM_DW, launch_gemm_dw(gw, s));
         }
 
         const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
         const bool ndw = need_dw && !h.edge;
-        if (!ng && !np && !ndw) continue;
+        if (!ng && !np && !ndw) {
+            if (P.v2) TRY(fork_dw(h, cap, tot, dyb, dbp));
+            continue;
+        }
         float* da = at<float>(ws, P.da);
         if (P.v2) {
-            TL(HGNN_K_GEMM_DA, launch_gemm3_da(at<float>(ws, P.dy), P.c2, tot, cap, P.c2, at<float>(ws, h.wt), P.c2,
-                                               h.k, da, h.kp, s));
+            TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2, tot, cap, P.c2, at<float>(ws, h.wt), P.c2, h.k, da, h.kp,
+                                               s));
+            // dW starts once dA is done: two MFMA GEMMs side by side only slow each other,
+            // dW beside the latency-bound dense-dW / aggregation-backward kernels does not
+            TRY(fork_dw(h, cap, tot, dyb, dbp));
         } else {
-        GemmDaArgs gd{};
-        gd.dy = at<float>(ws, P.dy);
-        gd.lddy = P.c2;
-        gd.m_valid = tot;
-        gd.m_cap = cap;
-        gd.o = P.c2;
-        gd.w0 = prm[h.pw_lin];
-        gd.w1 = prm[h.pw_relu];
-        gd.split = P.d;
-        gd.k = h.k;
-        gd.da = da;
-        gd.ldda = h.k;
-        TL(HGNN_K_GEMM_DA, launch_gemm_da(gd, s));
+            GemmDaArgs gd{};
+            gd.dy = dyb;
+            gd.lddy = P.c2;
+            gd.m_valid = tot;
+            gd.m_cap = cap;
+            gd.o = P.c2;
+            gd.w0 = prm[h.pw_lin];
+            gd.w1 = prm[h.pw_relu];
+            gd.split = P.d;
+            gd.k = h.k;
+            gd.da = da;
+            gd.ldda = h.k;
+            TL(HGNN_K_GEMM_DA, launch_gemm_da(gd, s));
         }
         if (ndw) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, da, h.kp, false, 1));
         if (ng) {
@@ -637,6 +704,8 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
             init[h.pin] = 1;
         }
     }
+    for (int p = 0; p < 2; ++p)
+        if (pending[p]) HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[p], 0));
     if (c->need_dx) {
         if (!dX) return HGNN_ERR_ARG;
         if (!init[0]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[0].grad), 0,
