@@ -72,6 +72,21 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, int C, int lane
     }
 }
 
+// Entry lists are fetched lane-parallel (lane e holds entry e of a 64-entry chunk)
+// and broadcast with readlane, and U feature rows are loaded before any is used,
+// so a row of n entries costs ~n/U dependent memory round trips instead of 2n.
+constexpr int AGG_U = 4;
+
+__device__ __forceinline__ float4 lane_entry(const float* __restrict__ entries, int stride, int start, int n, int lane) {
+    // W / WL entries: (col, v_0..v_{J-1}) padded to `stride` floats; P entries: (col, pm, pd, -)
+    if (lane < n) return *reinterpret_cast<const float4*>(entries + (long long)(start + lane) * stride);
+    return make_float4(__int_as_float(0), 0.f, 0.f, 0.f);
+}
+
+__device__ __forceinline__ float bcast(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
 template <int JT, int CG, int CP>
 __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
     const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -86,18 +101,38 @@ __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
             for (int i = 0; i < CG; ++i) acc[j][i] = 0.f;
         const RowInfo ri = a.g.rows[r];
         const int stride = a.g.stride;
-        for (int e = 0; e < ri.count; ++e) {
-            const float* ent = a.g.entries + (long long)(ri.start + e) * stride;
-            const int col = __float_as_int(ent[0]);
-            float v[JT];
+        for (int e0 = 0; e0 < ri.count; e0 += 64) {
+            const int n = min(64, ri.count - e0);
+            // JT <= 3: one float4 per entry; larger JT reads the extra coefficients below
+            const float4 me = lane_entry(a.g.entries, stride, ri.start + e0, n, lane);
+            float mx[JT > 3 ? JT - 3 : 1];
+            if constexpr (JT > 3) {
 #pragma unroll
-            for (int j = 0; j < JT; ++j) v[j] = ent[1 + j];
-            float x[CG];
-            load_row<CG>(a.xg + (long long)col * a.cg, a.cg, lane, x);
+                for (int j = 3; j < JT; ++j)
+                    mx[j - 3] = lane < n ? a.g.entries[(long long)(ri.start + e0 + lane) * stride + 1 + j] : 0.f;
+            }
+            for (int e = 0; e < n; e += AGG_U) {
+                float x[AGG_U][CG];
+                float v[AGG_U][JT];
 #pragma unroll
-            for (int j = 0; j < JT; ++j)
+                for (int u = 0; u < AGG_U; ++u) {
+                    const int eu = min(e + u, n - 1);
+                    const int col = __builtin_amdgcn_readlane(__float_as_int(me.x), eu);
+                    const bool live = e + u < n;
+                    v[u][0] = live ? bcast(me.y, eu) : 0.f;
+                    if constexpr (JT > 1) v[u][1] = live ? bcast(me.z, eu) : 0.f;
+                    if constexpr (JT > 2) v[u][2] = live ? bcast(me.w, eu) : 0.f;
 #pragma unroll
-                for (int i = 0; i < CG; ++i) acc[j][i] = fmaf(v[j], x[i], acc[j][i]);
+                    for (int j = 3; j < JT; ++j) v[u][j] = live ? bcast(mx[j - 3], eu) : 0.f;
+                    load_row<CG>(a.xg + (long long)col * a.cg, a.cg, lane, x[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u)
+#pragma unroll
+                    for (int j = 0; j < JT; ++j)
+#pragma unroll
+                        for (int i = 0; i < CG; ++i) acc[j][i] = fmaf(v[u][j], x[u][i], acc[j][i]);
+            }
         }
 #pragma unroll
         for (int j = 0; j < JT; ++j) store_row<CG>(o + j * a.cg, a.cg, lane, acc[j]);
@@ -107,15 +142,27 @@ __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
 #pragma unroll
         for (int i = 0; i < CP; ++i) am[i] = ad[i] = 0.f;
         const RowInfo ri = a.p.rows[r];
-        for (int e = 0; e < ri.count; ++e) {
-            const float4 ent = *reinterpret_cast<const float4*>(a.p.entries + (long long)(ri.start + e) * 4);
-            const int col = __float_as_int(ent.x);
-            float x[CP];
-            load_row<CP>(a.xp + (long long)col * a.cp, a.cp, lane, x);
+        for (int e0 = 0; e0 < ri.count; e0 += 64) {
+            const int n = min(64, ri.count - e0);
+            const float4 me = lane_entry(a.p.entries, 4, ri.start + e0, n, lane);
+            for (int e = 0; e < n; e += AGG_U) {
+                float x[AGG_U][CP], vm[AGG_U], vd[AGG_U];
 #pragma unroll
-            for (int i = 0; i < CP; ++i) {
-                am[i] = fmaf(ent.y, x[i], am[i]);
-                ad[i] = fmaf(ent.z, x[i], ad[i]);
+                for (int u = 0; u < AGG_U; ++u) {
+                    const int eu = min(e + u, n - 1);
+                    const int col = __builtin_amdgcn_readlane(__float_as_int(me.x), eu);
+                    const bool live = e + u < n;
+                    vm[u] = live ? bcast(me.y, eu) : 0.f;
+                    vd[u] = live ? bcast(me.z, eu) : 0.f;
+                    load_row<CP>(a.xp + (long long)col * a.cp, a.cp, lane, x[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u)
+#pragma unroll
+                    for (int i = 0; i < CP; ++i) {
+                        am[i] = fmaf(vm[u], x[u][i], am[i]);
+                        ad[i] = fmaf(vd[u], x[u][i], ad[i]);
+                    }
             }
         }
         const int base = JT * a.cg;
@@ -185,31 +232,64 @@ __global__ void __launch_bounds__(256) k_agg_bwd(AggBwdArgs a) {
     if constexpr (HG) {
         const RowInfo ri = a.g.rows[r];
         const int stride = a.g.stride;
-        for (int e = 0; e < ri.count; ++e) {
-            const float* ent = a.g.entries + (long long)(ri.start + e) * stride;
-            const int col = __float_as_int(ent[0]);
-            const float* src = a.ing + (long long)col * a.ldg + a.gofs;
+        constexpr int UB = 2;  // entries in flight (x JT slices each)
+        for (int e0 = 0; e0 < ri.count; e0 += 64) {
+            const int n = min(64, ri.count - e0);
+            const float4 me = lane_entry(a.g.entries, stride, ri.start + e0, n, lane);
+            float mx[JT > 3 ? JT - 3 : 1];
+            if constexpr (JT > 3) {
 #pragma unroll
-            for (int j = 0; j < JT; ++j) {
-                const float v = ent[1 + j];
-                float x[C];
-                load_row<C>(src + j * a.c, a.c, lane, x);
+                for (int j = 3; j < JT; ++j)
+                    mx[j - 3] = lane < n ? a.g.entries[(long long)(ri.start + e0 + lane) * stride + 1 + j] : 0.f;
+            }
+            for (int e = 0; e < n; e += UB) {
+                float x[UB][JT][C], v[UB][JT];
 #pragma unroll
-                for (int i = 0; i < C; ++i) acc[i] = fmaf(v, x[i], acc[i]);
+                for (int u = 0; u < UB; ++u) {
+                    const int eu = min(e + u, n - 1);
+                    const int col = __builtin_amdgcn_readlane(__float_as_int(me.x), eu);
+                    const bool live = e + u < n;
+                    v[u][0] = live ? bcast(me.y, eu) : 0.f;
+                    if constexpr (JT > 1) v[u][1] = live ? bcast(me.z, eu) : 0.f;
+                    if constexpr (JT > 2) v[u][2] = live ? bcast(me.w, eu) : 0.f;
+#pragma unroll
+                    for (int j = 3; j < JT; ++j) v[u][j] = live ? bcast(mx[j - 3], eu) : 0.f;
+                    const float* src = a.ing + (long long)col * a.ldg + a.gofs;
+#pragma unroll
+                    for (int j = 0; j < JT; ++j) load_row<C>(src + j * a.c, a.c, lane, x[u][j]);
+                }
+#pragma unroll
+                for (int u = 0; u < UB; ++u)
+#pragma unroll
+                    for (int j = 0; j < JT; ++j)
+#pragma unroll
+                        for (int i = 0; i < C; ++i) acc[i] = fmaf(v[u][j], x[u][j][i], acc[i]);
             }
         }
     }
     if constexpr (HP) {
         const RowInfo ri = a.p.rows[r];
-        for (int e = 0; e < ri.count; ++e) {
-            const float4 ent = *reinterpret_cast<const float4*>(a.p.entries + (long long)(ri.start + e) * 4);
-            const int col = __float_as_int(ent.x);
-            const float* src = a.inp + (long long)col * a.ldp;
-            float xm[C], xd[C];
-            load_row<C>(src + a.pofs_m, a.c, lane, xm);
-            load_row<C>(src + a.pofs_d, a.c, lane, xd);
+        for (int e0 = 0; e0 < ri.count; e0 += 64) {
+            const int n = min(64, ri.count - e0);
+            const float4 me = lane_entry(a.p.entries, 4, ri.start + e0, n, lane);
+            for (int e = 0; e < n; e += AGG_U) {
+                float xm[AGG_U][C], xd[AGG_U][C], vm[AGG_U], vd[AGG_U];
 #pragma unroll
-            for (int i = 0; i < C; ++i) acc[i] = fmaf(ent.z, xd[i], fmaf(ent.y, xm[i], acc[i]));
+                for (int u = 0; u < AGG_U; ++u) {
+                    const int eu = min(e + u, n - 1);
+                    const int col = __builtin_amdgcn_readlane(__float_as_int(me.x), eu);
+                    const bool live = e + u < n;
+                    vm[u] = live ? bcast(me.y, eu) : 0.f;
+                    vd[u] = live ? bcast(me.z, eu) : 0.f;
+                    const float* src = a.inp + (long long)col * a.ldp;
+                    load_row<C>(src + a.pofs_m, a.c, lane, xm[u]);
+                    load_row<C>(src + a.pofs_d, a.c, lane, xd[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u)
+#pragma unroll
+                    for (int i = 0; i < C; ++i) acc[i] = fmaf(vd[u], xd[u][i], fmaf(vm[u], xm[u][i], acc[i]));
+            }
         }
     }
     store_row<C>(o, a.c, lane, acc);

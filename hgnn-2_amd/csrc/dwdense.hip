@@ -20,11 +20,10 @@ namespace hgnn {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-namespace {
-constexpr int MAXI = 5;  // items per wave kept in registers
-}
-
-template <int FC>
+// MAXI = (n-tile, m-tile, slice) items per wave kept in registers: sized to the
+// graph so the accumulators do not cap occupancy (5 x 16 AGPRs at Nmax <= 32,
+// where only 3 items exist, left one wave per SIMD)
+template <int FC, int MAXI>
 __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int b = blockIdx.x;
@@ -40,6 +39,9 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     const int nb = a.node_off[b + 1] - off;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int h = lane >> 5, l31 = lane & 31;
+    // float4 staging needs 16-byte aligned rows and slices
+    const bool vec = !a.xdense && F % 4 == 0 && a.lda % 4 == 0 &&
+                     ((reinterpret_cast<uintptr_t>(a.dA) | reinterpret_cast<uintptr_t>(a.xp)) & 15) == 0;
 
     float* dWb = a.dW + (long long)b * nmax * nmax * J;
     for (int base = 0; base < nitems; base += 4 * MAXI) {  // block-uniform passes over the items
@@ -52,35 +54,127 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     for (int f0 = 0; f0 < F; f0 += FC) {
         const int fc = min(FC, F - f0);
         __syncthreads();
-        for (int i = threadIdx.x; i < npad * J * FC; i += blockDim.x) {
-            const int n = i / (J * FC), j = (i / FC) % J, f = i % FC;
-            float v = 0.f;
-            if (f < fc && n < nmax) {
-                const int k = j * F + f0 + f;
-                if (n < nb) {
-                    v = a.dA[(long long)(off + n) * a.lda + k];
-                } else if (a.dout) {
-                    for (int o = 0; o < a.dim_out; ++o)
-                        v = fmaf(a.dout[b * a.dim_out + o], a.fcw[(long long)o * a.kfc + k], v);
+        // Staging issues U independent loads per thread before touching LDS: the
+        // element-at-a-time loop was bound by one load latency per element.
+        constexpr int U = 8;
+        if (vec) {
+            // G rows (dA slices) and X rows share one index space, so every load of the
+            // chunk is in flight before the first LDS write
+            constexpr int F4 = FC / 4;
+            const int g4 = npad * J * F4;
+            const int t4 = g4 + npad * F4;
+            for (int base = 0; base < t4; base += 256 * U) {
+                float4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = base + u * 256 + threadIdx.x;
+                    v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (i < g4) {
+                        const int n = i / (J * F4), j = (i / F4) % J, f = (i % F4) * 4;
+                        if (f < fc && n < nmax) {
+                            const int k = j * F + f0 + f;
+                            if (n < nb) {
+                                v[u] = *reinterpret_cast<const float4*>(a.dA + (long long)(off + n) * a.lda + k);
+                            } else if (a.dout) {
+                                for (int o = 0; o < a.dim_out; ++o) {
+                                    const float d = a.dout[b * a.dim_out + o];
+                                    const float* w = a.fcw + (long long)o * a.kfc + k;
+                                    v[u].x = fmaf(d, w[0], v[u].x);
+                                    v[u].y = fmaf(d, w[1], v[u].y);
+                                    v[u].z = fmaf(d, w[2], v[u].z);
+                                    v[u].w = fmaf(d, w[3], v[u].w);
+                                }
+                            }
+                        }
+                    } else if (i < t4) {
+                        const int ix = i - g4;
+                        const int m = ix / F4, f = (ix % F4) * 4;
+                        if (f < fc && m < nmax) {
+                            const int c = f0 + f;
+                            if (m < nb) {
+                                v[u] = *reinterpret_cast<const float4*>(a.xp + (long long)(off + m) * F + c);
+                            } else if (a.pmean) {
+                                float t[4];
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) {
+                                    const float hh = __fdiv_rn(__fsub_rn(0.f, a.pmean[c + q]), a.pstd[c + q]);
+                                    t[q] = __fadd_rn(__fmul_rn(*a.pw, hh), *a.pb);
+                                }
+                                v[u] = make_float4(t[0], t[1], t[2], t[3]);
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = base + u * 256 + threadIdx.x;
+                    float* d = nullptr;
+                    if (i < g4) {
+                        const int n = i / (J * F4), j = (i / F4) % J, f = (i % F4) * 4;
+                        d = Gs + n * GP + j * FC + f;
+                    } else if (i < t4) {
+                        const int ix = i - g4;
+                        d = Xs + (ix / F4) * XP + (ix % F4) * 4;
+                    }
+                    if (d) {
+                        d[0] = v[u].x;
+                        d[1] = v[u].y;
+                        d[2] = v[u].z;
+                        d[3] = v[u].w;
+                    }
                 }
             }
-            Gs[n * GP + j * FC + f] = v;
-        }
-        for (int i = threadIdx.x; i < npad * FC; i += blockDim.x) {
-            const int m = i / FC, f = i % FC;
-            float v = 0.f;
-            if (f < fc && m < nmax) {
-                const int c = f0 + f;
-                if (a.xdense) {
-                    v = a.xdense[((long long)b * F + c) * nmax + m];
-                } else if (m < nb) {
-                    v = a.xp[(long long)(off + m) * F + c];
-                } else if (a.pmean) {
-                    const float hh = __fdiv_rn(__fsub_rn(0.f, a.pmean[c]), a.pstd[c]);
-                    v = __fadd_rn(__fmul_rn(*a.pw, hh), *a.pb);
+        } else {
+            const int gn = npad * J * FC;
+            for (int base = 0; base < gn; base += 256 * U) {
+                float v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = base + u * 256 + threadIdx.x;
+                    v[u] = 0.f;
+                    const int n = i / (J * FC), j = (i / FC) % J, f = i % FC;
+                    if (i < gn && f < fc && n < nmax) {
+                        const int k = j * F + f0 + f;
+                        if (n < nb) {
+                            v[u] = a.dA[(long long)(off + n) * a.lda + k];
+                        } else if (a.dout) {
+                            for (int o = 0; o < a.dim_out; ++o)
+                                v[u] = fmaf(a.dout[b * a.dim_out + o], a.fcw[(long long)o * a.kfc + k], v[u]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = base + u * 256 + threadIdx.x;
+                    if (i < gn) Gs[(i / (J * FC)) * GP + ((i / FC) % J) * FC + i % FC] = v[u];
                 }
             }
-            Xs[m * XP + f] = v;
+            const int xn = npad * FC;
+            for (int base = 0; base < xn; base += 256 * U) {
+                float v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = base + u * 256 + threadIdx.x;
+                    v[u] = 0.f;
+                    const int m = i / FC, f = i % FC;
+                    if (i < xn && f < fc && m < nmax) {
+                        const int c = f0 + f;
+                        if (a.xdense) {
+                            v[u] = a.xdense[((long long)b * F + c) * nmax + m];
+                        } else if (m < nb) {
+                            v[u] = a.xp[(long long)(off + m) * F + c];
+                        } else if (a.pmean) {
+                            const float hh = __fdiv_rn(__fsub_rn(0.f, a.pmean[c]), a.pstd[c]);
+                            v[u] = __fadd_rn(__fmul_rn(*a.pw, hh), *a.pb);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = base + u * 256 + threadIdx.x;
+                    if (i < xn) Xs[(i / FC) * XP + i % FC] = v[u];
+                }
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -102,16 +196,28 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
         if (it >= nitems) continue;
         const int j = it % J, tm = (it / J) % tiles, tn = it / (J * tiles);
         const int m = tm * 32 + l31;
+        // read all 16 previous values before any store: a load-add-store per element
+        // is serialised by the compiler (possible aliasing) into 16 memory round trips
+        float old[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int n = tn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (n < nmax && m < nmax) {
-                float* p = dWb + ((long long)n * nmax + m) * J + j;
-                *p = a.accumulate ? *p + acc[q][r] : acc[q][r];
-            }
+            old[r] = (a.accumulate && n < nmax && m < nmax) ? dWb[((long long)n * nmax + m) * J + j] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int n = tn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (n < nmax && m < nmax) dWb[((long long)n * nmax + m) * J + j] = old[r] + acc[q][r];
         }
     }
     }
+}
+
+template <int FC>
+static void launch_fc(const DwDenseArgs& a, int maxi, size_t lds, hipStream_t s) {
+    if (maxi <= 1) hipLaunchKernelGGL((k_dw_dense<FC, 1>), dim3(a.bs), dim3(256), lds, s, a);
+    else if (maxi <= 3) hipLaunchKernelGGL((k_dw_dense<FC, 3>), dim3(a.bs), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((k_dw_dense<FC, 5>), dim3(a.bs), dim3(256), lds, s, a);
 }
 
 int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
@@ -119,9 +225,11 @@ int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
     const int fc = npad <= 32 ? 64 : (npad <= 64 ? 32 : 16);
     const size_t lds = sizeof(float) * (size_t)npad * ((a.jt * fc + 1) + (fc + 1));
     if (lds > 64 * 1024) return 2;
-    if (fc == 64) hipLaunchKernelGGL(k_dw_dense<64>, dim3(a.bs), dim3(256), lds, s, a);
-    else if (fc == 32) hipLaunchKernelGGL(k_dw_dense<32>, dim3(a.bs), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL(k_dw_dense<16>, dim3(a.bs), dim3(256), lds, s, a);
+    const int tiles = npad / 32;
+    const int maxi = ceil_div(tiles * tiles * a.jt, 4);
+    if (fc == 64) launch_fc<64>(a, maxi, lds, s);
+    else if (fc == 32) launch_fc<32>(a, maxi, lds, s);
+    else launch_fc<16>(a, maxi, lds, s);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -3,6 +3,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../include tools/gemm_lab.hip -o /tmp/gemm_lab
 #include "../hgnn-2_amd/csrc/gemm2.hip"
 #include "../hgnn-2_amd/csrc/gemm3.hip"
+#include "../hgnn-2_amd/csrc/dwdense.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -433,9 +434,70 @@ void dw_lab(hipStream_t s) {
     }
 }
 
+void dwdense_lab(hipStream_t s) {
+    const int bs = 512, nmax = 29, F = 128, J = 3, lda = 640;
+    std::vector<int> off(bs + 1);
+    srand(3);
+    off[0] = 0;
+    for (int b = 0; b < bs; ++b) off[b + 1] = off[b] + 9 + rand() % 21;
+    const int rows = off[bs];
+    float *dA, *xp, *dW, *mean, *stdv, *pw, *pb;
+    int* noff;
+    CK(hipMalloc(&dA, (size_t)rows * lda * 4));
+    CK(hipMalloc(&xp, (size_t)rows * F * 4));
+    CK(hipMalloc(&dW, (size_t)bs * nmax * nmax * J * 4));
+    CK(hipMalloc(&mean, F * 4));
+    CK(hipMalloc(&stdv, F * 4));
+    CK(hipMalloc(&pw, 4));
+    CK(hipMalloc(&pb, 4));
+    CK(hipMalloc(&noff, (bs + 1) * 4));
+    CK(hipMemcpy(noff, off.data(), (bs + 1) * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(dA, 0, (size_t)rows * lda * 4));
+    CK(hipMemset(xp, 0, (size_t)rows * F * 4));
+    CK(hipMemset(dW, 0, (size_t)bs * nmax * nmax * J * 4));
+    std::vector<float> ones(F, 1.f);
+    CK(hipMemcpy(stdv, ones.data(), F * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(mean, 0, F * 4));
+    CK(hipMemset(pw, 0, 4));
+    CK(hipMemset(pb, 0, 4));
+    for (int acc = 0; acc < 2; ++acc) {
+        DwDenseArgs a{};
+        a.dA = dA;
+        a.lda = lda;
+        a.f = F;
+        a.jt = J;
+        a.xp = xp;
+        a.pmean = mean;
+        a.pstd = stdv;
+        a.pw = pw;
+        a.pb = pb;
+        a.node_off = noff;
+        a.bs = bs;
+        a.nmax = nmax;
+        a.dW = dW;
+        a.accumulate = acc;
+        launch_dw_dense(a, s);
+        CK(hipStreamSynchronize(s));
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        CK(hipEventRecord(e0, s));
+        for (int r = 0; r < 20; ++r) launch_dw_dense(a, s);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("dw_dense bs=%d nmax=%d F=%d accumulate=%d: %.1f us\n", bs, nmax, F, acc, ms * 1e3 / 20);
+    }
+}
+
 int main() {
     hipStream_t s;
     CK(hipStreamCreate(&s));
+    if (getenv("LAB_DWDENSE")) {
+        dwdense_lab(s);
+        return 0;
+    }
     if (getenv("LAB_DW")) {
         dw_lab(s);
         return 0;
