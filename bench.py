@@ -157,7 +157,8 @@ def main():
         ms, n = timer.elapsed(dominant)
         timer.close()
         counts = RF.batch_counts(W.detach(), WL, Pm, Pd, Nb, Eb)
-        roof = RF.roofline_entry(dominant, ms, n, counts, args.order, 5, args.d, args.layers, args.steps)
+        roof = RF.roofline_entry(dominant, ms, n, counts, args.order, 5, args.d, args.layers, args.steps,
+                                 pmc_path=os.path.join(REPO, "profiles", "pmc_traffic.json"))
         roof["class_ms_per_step_profile"] = {RF.NAMES[k]: round(v[0] / 2, 4) for k, v in per.items()}
 
     value = args.bs * world * args.steps / elapsed

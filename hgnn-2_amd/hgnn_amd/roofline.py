@@ -84,7 +84,49 @@ def class_work(kcls, counts, order, f_in, d, n_layers, jt=3):
     return fl, by
 
 
-def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, steps, jt=3):
+# kernel-name predicates of each class (rocprofv3 names of csrc/*.hip), for the PMC traffic join
+CLASS_KERNELS = {
+    K_STRUCT: ("k_plan", "k_extract", "k_pack_nodes", "k_pack_edges", "k_repack", "k_unpack_nodes"),
+    K_AGG_FWD: ("k_agg_fwd",),
+    K_GEMM_FWD: ("k_gemm3<", "k_gemm2<"),
+    K_BN_FWD: ("k_bn_finalize", "k_bn_apply"),
+    K_READOUT: ("k_readout",),
+    K_BN_BWD: ("k_bn_bwd",),
+    K_GEMM_DW: ("k_gemm3_tn", "k_gemm2_dw"),
+    K_GEMM_DA: ("k_gemm3<", "k_gemm2_da"),
+    K_AGG_BWD: ("k_agg_bwd",),
+    K_DW_DENSE: ("k_dw_dense",),
+    K_DW_REDUCE: ("k_dw_reduce", "k_db_reduce"),
+}
+
+
+def _in_class(kcls, name):
+    if not any(t in name for t in CLASS_KERNELS[kcls]):
+        return False
+    if "k_gemm3<" in name:  # k_gemm3<BM, BN, BK, WGM, WGN, EPI>: EPI 0 = forward, 1 = dA
+        epi = name.split(">")[0].rsplit(",", 1)[-1].strip()
+        return (kcls == K_GEMM_FWD) == (epi == "0")
+    return True
+
+
+def pmc_traffic(kcls, path):
+    """HBM bytes per launch of class kcls from a tools/pmc_summary.py JSON (FETCH_SIZE x2 + WRITE_SIZE,
+    MI355X_MICROARCH.md HBM section), launch-weighted over the class's kernels; None if absent."""
+    import json
+    import os
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        rows = json.load(fh)
+    tot = n = 0.0
+    for name, r in rows.items():
+        if _in_class(kcls, name) and r.get("traffic_bytes") is not None:
+            tot += r["traffic_bytes"] * r["launches"]
+            n += r["launches"]
+    return tot / n if n else None
+
+
+def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, steps, jt=3, pmc_path=None):
     """bench.py 'roofline' object for a kernel class measured over `steps` steps."""
     fl, by = class_work(kcls, counts, order, f_in, d, n_layers, jt)
     sec = ms_total / 1e3
@@ -102,7 +144,9 @@ def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, s
         "peak": peak,
         "unit": unit,
         "frac": round(achieved / peak, 4),
-        "traffic": None,
+        "traffic": pmc_traffic(kcls, pmc_path),
+        "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_traffic.json)",
+        "algorithmic_bytes_per_launch": by / max(per_launch, 1e-9),
         "launches_per_step": per_launch,
         "avg_launch_us": round(ms_total * 1e3 / max(launches, 1), 3),
         "algorithmic_per_step": {"flops": fl, "bytes": by},

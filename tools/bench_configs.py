@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Throughput of the other BASELINE.json configurations on one GPU (not the bench line).
+
+bench.py measures the headline metric (config 2).  This script times the
+remaining configurations of BASELINE.json on the same executor, each as
+graphs/s of a training pass (forward + loss + backward) with inputs resident
+in HBM, and the LG-GNN forward alone (the north star's "batched LG-GNN
+forward" roofline):
+
+  cfg1   GNN_simple(0, 2, 20, 5, 1, 1), 32 SBM N=50 graphs per step
+  cfg2f  GNN_lg d=64 order 2 L=5, 512 QM9-shape graphs, forward only (train-mode BN)
+  cfg2o1 / cfg2o3  the same step with orders 1 / 3
+  cfg3   CCN_1D(5, 1, 2, 2), 256 QM9-shape graphs (A + I), per-graph MSE summed
+  cfg4   GNN_lg d=128 order 2 L=5, 512 QM9-shape graphs (one GPU's share of 4096)
+  cfg5   CCN_2D(5, 1, 2, 2), 64 SBM N=200 graphs (A + I)
+
+Prints one JSON line per configuration.  Usage:
+  python tools/bench_configs.py [--only cfg3,cfg5] [--steps 20] [--warmup 5]
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "hgnn-2_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+
+def lg_batch(bs, seed, sbm_n=None):
+    import hgnn_amd.datagen as dg
+    from functions.batching import prepare_batch
+    from functions.operators import graph_operators
+    graphs = dg.sbm_dataset(bs, n=sbm_n, seed=seed) if sbm_n else dg.qm9_shape_dataset(bs, seed=seed)
+    data = [[X, A, t, *graph_operators([X, A], 1, True)] for X, A, t in graphs]
+    return [t.cuda() for t in prepare_batch(data, 0, 1)]
+
+
+def ccn_batch(graphs):
+    bs = len(graphs)
+    nmax = max(X.shape[0] for X, _, _ in graphs)
+    f = graphs[0][0].shape[1]
+    X = torch.zeros(bs, nmax, f)
+    A = torch.zeros(bs, nmax, nmax)
+    T = torch.zeros(bs, 1)
+    nb = torch.zeros(bs, dtype=torch.int64)
+    for b, (x, a, t) in enumerate(graphs):
+        n = x.shape[0]
+        X[b, :n] = x
+        A[b, :n, :n] = a + torch.eye(n)  # scripts/train_ccn.py:36
+        T[b, 0] = t[0]
+        nb[b] = n
+    return X.cuda(), A.cuda(), T.cuda(), nb.cuda()
+
+
+def timeit(step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def run_lg(name, desc, d, order, bs, steps, warmup, backward=True):
+    from models.gnns.model_mnb import GNN_lg
+    torch.manual_seed(0)
+    model = GNN_lg(0, d, 5, 5, 1, 1, order).cuda()
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = lg_batch(bs, 1000)
+    crit = torch.nn.MSELoss()
+    if backward:
+        X.requires_grad_(True)
+        W.requires_grad_(True)
+
+    def step():
+        if backward:
+            model.zero_grad(set_to_none=True)
+            X.grad = W.grad = None
+            crit(model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg), T).backward()
+        else:
+            with torch.no_grad():
+                model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+
+    sec = timeit(step, steps, warmup)
+    return dict(config=name, workload=desc, graphs_per_step=bs, ms_per_step=round(sec * 1e3, 4),
+                value=round(bs / sec, 2), unit="graphs/s", dtype="fp32",
+                nodes=int(Nb.sum()), edge_slots=int(Eb.sum()))
+
+
+def run_simple(steps, warmup):
+    from models.gnns.model_mnb import GNN_simple
+    torch.manual_seed(0)
+    model = GNN_simple(0, 2, 20, 5, 1, 1).cuda()
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = lg_batch(32, 1000, sbm_n=50)
+    X.requires_grad_(True)
+    W.requires_grad_(True)
+    crit = torch.nn.MSELoss()
+
+    def step():
+        model.zero_grad(set_to_none=True)
+        X.grad = W.grad = None
+        crit(model([X, W], Nb, mask), T).backward()
+
+    sec = timeit(step, steps, warmup)
+    return dict(config="cfg1", workload="GNN_simple(0,2,20,5,1,1) fwd+bwd, 32 SBM N=50 graphs",
+                graphs_per_step=32, ms_per_step=round(sec * 1e3, 4), value=round(32 / sec, 2), unit="graphs/s",
+                dtype="fp32")
+
+
+def run_ccn(name, order, graphs, desc, steps, warmup):
+    from models.compnets.model_ccn import CCN_1D, CCN_2D
+    torch.manual_seed(0)
+    net = (CCN_1D if order == 1 else CCN_2D)(5, 1, 2, 2).cuda()
+    X, A, T, nb = ccn_batch(graphs)
+    X.requires_grad_(True)
+
+    def step():
+        net.zero_grad(set_to_none=True)
+        X.grad = None
+        out = net.forward_batch(X, A, nb)
+        ((out - T) ** 2).sum().backward()  # sum of the per-graph MSE losses (scripts/train_ccn.py:52-60)
+
+    sec = timeit(step, steps, warmup)
+    deg = (A > 0).sum(-1).double()
+    return dict(config=name, workload=desc, graphs_per_step=len(graphs), ms_per_step=round(sec * 1e3, 4),
+                value=round(len(graphs) / sec, 2), unit="graphs/s", dtype="fp32",
+                sum_d=int(deg.sum()), sum_d2=int((deg ** 2).sum()), sum_d3=int((deg ** 3).sum()),
+                d_max=int(deg.max()))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    a = ap.parse_args()
+    only = set(x for x in a.only.split(",") if x)
+    import hgnn_amd.datagen as dg
+    jobs = {
+        "cfg1": lambda: run_simple(a.steps, a.warmup),
+        "cfg2f": lambda: run_lg("cfg2f", "GNN_lg d=64 order 2 L=5, forward only, 512 QM9-shape", 64, 2, 512,
+                                a.steps, a.warmup, backward=False),
+        "cfg2o1": lambda: run_lg("cfg2o1", "GNN_lg d=64 order 1 L=5 fwd+bwd, 512 QM9-shape", 64, 1, 512, a.steps,
+                                 a.warmup),
+        "cfg2o3": lambda: run_lg("cfg2o3", "GNN_lg d=64 order 3 L=5 fwd+bwd, 512 QM9-shape", 64, 3, 512, a.steps,
+                                 a.warmup),
+        "cfg3": lambda: run_ccn("cfg3", 1, dg.qm9_shape_dataset(256, seed=0),
+                                "CCN_1D(5,1,2,2) fwd+bwd, 256 QM9-shape graphs", a.steps, a.warmup),
+        "cfg4": lambda: run_lg("cfg4", "GNN_lg d=128 order 2 L=5 fwd+bwd, 512 QM9-shape (1 GPU of 4096)", 128, 2,
+                               512, a.steps, a.warmup),
+        "cfg5": lambda: run_ccn("cfg5", 2, dg.sbm_dataset(64, n=200, seed=0),
+                                "CCN_2D(5,1,2,2) fwd+bwd, 64 SBM N=200 graphs", max(3, a.steps // 4),
+                                max(1, a.warmup // 2)),
+    }
+    for k, fn in jobs.items():
+        if only and k not in only:
+            continue
+        print(json.dumps(fn()), flush=True)
+
+
+if __name__ == "__main__":
+    main()
