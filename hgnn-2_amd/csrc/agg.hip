@@ -87,6 +87,32 @@ __device__ __forceinline__ float bcast(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// Per-lane BN constants of the CPL channels a lane owns (lane * CPL + i).
+template <int CPL>
+struct LaneBn {
+    float mu[CPL], sd[CPL], w, b;
+    bool on;
+    __device__ __forceinline__ void init(const BnView& v, int C, int lane) {
+        on = v.mean != nullptr;
+        w = b = 0.f;
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) mu[i] = 0.f, sd[i] = 1.f;
+        if (!on) return;
+        w = *v.w;
+        b = *v.b;
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) {
+            const int c = lane * CPL + i;
+            if (c < C) mu[i] = v.mean[c], sd[i] = v.std[c];
+        }
+    }
+    __device__ __forceinline__ void apply(float (&x)[CPL]) const {
+        if (!on) return;
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) x[i] = bn_z(x[i], mu[i], sd[i], w, b);
+    }
+};
+
 template <int JT, int CG, int CP>
 __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
     const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -101,6 +127,8 @@ __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
             for (int i = 0; i < CG; ++i) acc[j][i] = 0.f;
         const RowInfo ri = a.g.rows[r];
         const int stride = a.g.stride;
+        LaneBn<CG> bn;
+        bn.init(a.gbn, a.cg, lane);
         for (int e0 = 0; e0 < ri.count; e0 += 64) {
             const int n = min(64, ri.count - e0);
             // JT <= 3: one float4 per entry; larger JT reads the extra coefficients below
@@ -127,6 +155,8 @@ __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
                     load_row<CG>(a.xg + (long long)col * a.cg, a.cg, lane, x[u]);
                 }
 #pragma unroll
+                for (int u = 0; u < AGG_U; ++u) bn.apply(x[u]);
+#pragma unroll
                 for (int u = 0; u < AGG_U; ++u)
 #pragma unroll
                     for (int j = 0; j < JT; ++j)
@@ -142,6 +172,8 @@ __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
 #pragma unroll
         for (int i = 0; i < CP; ++i) am[i] = ad[i] = 0.f;
         const RowInfo ri = a.p.rows[r];
+        LaneBn<CP> bn;
+        bn.init(a.pbn, a.cp, lane);
         for (int e0 = 0; e0 < ri.count; e0 += 64) {
             const int n = min(64, ri.count - e0);
             const float4 me = lane_entry(a.p.entries, 4, ri.start + e0, n, lane);
@@ -156,6 +188,8 @@ __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
                     vd[u] = live ? bcast(me.z, eu) : 0.f;
                     load_row<CP>(a.xp + (long long)col * a.cp, a.cp, lane, x[u]);
                 }
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u) bn.apply(x[u]);
 #pragma unroll
                 for (int u = 0; u < AGG_U; ++u)
 #pragma unroll

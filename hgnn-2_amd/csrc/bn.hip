@@ -224,16 +224,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
             const float m1 = a.sums[ch * 4 + 0] * inv_n;
             const float m2 = a.sums[ch * 4 + 1] * inv_n;
             auto one = [&](float yv, float dzv) {
-                const float g = wv * dzv;
-                float d;
-                if (a.training) {
-                    const float h = __fdiv_rn(__fsub_rn(yv, mu), sd);
-                    d = (g - m1 - h * m2) / sd;
-                } else {
-                    d = g / sd;
-                }
-                if (ch >= a.relu_from && !(yv > 0.f)) d = 0.f;
-                return d;
+                return bn_bwd_dy(yv, dzv, mu, sd, wv, m1, m2, a.training != 0, ch >= a.relu_from);
             };
             int r = r0 + rg;
             for (; r + 3 * rgn < r1; r += 4 * rgn) {
@@ -271,12 +262,13 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
     }
 }
 
-int launch_bn_backward(const BnBwdArgs& a, hipStream_t s) {
+int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     const int tiles = bn_bwd_tiles(a.cap_rows);
     if (tiles > 0) hipLaunchKernelGGL(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
     HGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_bn_bwd_fin, dim3(a.c), dim3(256), 0, s, a);
     HGNN_LAUNCH_CHECK();
+    if (!apply) return 0;
     hipLaunchKernelGGL(k_bn_bwd_apply, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;

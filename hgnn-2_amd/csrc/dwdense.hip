@@ -93,6 +93,12 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
                             const int c = f0 + f;
                             if (m < nb) {
                                 v[u] = *reinterpret_cast<const float4*>(a.xp + (long long)(off + m) * F + c);
+                                if (a.pmean) {
+                                    v[u].x = bn_z(v[u].x, a.pmean[c], a.pstd[c], *a.pw, *a.pb);
+                                    v[u].y = bn_z(v[u].y, a.pmean[c + 1], a.pstd[c + 1], *a.pw, *a.pb);
+                                    v[u].z = bn_z(v[u].z, a.pmean[c + 2], a.pstd[c + 2], *a.pw, *a.pb);
+                                    v[u].w = bn_z(v[u].w, a.pmean[c + 3], a.pstd[c + 3], *a.pw, *a.pb);
+                                }
                             } else if (a.pmean) {
                                 float t[4];
 #pragma unroll
@@ -163,6 +169,7 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
                             v[u] = a.xdense[((long long)b * F + c) * nmax + m];
                         } else if (m < nb) {
                             v[u] = a.xp[(long long)(off + m) * F + c];
+                            if (a.pmean) v[u] = bn_z(v[u], a.pmean[c], a.pstd[c], *a.pw, *a.pb);
                         } else if (a.pmean) {
                             const float hh = __fdiv_rn(__fsub_rn(0.f, a.pmean[c]), a.pstd[c]);
                             v[u] = __fadd_rn(__fmul_rn(*a.pw, hh), *a.pb);

@@ -19,7 +19,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-enum { E3_FWD = 0, E3_STORE = 1 };
+enum { E3_FWD = 0, E3_STORE = 1, E3_DA_BN = 2 };
 
 struct G3 {
     const float* a;
@@ -35,6 +35,18 @@ struct G3 {
     const float* bias;
     int relu_from;
     float* bn_part;  // [ceil(m_cap / 64)][n][3] (count, mean, M2)
+    // E3_DA_BN: A = dY computed on load from (y, dz) and the BN statistics (a = y, lda = k)
+    const float* dz;
+    const float* mean;
+    const float* stdv;
+    const float* bn_w;
+    const float* sums;  // [k][4] from k_bn_bwd_fin
+    int bn_relu_from;
+    int training;
+    float* dy_out;      // [rows][k], written by the blockIdx.y == 0 column of tiles
+    float* dbpart;      // [tiles][k] column sums of dY
+    float* dw_s;        // BN scalar grads
+    float* db_s;
 };
 
 template <int BM, int BN, int BK, int WGM, int WGN, int EPI>
@@ -52,13 +64,67 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
     const int wm = wv / WGN, wn = wv % WGN;
     const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     const int Mv = p.m_valid ? *p.m_valid : p.m_cap;
-    if (m0 >= Mv) return;
+    if (m0 >= Mv && !(EPI == E3_DA_BN && blockIdx.x == 0 && blockIdx.y == 0)) return;
     const int K = p.k, N = p.n;
 
     // The k tail (K % 4 != 0: the padding columns of the aggregate) is zeroed when the
     // staged registers are written to LDS, not right after the load: masking there
     // makes the compiler wait for every load at once (vmcnt(0)) and kills the prefetch.
     float4 ra[AF4], rb[BF4];
+    float4 rz[EPI == E3_DA_BN ? AF4 : 1];
+    // E3_DA_BN: per-channel affine form of the BN backward, dY = ca dz + cb (y - mu) + ce
+    // (train: ca = w / sd, cb = -m2 / sd^2, ce = -m1 / sd; eval: ca = w / sd), in LDS
+    constexpr int KB = EPI == E3_DA_BN ? 512 : 1;
+    __shared__ float colsum[KB], cA[KB], cB[KB], cE[KB], cMu[KB];
+    if constexpr (EPI == E3_DA_BN) {
+        const float inv_n = Mv > 0 ? 1.0f / (float)Mv : 0.f;
+        const float wv = *p.bn_w;
+        for (int ch = tid; ch < K; ch += NT) {
+            const float sd = p.stdv[ch];
+            colsum[ch] = 0.f;
+            cA[ch] = wv / sd;
+            cMu[ch] = p.mean[ch];
+            if (p.training) {
+                const float m1 = p.sums[ch * 4 + 0] * inv_n, m2 = p.sums[ch * 4 + 1] * inv_n;
+                cB[ch] = -m2 / (sd * sd);
+                cE[ch] = -m1 / sd;
+            } else {
+                cB[ch] = 0.f;
+                cE[ch] = 0.f;
+            }
+        }
+        if (blockIdx.x == 0 && blockIdx.y == 0 && (tid >> 6) == 0) {
+            // BN scalar grads: dw = sum_c sum_r dz h, db = sum_c sum_r dz (k_bn_bwd_apply formerly)
+            double t1 = 0.0, t2 = 0.0;
+            for (int ch = lane; ch < K; ch += 64) {
+                t1 += (double)p.sums[ch * 4 + 2];
+                t2 += (double)p.sums[ch * 4 + 3];
+            }
+            t1 = wave_sum_d(t1);
+            t2 = wave_sum_d(t2);
+            if (lane == 0) {
+                *p.dw_s = (float)t1;
+                *p.db_s = (float)t2;
+            }
+        }
+        if (m0 >= Mv) return;  // block (0, 0) of an empty batch: scalar grads only
+        __syncthreads();        // constants ready before the first staging
+    }
+    // dY for the staged float4 at (row gm, channels gk..gk+3); zero outside the matrix
+    auto bn_dy = [&](float4 yv, float4 dzv, int gm, int gk) {
+        const float yy[4] = {yv.x, yv.y, yv.z, yv.w}, zz[4] = {dzv.x, dzv.y, dzv.z, dzv.w};
+        float d[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int ch = gk + q;
+            d[q] = 0.f;
+            if (gm < Mv && ch < K) {
+                d[q] = fmaf(cA[ch], zz[q], fmaf(cB[ch], yy[q] - cMu[ch], cE[ch]));
+                if (ch >= p.bn_relu_from && !(yy[q] > 0.f)) d[q] = 0.f;
+            }
+        }
+        return make_float4(d[0], d[1], d[2], d[3]);
+    };
     auto mask_tail = [](float4 v, int gk, int kend) {
         if (gk + 3 >= kend) {
             if (gk >= kend) v.x = 0.f;
@@ -76,6 +142,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (gm < Mv && gk < K) v = *reinterpret_cast<const float4*>(p.a + (long long)gm * p.lda + gk);
             ra[i] = v;
+            if constexpr (EPI == E3_DA_BN) {
+                float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (gm < Mv && gk < K) z = *reinterpret_cast<const float4*>(p.dz + (long long)gm * p.lda + gk);
+                rz[i] = z;
+            }
         }
 #pragma unroll
         for (int i = 0; i < BF4; ++i) {
@@ -91,7 +162,31 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
 #pragma unroll
         for (int i = 0; i < AF4; ++i) {
             const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
-            *reinterpret_cast<float4*>(&As[buf][row * LDK + kq]) = tail ? mask_tail(ra[i], k0 + kq, K) : ra[i];
+            if constexpr (EPI == E3_DA_BN) {
+                const int gm = m0 + row, gk = k0 + kq;
+                const float4 d = bn_dy(ra[i], rz[i], gm, gk);
+                *reinterpret_cast<float4*>(&As[buf][row * LDK + kq]) = d;
+                if (blockIdx.y == 0) {
+                    if (gm < Mv && gk < K) *reinterpret_cast<float4*>(p.dy_out + (long long)gm * p.lda + gk) = d;
+                    // column sums: lanes with equal lane % (BK / 4) hold the same 4 columns
+                    float4 cs = d;
+#pragma unroll
+                    for (int off = BK / 4; off < 64; off <<= 1) {
+                        cs.x += __shfl_xor(cs.x, off, 64);
+                        cs.y += __shfl_xor(cs.y, off, 64);
+                        cs.z += __shfl_xor(cs.z, off, 64);
+                        cs.w += __shfl_xor(cs.w, off, 64);
+                    }
+                    if (lane < BK / 4 && gk < K) {
+                        atomicAdd(&colsum[gk], cs.x);
+                        atomicAdd(&colsum[gk + 1], cs.y);
+                        atomicAdd(&colsum[gk + 2], cs.z);
+                        atomicAdd(&colsum[gk + 3], cs.w);
+                    }
+                }
+            } else {
+                *reinterpret_cast<float4*>(&As[buf][row * LDK + kq]) = tail ? mask_tail(ra[i], k0 + kq, K) : ra[i];
+            }
         }
 #pragma unroll
         for (int i = 0; i < BF4; ++i) {
@@ -235,6 +330,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
                     if (gm < Mv && gn < N) p.c[(long long)gm * p.ldc + gn] = acc[i][j][r];
                 }
             }
+        if constexpr (EPI == E3_DA_BN) {
+            if (blockIdx.y == 0)  // colsum complete: the main loop ended with a barrier
+                for (int i = tid; i < K; i += NT) p.dbpart[(long long)blockIdx.x * K + i] = colsum[i];
+        }
     }
 }
 
@@ -367,6 +466,38 @@ size_t dw3_slab_floats(int r_cap, int o, int k) {
 }
 
 // slabs[z][o][k] = sum_{r in chunk z} dY[r, o] A[r, k]
+int launch_gemm3_da_bn(const BnBwdArgs& bn, const int* m_valid, int m_cap, int o, const float* wt, int ldw, int kout,
+                       float* da, int ldda, hipStream_t s) {
+    if (m_cap <= 0) return 0;
+    if (o > 512 || o % 4 != 0 || bn.c != o) return 2;
+    G3 p{};
+    p.a = bn.y;
+    p.lda = o;
+    p.b = wt;
+    p.ldb = ldw;
+    p.m_cap = m_cap;
+    p.m_valid = m_valid;
+    p.k = o;
+    p.n = kout;
+    p.c = da;
+    p.ldc = ldda;
+    p.dz = bn.dz;
+    p.mean = bn.mean;
+    p.stdv = bn.std;
+    p.bn_w = bn.w;
+    p.sums = bn.sums;
+    p.bn_relu_from = bn.relu_from;
+    p.training = bn.training;
+    p.dy_out = bn.dy;
+    p.dbpart = bn.dbpart;
+    p.dw_s = bn.dw;
+    p.db_s = bn.db;
+    hipLaunchKernelGGL((k_gemm3<64, 128, 32, 2, 2, E3_DA_BN>), dim3(ceil_div(m_cap, 64), ceil_div(kout, 128)),
+                       dim3(256), 0, s, p);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
                     int kchunk, float* slabs, hipStream_t s) {
     if (r_cap <= 0) return 0;

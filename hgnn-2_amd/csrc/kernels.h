@@ -57,6 +57,20 @@ int launch_pack_edges(const float* XL, int bs, int emax, BatchMeta m, float* out
 int launch_unpack_nodes(const float* in, int bs, int f, int nmax, BatchMeta m, float* X, hipStream_t s);
 
 // ---------------------------------------------------------------- aggregation
+// BN of a layer output applied where it is read: z = w ((y - mean_c) / std_c) + b
+// (batch_normalization.py:43, 76), bit-identical to a separate apply pass.
+// mean == nullptr: the features are read as stored.
+struct BnView {
+    const float* mean;
+    const float* std;
+    const float* w;
+    const float* b;
+};
+
+__device__ __forceinline__ float bn_z(float y, float mu, float sd, float w, float b) {
+    return __fadd_rn(__fmul_rn(w, __fdiv_rn(__fsub_rn(y, mu), sd)), b);
+}
+
 struct AggFwdArgs {
     const int* total_rows;  // device
     int cap_rows;
@@ -64,10 +78,12 @@ struct AggFwdArgs {
     StructView g;
     const float* xg;
     int cg, jtot;
+    BnView gbn;             // xg holds pre-BN y (mean != null) or the features themselves
     // P part: out[:, jtot*Cg + c] = sum pm * Xp[col, c];  [.. + Cp + c] = sum pd * Xp[col, c]
     StructView p;
     const float* xp;
     int cp;
+    BnView pbn;
     float* out;
     int ldo;
 };
@@ -220,17 +236,40 @@ struct BnBwdArgs {
     float* db;             // scalar out
     float* dbpart;         // optional out: per-64-row-tile column sums of dy [tiles][c]
 };
-int launch_bn_backward(const BnBwdArgs& a, hipStream_t s);
+// apply = 0: only the statistics (part + fin); dY is then produced by the dA GEMM
+// (launch_gemm3_da_bn), which applies the BN backward while staging its A operand.
+int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply = 1);
 int bn_bwd_tiles(int cap_rows);
+// dA = BNbwd(y, dz) . WT^T with dY computed on load; also writes dY (for dW), the
+// per-64-row-tile column sums of dY (conv bias grads) and the BN scalar grads.
+int launch_gemm3_da_bn(const BnBwdArgs& bn, const int* m_valid, int m_cap, int o, const float* wt, int ldw, int kout,
+                       float* da, int ldda, hipStream_t s);
+
+// dY of BN backward + ReLU for one element (batch_normalization.py:65-77 autograd):
+// g = w dz, h = (y - mean) / std, train: (g - m1 - h m2) / std with m1 = mean(g),
+// m2 = mean(g h) over the real rows; eval: g / std; ReLU branch masked where y <= 0.
+__device__ __forceinline__ float bn_bwd_dy(float yv, float dzv, float mu, float sd, float wv, float m1, float m2,
+                                           bool training, bool relu) {
+    const float g = wv * dzv;
+    float d;
+    if (training) {
+        const float h = __fdiv_rn(__fsub_rn(yv, mu), sd);
+        d = (g - m1 - h * m2) / sd;
+    } else {
+        d = g / sd;
+    }
+    if (relu && !(yv > 0.f)) d = 0.f;
+    return d;
+}
 
 // ---------------------------------------------------------------- dense dW of the operators
 struct DwDenseArgs {
     const float* dA;       // node-half aggregate gradient [rows][lda]; G block = cols [0, jt*f)
     int lda;
     int f, jt;
-    const float* xp;       // packed layer input [rows][f]  (unless xdense)
+    const float* xp;       // packed layer input [rows][f]  (unless xdense); pre-BN y when pmean != null
     const float* xdense;   // dense (bs, f, nmax) layer input (layer 0), or null
-    const float* pmean;    // BN stats of the producer of xp (padded value), or null -> 0
+    const float* pmean;    // BN stats of the producer of xp (applied on load; padded value), or null -> 0
     const float* pstd;
     const float* pw;
     const float* pb;

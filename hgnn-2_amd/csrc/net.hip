@@ -9,6 +9,7 @@
 // activations live in one caller-provided workspace laid out here, so a
 // forward+backward is a fixed sequence of launches with no allocation and no
 // host synchronisation (graph-capturable).
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -211,8 +212,8 @@ Program build_program(const hgnn_net_config* c) {
     }
     for (auto& f : P.feats) {
         const size_t cap = f.edge ? P.cap_e : P.cap_n;
-        f.z = B.take(cap * f.c * sizeof(float));
         if (f.has_y) f.y = B.take(cap * f.c * sizeof(float));
+        else f.z = B.take(cap * f.c * sizeof(float));
         f.grad = B.take(cap * f.c * sizeof(float));
     }
     size_t max_da = 0, max_slab = 0;
@@ -253,6 +254,29 @@ Program build_program(const hgnn_net_config* c) {
 template <typename T>
 T* at(void* ws, size_t off) {
     return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
+}
+
+// A layer output is kept pre-BN (y) only; its readers apply the BN of the half
+// that produced it on load (BnView).  Inputs (feature 0, XL) are stored as is.
+const Half* producer(const Program& P, int f) {
+    for (const Half& h : P.halves)
+        if (h.out == f) return &h;
+    return nullptr;
+}
+
+const float* feat_src(const Program& P, void* ws, int f) {
+    return P.feats[f].has_y ? at<float>(ws, P.feats[f].y) : at<float>(ws, P.feats[f].z);
+}
+
+BnView feat_bn(const Program& P, void* ws, const float* const* prm, int f) {
+    BnView v{};
+    const Half* h = producer(P, f);
+    if (!h) return v;
+    v.mean = at<float>(ws, h->mean);
+    v.std = at<float>(ws, h->stdv);
+    v.w = prm[h->pbn_w];
+    v.b = prm[h->pbn_b];
+    return v;
 }
 
 BatchMeta meta_of(const Program& P, void* ws) {
@@ -361,12 +385,14 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
         ag.total_rows = tot;
         ag.cap_rows = cap;
         ag.g = view(P, ws, h.edge ? S_WL : S_W);
-        ag.xg = at<float>(ws, P.feats[h.gin].z);
+        ag.xg = feat_src(P, ws, h.gin);
+        ag.gbn = feat_bn(P, ws, prm, h.gin);
         ag.cg = h.cg;
         ag.jtot = P.jt;
         if (h.pin >= 0) {
             ag.p = view(P, ws, h.edge ? S_PE : S_PN);
-            ag.xp = at<float>(ws, P.feats[h.pin].z);
+            ag.xp = feat_src(P, ws, h.pin);
+            ag.pbn = feat_bn(P, ws, prm, h.pin);
             ag.cp = h.cp;
         }
         ag.out = at<float>(ws, h.a);
@@ -413,20 +439,20 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
         bf.momentum = 0.1f;
         if (!c->training && !run) return HGNN_ERR_ARG;
         TL(HGNN_K_BN_FWD, launch_bn_finalize(bf, s));
-        TL(HGNN_K_BN_FWD, launch_bn_apply(at<float>(ws, P.feats[h.out].y), tot, cap, P.c2, bf.mean, bf.std, bf.w, bf.b,
-                            at<float>(ws, P.feats[h.out].z), s));
     }
 
     AggFwdArgs ag{};
     ag.total_rows = tot_n;
     ag.cap_rows = P.cap_n;
     ag.g = view(P, ws, S_W);
-    ag.xg = at<float>(ws, P.feats[P.last_gin].z);
+    ag.xg = feat_src(P, ws, P.last_gin);
+    ag.gbn = feat_bn(P, ws, prm, P.last_gin);
     ag.cg = P.feats[P.last_gin].c;
     ag.jtot = P.jt;
     if (P.last_pin >= 0) {
         ag.p = view(P, ws, S_PN);
-        ag.xp = at<float>(ws, P.feats[P.last_pin].z);
+        ag.xp = feat_src(P, ws, P.last_pin);
+        ag.pbn = feat_bn(P, ws, prm, P.last_pin);
         ag.cp = P.feats[P.last_pin].c;
     }
     ag.out = at<float>(ws, P.a_last);
@@ -473,6 +499,18 @@ static int side_stream(SideStream** out) {
     return 0;
 }
 
+// HGNN_FUSED_DA=1 folds the BN-backward apply pass into the dA GEMM's operand staging.  Measured
+// on the box (tools/ab.sh, 3x2 alternating runs): 281.2-282.4K vs 279.3-282.3K graphs/s -- the
+// saved pass (~80 us/step) is spent again as the 5 N-tiles of each row tile redo the transform.
+// Off by default.
+static bool fused_da_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("HGNN_FUSED_DA");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float* const* prm, void* ws,
                  const float* dout, float* const* grads, float* dX, float* dW, hipStream_t s, Timer* tm) {
     const Program P = build_program(c);
@@ -498,14 +536,12 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         if (gin == 0) {
             a.xdense = in->d_X;
         } else {
-            a.xp = at<float>(ws, P.feats[gin].z);
-            for (const Half& hp : P.halves) {
-                if (hp.out != gin) continue;
-                a.pmean = at<float>(ws, hp.mean);
-                a.pstd = at<float>(ws, hp.stdv);
-                a.pw = prm[hp.pbn_w];
-                a.pb = prm[hp.pbn_b];
-            }
+            a.xp = feat_src(P, ws, gin);
+            const BnView v = feat_bn(P, ws, prm, gin);
+            a.pmean = v.mean;
+            a.pstd = v.std;
+            a.pw = v.w;
+            a.pb = v.b;
         }
         if (readout) {
             a.dout = dout;
@@ -619,7 +655,11 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         bb.dw = grads[h.pbn_w];
         bb.db = grads[h.pbn_b];
         bb.dbpart = P.v2 ? dbp : nullptr;
-        TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s));
+        const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
+        const bool ndw = need_dw && !h.edge;
+        // with a dA GEMM the BN backward's apply pass is fused into its operand staging
+        const bool fused_da = P.v2 && (ng || np || ndw) && fused_da_enabled();
+        TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s, fused_da ? 0 : 1));
 
         if (!P.v2) {
             GemmDwArgs gw{};
@@ -640,16 +680,18 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
             TL(HGNN_K_GEMM_DW, launch_gemm_dw(gw, s));
         }
 
-        const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
-        const bool ndw = need_dw && !h.edge;
         if (!ng && !np && !ndw) {
             if (P.v2) TRY(fork_dw(h, cap, tot, dyb, dbp));
             continue;
         }
         float* da = at<float>(ws, P.da);
         if (P.v2) {
-            TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2, tot, cap, P.c2, at<float>(ws, h.wt), P.c2, h.k, da, h.kp,
-                                               s));
+            if (fused_da)
+                TL(HGNN_K_GEMM_DA,
+                   launch_gemm3_da_bn(bb, tot, cap, P.c2, at<float>(ws, h.wt), P.c2, h.k, da, h.kp, s));
+            else
+                TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2, tot, cap, P.c2, at<float>(ws, h.wt), P.c2, h.k, da,
+                                                   h.kp, s));
             // dW starts once dA is done: two MFMA GEMMs side by side only slow each other,
             // dW beside the latency-bound dense-dW / aggregation-backward kernels does not
             TRY(fork_dw(h, cap, tot, dyb, dbp));

@@ -1,0 +1,14 @@
+#!/bin/bash
+# A/B of an env switch on one box: alternating bench runs (no CPU baseline).
+# usage: VAR=HGNN_FUSED_DA A=0 B=1 REPS=3 bash tools/ab.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+for r in $(seq 1 ${REPS:-3}); do
+  for v in ${A:-0} ${B:-1}; do
+    out=gpurun_out/ab_${v}_${r}.json
+    env $VAR=$v timeout -k 10 300 python bench.py --steps ${STEPS:-50} --warmup 5 --cpu-baseline 0 ${BENCH_ARGS:-} > $out 2> gpurun_out/ab.err
+    rc=$?; if [ $rc -ne 0 ]; then tail -5 gpurun_out/ab.err; exit $rc; fi
+    python -c "import json; d=json.loads(open('$out').read().strip().splitlines()[-1]); print('$VAR=$v', d['value'], d['ms_per_step'], d['roofline']['class_ms_per_step_profile'])"
+  done
+done
