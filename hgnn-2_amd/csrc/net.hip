@@ -264,7 +264,9 @@ const Half* producer(const Program& P, int f) {
     return nullptr;
 }
 
-const float* feat_src(const Program& P, void* ws, int f) {
+const float* feat_src(const Program& P, void* ws, int f, const float* x0 = nullptr, const float* xl0 = nullptr) {
+    if (f == 0 && x0) return x0;
+    if (f == 1 && xl0 && P.feats[1].edge && !P.feats[1].has_y) return xl0;
     return P.feats[f].has_y ? at<float>(ws, P.feats[f].y) : at<float>(ws, P.feats[f].z);
 }
 
@@ -278,6 +280,16 @@ BnView feat_bn(const Program& P, void* ws, const float* const* prm, int f) {
     v.b = prm[h->pbn_b];
     return v;
 }
+
+// Where a call's batch structure lives: the workspace (filled by the device
+// extraction from the dense inputs) or a CSR batch image built on the host.
+struct Src {
+    BatchMeta m;
+    StructView v[S_COUNT];
+    const float* x0 = nullptr;   // packed node input (CSR batch) -- else feats[0].z
+    const float* xl0 = nullptr;  // packed edge input (CSR batch) -- else feats[1].z
+    long long nodes = 0;         // host node count (CSR batch)
+};
 
 BatchMeta meta_of(const Program& P, void* ws) {
     BatchMeta m;
@@ -294,6 +306,26 @@ StructView view(const Program& P, void* ws, int kind) {
     v.entries = at<float>(ws, P.ent[kind]);
     v.stride = (kind == S_PN || kind == S_PE) ? 4 : P.entry_stride_w;
     return v;
+}
+
+Src make_src(const Program& P, void* ws, const hgnn_csr_batch* csr) {
+    Src r;
+    r.m = meta_of(P, ws);
+    for (int k = 0; k < S_COUNT; ++k) r.v[k] = view(P, ws, k);
+    if (csr) {
+        r.m.node_off = const_cast<int*>(static_cast<const int*>(csr->d_node_off));
+        r.m.edge_off = const_cast<int*>(static_cast<const int*>(csr->d_edge_off));
+        r.m.totals = const_cast<int*>(static_cast<const int*>(csr->d_totals));
+        for (int k = 0; k < S_COUNT; ++k) {
+            r.v[k].rows = static_cast<const RowInfo*>(csr->d_rows[k]);
+            r.v[k].entries = csr->d_entries[k];
+            r.v[k].stride = (k == S_PN || k == S_PE) ? 4 : csr->stride_w;
+        }
+        r.x0 = csr->d_x;
+        r.xl0 = csr->d_xl;
+        r.nodes = csr->nodes;
+    }
+    return r;
 }
 
 #define TRY(x)                  \
@@ -323,12 +355,14 @@ struct Timer {
         }                                                                               \
     } while (0)
 
-int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float* const* prm,
-                float* const* run, void* ws, float* out, hipStream_t s, Timer* tm) {
+int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
+                const float* const* prm, float* const* run, void* ws, float* out, hipStream_t s, Timer* tm) {
     const Program P = build_program(c);
     const bool lg = c->kind == 1;
-    BatchMeta m = meta_of(P, ws);
+    const Src src = make_src(P, ws, csr);
+    BatchMeta m = src.m;
     HGNN_HOST_CHECK(hipMemsetAsync(m.err, 0, sizeof(uint32_t), s));
+    if (!csr) {
     TL(HGNN_K_STRUCT, launch_plan(in->d_N_batch, lg ? in->d_E_batch : nullptr, c->bs, c->nmax, lg ? c->emax : 0, m, s));
 
     ExtractArgs ex{};
@@ -353,6 +387,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
     TL(HGNN_K_STRUCT, launch_extract(ex, s));
     TL(HGNN_K_STRUCT, launch_pack_nodes(in->d_X, c->bs, c->f_in, c->nmax, m, at<float>(ws, P.feats[0].z), s));
     if (lg) TL(HGNN_K_STRUCT, launch_pack_edges(in->d_XL, c->bs, c->emax, m, at<float>(ws, P.feats[1].z), s));
+    }
 
     const int* tot_n = m.totals;
     const int* tot_e = m.totals + 1;
@@ -384,14 +419,14 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
         AggFwdArgs ag{};
         ag.total_rows = tot;
         ag.cap_rows = cap;
-        ag.g = view(P, ws, h.edge ? S_WL : S_W);
-        ag.xg = feat_src(P, ws, h.gin);
+        ag.g = src.v[h.edge ? S_WL : S_W];
+        ag.xg = feat_src(P, ws, h.gin, src.x0, src.xl0);
         ag.gbn = feat_bn(P, ws, prm, h.gin);
         ag.cg = h.cg;
         ag.jtot = P.jt;
         if (h.pin >= 0) {
-            ag.p = view(P, ws, h.edge ? S_PE : S_PN);
-            ag.xp = feat_src(P, ws, h.pin);
+            ag.p = src.v[h.edge ? S_PE : S_PN];
+            ag.xp = feat_src(P, ws, h.pin, src.x0, src.xl0);
             ag.pbn = feat_bn(P, ws, prm, h.pin);
             ag.cp = h.cp;
         }
@@ -444,14 +479,14 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float
     AggFwdArgs ag{};
     ag.total_rows = tot_n;
     ag.cap_rows = P.cap_n;
-    ag.g = view(P, ws, S_W);
-    ag.xg = feat_src(P, ws, P.last_gin);
+    ag.g = src.v[S_W];
+    ag.xg = feat_src(P, ws, P.last_gin, src.x0, src.xl0);
     ag.gbn = feat_bn(P, ws, prm, P.last_gin);
     ag.cg = P.feats[P.last_gin].c;
     ag.jtot = P.jt;
     if (P.last_pin >= 0) {
-        ag.p = view(P, ws, S_PN);
-        ag.xp = feat_src(P, ws, P.last_pin);
+        ag.p = src.v[S_PN];
+        ag.xp = feat_src(P, ws, P.last_pin, src.x0, src.xl0);
         ag.pbn = feat_bn(P, ws, prm, P.last_pin);
         ag.cp = P.feats[P.last_pin].c;
     }
@@ -511,10 +546,12 @@ static bool fused_da_enabled() {
     return on;
 }
 
-int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const float* const* prm, void* ws,
-                 const float* dout, float* const* grads, float* dX, float* dW, hipStream_t s, Timer* tm) {
+int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
+                 const float* const* prm, void* ws, const float* dout, float* const* grads, float* dX, float* dW,
+                 hipStream_t s, Timer* tm) {
     const Program P = build_program(c);
-    BatchMeta m = meta_of(P, ws);
+    const Src src = make_src(P, ws, csr);
+    BatchMeta m = src.m;
     const int* tot_n = m.totals;
     const int* tot_e = m.totals + 1;
     std::vector<char> init(P.feats.size(), 0);
@@ -525,7 +562,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         return true;
     };
     const bool need_dw = c->need_dw != 0;
-    if (need_dw && (!dW || !in || !in->d_X)) return HGNN_ERR_ARG;
+    if (need_dw && (!dW || !in || !in->d_X || csr)) return HGNN_ERR_ARG;
     // dense dW contribution of one graph_oper(W, X_l): G block of dA (node rows) x X_l
     auto dw_dense = [&](int gin, const float* da, int lda, bool readout, int accumulate) -> int {
         DwDenseArgs a{};
@@ -536,7 +573,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         if (gin == 0) {
             a.xdense = in->d_X;
         } else {
-            a.xp = feat_src(P, ws, gin);
+            a.xp = feat_src(P, ws, gin, src.x0, src.xl0);
             const BnView v = feat_bn(P, ws, prm, gin);
             a.pmean = v.mean;
             a.pstd = v.std;
@@ -570,7 +607,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
             AggBwdArgs ab{};
             ab.total_rows = tot_n;
             ab.cap_rows = P.cap_n;
-            ab.g = view(P, ws, S_WT);
+            ab.g = src.v[S_WT];
             ab.ing = da;
             ab.ldg = P.k_last;
             ab.gofs = 0;
@@ -587,7 +624,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
             AggBwdArgs ab{};
             ab.total_rows = tot_e;
             ab.cap_rows = P.cap_e;
-            ab.p = view(P, ws, S_PE);
+            ab.p = src.v[S_PE];
             ab.inp = da;
             ab.ldp = P.k_last;
             ab.pofs_m = P.jt * cg;
@@ -715,7 +752,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
             AggBwdArgs ab{};
             ab.total_rows = tot;
             ab.cap_rows = cap;
-            ab.g = view(P, ws, h.edge ? S_WLT : S_WT);
+            ab.g = src.v[h.edge ? S_WLT : S_WT];
             ab.ing = da;
             ab.ldg = h.kp;
             ab.gofs = 0;
@@ -732,7 +769,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
             AggBwdArgs ab{};
             ab.total_rows = other_edge ? tot_e : tot_n;
             ab.cap_rows = other_edge ? P.cap_e : P.cap_n;
-            ab.p = view(P, ws, h.edge ? S_PN : S_PE);
+            ab.p = src.v[h.edge ? S_PN : S_PE];
             ab.inp = da;
             ab.ldp = h.kp;
             ab.pofs_m = P.jt * h.cg;
@@ -752,7 +789,11 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const floa
         if (!dX) return HGNN_ERR_ARG;
         if (!init[0]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[0].grad), 0,
                                                      (size_t)P.cap_n * c->f_in * sizeof(float), s));
-        TL(HGNN_K_STRUCT, launch_unpack_nodes(at<float>(ws, P.feats[0].grad), c->bs, c->f_in, c->nmax, m, dX, s));
+        if (csr)
+            HGNN_HOST_CHECK(hipMemcpyAsync(dX, at<float>(ws, P.feats[0].grad), (size_t)src.nodes * c->f_in * sizeof(float),
+                                           hipMemcpyDeviceToDevice, s));
+        else
+            TL(HGNN_K_STRUCT, launch_unpack_nodes(at<float>(ws, P.feats[0].grad), c->bs, c->f_in, c->nmax, m, dX, s));
     }
     return 0;
 }
@@ -772,6 +813,7 @@ const char* hgnn_status_string(int status) {
         case HGNN_ERR_ARG: return "invalid argument";
         case HGNN_ERR_UNSUPPORTED: return "unsupported configuration";
         case HGNN_ERR_HIP: return "HIP runtime error";
+        case HGNN_ERR_INDEX: return "index out of range";
         default: return "unknown status";
     }
 }
@@ -802,15 +844,16 @@ int hgnn_net_forward(const hgnn_net_config* cfg, const hgnn_net_inputs* in, cons
     if (!in->d_X || !in->d_W || !in->d_N_batch || !in->d_mask) return HGNN_ERR_ARG;
     if (cfg->kind == 1 && (!in->d_XL || !in->d_WL || !in->d_Pm || !in->d_Pd || !in->d_E_batch || !in->d_mask_lg))
         return HGNN_ERR_ARG;
-    return net_forward(cfg, in, params, bn_running, workspace, d_out, static_cast<hipStream_t>(stream), nullptr);
+    return net_forward(cfg, in, nullptr, params, bn_running, workspace, d_out, static_cast<hipStream_t>(stream),
+                       nullptr);
 }
 
 int hgnn_net_backward(const hgnn_net_config* cfg, const hgnn_net_inputs* in, const float* const* params,
                       void* workspace, const float* d_dout, float* const* grads, float* d_dX, float* d_dW,
                       void* stream) {
     if (!valid_config(cfg) || !params || !workspace || !d_dout || !grads) return HGNN_ERR_ARG;
-    return net_backward(cfg, in, params, workspace, d_dout, grads, d_dX, d_dW, static_cast<hipStream_t>(stream),
-                        nullptr);
+    return net_backward(cfg, in, nullptr, params, workspace, d_dout, grads, d_dX, d_dW,
+                        static_cast<hipStream_t>(stream), nullptr);
 }
 
 void* hgnn_timer_create(int max_launches, unsigned class_mask) {
@@ -860,7 +903,7 @@ void hgnn_timer_destroy(void* timer) {
 int hgnn_net_forward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* in, const float* const* params,
                            float* const* bn_running, void* workspace, float* d_out, void* stream, void* timer) {
     if (!valid_config(cfg) || !in || !params || !workspace || !d_out) return HGNN_ERR_ARG;
-    return net_forward(cfg, in, params, bn_running, workspace, d_out, static_cast<hipStream_t>(stream),
+    return net_forward(cfg, in, nullptr, params, bn_running, workspace, d_out, static_cast<hipStream_t>(stream),
                        static_cast<Timer*>(timer));
 }
 
@@ -868,8 +911,53 @@ int hgnn_net_backward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* i
                             void* workspace, const float* d_dout, float* const* grads, float* d_dX, float* d_dW,
                             void* stream, void* timer) {
     if (!valid_config(cfg) || !params || !workspace || !d_dout || !grads) return HGNN_ERR_ARG;
-    return net_backward(cfg, in, params, workspace, d_dout, grads, d_dX, d_dW, static_cast<hipStream_t>(stream),
-                        static_cast<Timer*>(timer));
+    return net_backward(cfg, in, nullptr, params, workspace, d_dout, grads, d_dX, d_dW,
+                        static_cast<hipStream_t>(stream), static_cast<Timer*>(timer));
+}
+
+static bool csr_matches(const hgnn_net_config* cfg, const hgnn_csr_batch* b) {
+    if (!b || !b->d_node_off || !b->d_totals || !b->d_x || !b->d_rows[S_W] || !b->d_rows[S_WT]) return false;
+    if (cfg->kind == 1 && (!b->d_xl || !b->d_rows[S_WL] || !b->d_rows[S_WLT] || !b->d_rows[S_PN] || !b->d_rows[S_PE]))
+        return false;
+    return b->stride_w == (cfg->j_tot <= 3 ? 4 : 8);
+}
+
+int hgnn_csr_batch_view(const hgnn_csr_layout* L, const void* d_base, hgnn_csr_batch* out) {
+    if (!L || !d_base || !out) return HGNN_ERR_ARG;
+    const char* b = static_cast<const char*>(d_base);
+    hgnn_csr_batch r{};
+    r.d_node_off = b + L->off_node_off;
+    r.d_edge_off = b + L->off_edge_off;
+    r.d_totals = b + L->off_totals;
+    r.d_n_batch = reinterpret_cast<const int64_t*>(b + L->off_n_batch);
+    r.d_e_batch = reinterpret_cast<const int64_t*>(b + L->off_e_batch);
+    r.d_x = reinterpret_cast<const float*>(b + L->off_x);
+    r.d_xl = reinterpret_cast<const float*>(b + L->off_xl);
+    for (int k = 0; k < S_COUNT; ++k) {
+        r.d_rows[k] = b + L->off_rows[k];
+        r.d_entries[k] = reinterpret_cast<const float*>(b + L->off_entries[k]);
+    }
+    r.stride_w = L->stride_w;
+    r.nodes = L->nodes;
+    r.edges = L->edges;
+    *out = r;
+    return HGNN_OK;
+}
+
+int hgnn_net_forward_csr(const hgnn_net_config* cfg, const hgnn_csr_batch* batch, const float* const* params,
+                         float* const* bn_running, void* workspace, float* d_out, void* stream) {
+    if (!valid_config(cfg) || !csr_matches(cfg, batch) || !params || !workspace || !d_out) return HGNN_ERR_ARG;
+    return net_forward(cfg, nullptr, batch, params, bn_running, workspace, d_out, static_cast<hipStream_t>(stream),
+                       nullptr);
+}
+
+int hgnn_net_backward_csr(const hgnn_net_config* cfg, const hgnn_csr_batch* batch, const float* const* params,
+                          void* workspace, const float* d_dout, float* const* grads, float* d_dX, void* stream) {
+    if (!valid_config(cfg) || !csr_matches(cfg, batch) || !params || !workspace || !d_dout || !grads)
+        return HGNN_ERR_ARG;
+    if (cfg->need_dw) return HGNN_ERR_ARG;
+    return net_backward(cfg, nullptr, batch, params, workspace, d_dout, grads, d_dX, nullptr,
+                        static_cast<hipStream_t>(stream), nullptr);
 }
 
 }  // extern "C"

@@ -95,3 +95,10 @@ def prepare_batch(batch, task, J=1):
         mask[i, :n, :n] = 1
         mask_lg[i, :e, :e] = 1
     return X, W, T, XL, WL, Pm, Pd, mask, mask_lg, N_batch, E_batch
+
+
+def prepare_batch_csr(batch, task, J=1, device="cuda"):
+    """Native sparse counterpart of prepare_batch for the executor (hgnn_amd.csr.CsrBatch):
+    operators built from each instance's A by csrc/builder.cpp, no dense padding."""
+    from hgnn_amd.csr import prepare_batch_csr as _p
+    return _p(batch, task, J, device)

@@ -17,7 +17,8 @@ import torch  # noqa: F401  (load torch's HIP runtime before ours)
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhgnn_amd.so")
 
 HGNN_OK = 0
-STATUS = {0: "ok", 1: "invalid argument", 2: "unsupported configuration", 3: "HIP runtime error"}
+STATUS = {0: "ok", 1: "invalid argument", 2: "unsupported configuration", 3: "HIP runtime error",
+          4: "index out of range"}
 DEVERR = {
     0x1: "operator entry outside a graph's real block (padding must be zero)",
     0x2: "mask[:, :, 0] disagrees with N_batch / E_batch",
@@ -37,6 +38,24 @@ class NetConfig(ctypes.Structure):
 class NetInputs(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
         "d_X", "d_XL", "d_W", "d_WL", "d_Pm", "d_Pd", "d_N_batch", "d_E_batch", "d_mask", "d_mask_lg")]
+
+
+class CsrLayout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("bs", "nmax", "emax", "f_in", "j_tot", "dual", "stride_w",
+                                               "reserved")] + \
+               [("nodes", ctypes.c_int64), ("edges", ctypes.c_int64), ("rows", ctypes.c_int64 * 6),
+                ("nnz", ctypes.c_int64 * 6)] + \
+               [(n, ctypes.c_int64) for n in ("off_node_off", "off_edge_off", "off_totals", "off_n_batch",
+                                               "off_e_batch", "off_x", "off_xl")] + \
+               [("off_rows", ctypes.c_int64 * 6), ("off_entries", ctypes.c_int64 * 6), ("bytes", ctypes.c_int64)]
+
+
+class CsrBatch(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("d_node_off", "d_edge_off", "d_totals", "d_n_batch", "d_e_batch",
+                                                "d_x", "d_xl")] + \
+               [("d_rows", ctypes.c_void_p * 6), ("d_entries", ctypes.c_void_p * 6),
+                ("stride_w", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("nodes", ctypes.c_int64), ("edges", ctypes.c_int64)]
 
 
 class CcnConfig(ctypes.Structure):
@@ -85,6 +104,14 @@ SIGNATURES = {
     "hgnn_collapse6to3": ([_VP, _VP, _I, _I, _VP], _I),
     "hgnn_collapse6to3_backward": ([_VP, _VP, _I, _I, _VP], _I),
     "hgnn_ccn_plan_offsets": ([ctypes.POINTER(CcnConfig), ctypes.c_longlong, ctypes.POINTER(ctypes.c_size_t)], _I),
+    "hgnn_graph_edge_slots": ([_I, _VP], _I),
+    "hgnn_graph_operators": ([_I, _VP, _I, _I, _VP, _I, _VP, _VP, _VP], _I),
+    "hgnn_csr_batch_plan": ([_I, _VP, _VP, _I, _I, _I, ctypes.POINTER(CsrLayout)], _I),
+    "hgnn_csr_batch_build": ([_I, _VP, _VP, _VP, _I, _I, _I, ctypes.POINTER(CsrLayout), _VP], _I),
+    "hgnn_csr_batch_view": ([ctypes.POINTER(CsrLayout), _VP, ctypes.POINTER(CsrBatch)], _I),
+    "hgnn_net_forward_csr": ([ctypes.POINTER(NetConfig), ctypes.POINTER(CsrBatch), _VP, _VP, _VP, _VP, _VP], _I),
+    "hgnn_net_backward_csr": ([ctypes.POINTER(NetConfig), ctypes.POINTER(CsrBatch), _VP, _VP, _VP, _VP, _VP,
+                               _VP], _I),
     "hgnn_conv1x1_workspace_bytes": ([_I, _I, _I, _I], ctypes.c_size_t),
     "hgnn_conv1x1_forward": ([_VP, _VP, _VP, _VP, _I, _I, _I, _I, _I, _VP, _VP], _I),
     "hgnn_conv1x1_backward": ([_VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _I, _VP, _VP], _I),

@@ -279,3 +279,71 @@ def run_net(spec, X, W, N_batch, mask, XL=None, WL=None, Pm=None, Pd=None, E_bat
     params = [p if p.is_contiguous() else p.contiguous() for p in params]
     tensors = (XL, WL, Pm, Pd, Nb, Eb, mask, mask_lg)
     return _NetFn.apply(spec, tensors, X, W, *params)
+
+
+def _csr_config(spec, batch):
+    cfg = L.NetConfig()
+    cfg.kind = spec.kind
+    cfg.order = spec.order
+    cfg.bs = batch.bs
+    cfg.nmax = batch.nmax
+    cfg.emax = batch.emax if spec.kind == 1 else 0
+    cfg.f_in = batch.f_in
+    cfg.d = spec.d
+    cfg.n_layers = spec.n_layers
+    cfg.j_tot = batch.j_tot
+    cfg.dim_out = spec.dim_out
+    cfg.training = 1 if spec.training else 0
+    return cfg
+
+
+class _NetCsrFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec, batch, x, *params):
+        dev = batch.device
+        cfg = _csr_config(spec, batch)
+        lib = L.lib()
+        nbytes = lib.hgnn_net_workspace_bytes(ctypes.byref(cfg))
+        if nbytes == 0:
+            raise RuntimeError("hgnn_amd: unsupported network configuration for this CSR batch")
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        out = torch.empty(cfg.bs, cfg.dim_out, dtype=torch.float32, device=dev)
+        L.check(lib.hgnn_net_forward_csr(ctypes.byref(cfg), ctypes.byref(batch.view), L.ptr_array(params),
+                                         L.ptr_array(spec.running), ctypes.c_void_p(ws.data_ptr()),
+                                         ctypes.c_void_p(out.data_ptr()), L.stream_handle(dev)),
+                "network forward (csr)")
+        ctx.cfg, ctx.ws, ctx.batch, ctx.params = cfg, ws, batch, params
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        cfg = ctx.cfg
+        batch = ctx.batch
+        dout = dout.contiguous().to(torch.float32)
+        grads = [torch.empty_like(p) for p in ctx.params]
+        dX = torch.empty(batch.nodes, batch.f_in, dtype=torch.float32, device=batch.device) \
+            if ctx.needs_input_grad[2] else None
+        cfg.need_dx = 1 if dX is not None else 0
+        cfg.need_dw = 0
+        L.check(L.lib().hgnn_net_backward_csr(ctypes.byref(cfg), ctypes.byref(batch.view), L.ptr_array(ctx.params),
+                                              ctypes.c_void_p(ctx.ws.data_ptr()), ctypes.c_void_p(dout.data_ptr()),
+                                              L.ptr_array(grads), L.ptr(dX), L.stream_handle(batch.device)),
+                "network backward (csr)")
+        return (None, None, dX, *grads)
+
+
+def run_net_csr(spec, batch):
+    """GNN_simple / GNN_lg forward on a hgnn_amd.csr.CsrBatch.  The differentiable node
+    input is batch.x (packed (nodes, f_in)); set batch.x.requires_grad_() for dX."""
+    if not batch.image.is_cuda:
+        raise RuntimeError("hgnn_amd: the CSR batch must be on the GPU (CsrBatch(..., device='cuda'))")
+    if spec.kind == 1 and not batch.dual:
+        raise RuntimeError("hgnn_amd: GNN_lg needs a CSR batch built with dual=True")
+    ks, k_last = expected_k(spec.kind, spec.order, batch.f_in, spec.d, spec.n_layers, batch.j_tot)
+    params = [p if p.is_contiguous() else p.contiguous() for p in spec.params]
+    if params[-2].shape != (spec.dim_out, k_last, 1):
+        raise RuntimeError(f"hgnn_amd: fc weight {tuple(params[-2].shape)} != ({spec.dim_out}, {k_last}, 1)")
+    for p in params:
+        if p.device != batch.device or p.dtype != torch.float32:
+            raise RuntimeError("hgnn_amd: parameters must be float32 on the batch's device")
+    return _NetCsrFn.apply(spec, batch, batch.x, *params)

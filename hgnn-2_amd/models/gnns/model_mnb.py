@@ -16,7 +16,7 @@ training mode exactly as the reference rebinds them.
 import torch
 import torch.nn as nn
 
-from hgnn_amd.net import NetSpec, run_net
+from hgnn_amd.net import NetSpec, run_net, run_net_csr
 from models.layers import layers_mnb
 
 
@@ -52,16 +52,22 @@ class GNN_simple(nn.Module):
     def _layers(self):
         return [self.layer0] + [self._modules['layer{}'.format(i + 1)] for i in range(self.n_layers - 2)]
 
-    def forward(self, state, N_batch, mask):
-        X, W = state
+    def _spec(self, device):
         params, running = [], []
         for layer in self._layers():
             params += _simple_params(layer)
-            running += list(layer.bn1.running_on(X.device))
+            running += list(layer.bn1.running_on(device))
         params += [self.layerlast.fc.weight, self.layerlast.fc.bias]
-        spec = NetSpec(kind=0, order=0, d=self.n_features, n_layers=self.n_layers, dim_out=self.n_outputs,
+        return NetSpec(kind=0, order=0, d=self.n_features, n_layers=self.n_layers, dim_out=self.n_outputs,
                        params=params, running=running, training=self.training)
-        return run_net(spec, X, W, N_batch, mask)
+
+    def forward(self, state, N_batch, mask):
+        X, W = state
+        return run_net(self._spec(X.device), X, W, N_batch, mask)
+
+    def forward_csr(self, batch):
+        """Same network on a hgnn_amd.csr.CsrBatch (native batcher, no dense operators)."""
+        return run_net_csr(self._spec(batch.device), batch)
 
 
 class GNN_lg(nn.Module):
@@ -93,14 +99,20 @@ class GNN_lg(nn.Module):
     def _layers(self):
         return [self.layer0] + [self._modules['layer{}'.format(i + 1)] for i in range(self.n_layers - 2)]
 
-    def forward(self, state, N_batch, mask, E_batch, mask_lg):
-        X, XL, W, WL, Pm, Pd = state
+    def _spec(self, device):
         params, running = [], []
         for layer in self._layers():
             params += _lg_params(layer)
-            running += list(layer.bn1.running_on(X.device)) + list(layer.bn2.running_on(X.device))
+            running += list(layer.bn1.running_on(device)) + list(layer.bn2.running_on(device))
         params += [self.layerlast.fc.weight, self.layerlast.fc.bias]
         order = self.order if self.order in (1, 2) else 3
-        spec = NetSpec(kind=1, order=order, d=self.n_features, n_layers=self.n_layers, dim_out=self.n_outputs,
+        return NetSpec(kind=1, order=order, d=self.n_features, n_layers=self.n_layers, dim_out=self.n_outputs,
                        params=params, running=running, training=self.training)
-        return run_net(spec, X, W, N_batch, mask, XL, WL, Pm, Pd, E_batch, mask_lg)
+
+    def forward(self, state, N_batch, mask, E_batch, mask_lg):
+        X, XL, W, WL, Pm, Pd = state
+        return run_net(self._spec(X.device), X, W, N_batch, mask, XL, WL, Pm, Pd, E_batch, mask_lg)
+
+    def forward_csr(self, batch):
+        """Same network on a hgnn_amd.csr.CsrBatch (native batcher, no dense operators)."""
+        return run_net_csr(self._spec(batch.device), batch)

@@ -44,6 +44,7 @@ extern "C" {
 #define HGNN_ERR_ARG 1          /* invalid argument: null pointer, bad size   */
 #define HGNN_ERR_UNSUPPORTED 2  /* configuration not compiled (e.g. J > 3)    */
 #define HGNN_ERR_HIP 3          /* HIP launch / runtime failure               */
+#define HGNN_ERR_INDEX 4        /* input the reference rejects with IndexError */
 
 #define HGNN_DEVERR_PAD_NONZERO 0x1u  /* operator entry outside the real block */
 #define HGNN_DEVERR_MASK 0x2u         /* mask[:, :, 0] != (n < N_batch[b])      */
@@ -155,6 +156,65 @@ int hgnn_net_backward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* i
                             const float* const* params, void* workspace,
                             const float* d_dout, float* const* grads,
                             float* d_dX, float* d_dW, void* stream, void* timer);
+
+/* ------------------------------------------------------------------------
+ * Native operator builder and sparse batcher (host C++, csrc/builder.cpp).
+ *
+ * hgnn_graph_operators replaces graph_operators (functions/operators.py:11-83,
+ * twin preprocessing/preprocessing.py:100-170): dense per-graph W (n, n, J+2) and,
+ * with dual, WL (m, m, J+2), Pm, Pd (n, m), m = hgnn_graph_edge_slots(n, A) =
+ * nnz(A) incl. the diagonal.  Bit-exact, edge-slot quirk included.  Returns
+ * HGNN_ERR_INDEX where the reference raises IndexError.
+ *
+ * hgnn_csr_batch_plan / _build replace prepare_batch (functions/batching.py:77-185)
+ * for the executor: a batch of graphs (A_b (n_b, n_b), X_b (n_b, f_in) row-major,
+ * host memory) goes straight into one host image holding the packed operator row
+ * lists the executor walks, packed X / XL and the batch offsets.  Plan gives the
+ * layout (byte offsets, sizes); build fills an image of layout.bytes bytes; the
+ * caller copies it to the device and describes it with hgnn_csr_batch_view.
+ * ---------------------------------------------------------------------- */
+typedef struct hgnn_csr_layout {
+    int32_t bs, nmax, emax, f_in, j_tot, dual, stride_w, reserved;
+    int64_t nodes, edges;      /* packed node rows, packed edge-slot rows          */
+    int64_t rows[6], nnz[6];   /* per list kind: W, WT, WL, WLT, PN (node->slot), PE */
+    int64_t off_node_off, off_edge_off, off_totals, off_n_batch, off_e_batch, off_x, off_xl;
+    int64_t off_rows[6], off_entries[6];
+    int64_t bytes;
+} hgnn_csr_layout;
+int hgnn_graph_edge_slots(int n, const float* A);
+int hgnn_graph_operators(int n, const float* A, int J, int dual, float* W, int m, float* WL,
+                         float* Pm, float* Pd);
+int hgnn_csr_batch_plan(int bs, const int* n_nodes, const float* const* A, int f_in, int J, int dual,
+                        hgnn_csr_layout* layout);
+int hgnn_csr_batch_build(int bs, const int* n_nodes, const float* const* A, const float* const* X,
+                         int f_in, int J, int dual, const hgnn_csr_layout* layout, void* image);
+
+/* Device view of a CSR batch image (d_base = its device copy). */
+typedef struct hgnn_csr_batch {
+    const void* d_node_off;    /* int32 (bs + 1) */
+    const void* d_edge_off;    /* int32 (bs + 1) */
+    const void* d_totals;      /* int32 [nodes, edges] */
+    const int64_t* d_n_batch;  /* (bs,) */
+    const int64_t* d_e_batch;
+    const float* d_x;          /* packed [nodes][f_in] */
+    const float* d_xl;         /* packed [edges] */
+    const void* d_rows[6];
+    const float* d_entries[6];
+    int32_t stride_w, reserved;
+    int64_t nodes, edges;
+} hgnn_csr_batch;
+int hgnn_csr_batch_view(const hgnn_csr_layout* layout, const void* d_base, hgnn_csr_batch* out);
+
+/* The executor on a CSR batch: cfg->bs / nmax / emax / f_in / j_tot from the
+ * layout; no dense operator, mask or padding is read (no plan / extraction
+ * pass).  Backward: need_dw must be 0 (there is no dense W); d_dX is packed
+ * [nodes][f_in]. */
+int hgnn_net_forward_csr(const hgnn_net_config* cfg, const hgnn_csr_batch* batch,
+                         const float* const* params, float* const* bn_running,
+                         void* workspace, float* d_out, void* stream);
+int hgnn_net_backward_csr(const hgnn_net_config* cfg, const hgnn_csr_batch* batch,
+                          const float* const* params, void* workspace,
+                          const float* d_dout, float* const* grads, float* d_dX, void* stream);
 
 /* ------------------------------------------------------------------------
  * Covariant compositional networks: CCN_1D / CCN_2D forward + backward.

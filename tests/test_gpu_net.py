@@ -201,3 +201,39 @@ def test_empty_line_graph_and_single_node_graphs():
     gmax = max(v.abs().max().item() for v in ref_g.values())
     for k, p in model.named_parameters():
         assert torch.all((p.grad.cpu().double() - ref_g[k]).abs() <= 1e-4 * gmax + 1e-5 * ref_g[k].abs()), k
+
+
+@pytest.mark.parametrize("kind,order", [("lg", 1), ("lg", 2), ("lg", 3), ("simple", 0)])
+def test_csr_batch_path_equals_dense_path(kind, order):
+    """The native batcher's CSR batch (no dense operators, no extraction pass) runs the
+    same kernels on the same lists: outputs, parameter grads and dX are bitwise equal."""
+    import copy
+
+    import hgnn_amd.datagen as dg
+    from hgnn_amd.csr import CsrBatch
+    from models.gnns.model_mnb import GNN_lg, GNN_simple
+    graphs = dg.qm9_shape_dataset(96, seed=404)
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _cuda(_batch(graphs))
+    torch.manual_seed(5)
+    model = (GNN_lg(0, 16, 4, 5, 1, 1, order) if kind == "lg" else GNN_simple(0, 8, 4, 5, 1, 1)).cuda()
+    twin = copy.deepcopy(model)
+    X.requires_grad_(True)
+    out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg) if kind == "lg" else model([X, W], Nb, mask)
+    (out * torch.linspace(-1, 1, out.numel(), device="cuda").view_as(out)).sum().backward()
+    b = CsrBatch([(x, a) for x, a, _ in graphs], dual=kind == "lg")
+    b.x.requires_grad_(True)
+    out2 = twin.forward_csr(b)
+    (out2 * torch.linspace(-1, 1, out2.numel(), device="cuda").view_as(out2)).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    for (n, p), (_, q) in zip(model.named_parameters(), twin.named_parameters()):
+        assert torch.equal(p.grad, q.grad), n
+    n0 = 0
+    nb = Nb.cpu().tolist()
+    for g, n in enumerate(nb):
+        assert torch.equal(X.grad[g, :, :n].t(), b.x.grad[n0:n0 + n]), g
+        n0 += n
+    # running statistics advanced identically
+    for (n, m1), (_, m2) in zip(model.named_modules(), twin.named_modules()):
+        if hasattr(m1, "running_mean") and torch.is_tensor(getattr(m1, "running_mean")):
+            assert torch.equal(m1.running_mean.cpu(), m2.running_mean.cpu()), n

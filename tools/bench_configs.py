@@ -10,6 +10,7 @@ forward" roofline):
   cfg1   GNN_simple(0, 2, 20, 5, 1, 1), 32 SBM N=50 graphs per step
   cfg2f  GNN_lg d=64 order 2 L=5, 512 QM9-shape graphs, forward only (train-mode BN)
   cfg2o1 / cfg2o3  the same step with orders 1 / 3
+  cfg2csr the config-2 step on a CsrBatch from the native batcher (no dense W -> no dense dW)
   cfg3   CCN_1D(5, 1, 2, 2), 256 QM9-shape graphs (A + I), per-graph MSE summed
   cfg4   GNN_lg d=128 order 2 L=5, 512 QM9-shape graphs (one GPU's share of 4096)
   cfg5   CCN_2D(5, 1, 2, 2), 64 SBM N=200 graphs (A + I)
@@ -93,6 +94,33 @@ def run_lg(name, desc, d, order, bs, steps, warmup, backward=True):
                 nodes=int(Nb.sum()), edge_slots=int(Eb.sum()))
 
 
+def run_lg_csr(steps, warmup, bs=512):
+    """Config 2 on the native batcher's CsrBatch: no dense operators, no extraction pass, and
+    (as there is no dense W) no dense dW -- the SURVEY §8 b default input-gradient policy."""
+    import hgnn_amd.datagen as dg
+    from hgnn_amd.csr import CsrBatch
+    from models.gnns.model_mnb import GNN_lg
+    torch.manual_seed(0)
+    model = GNN_lg(0, 64, 5, 5, 1, 1, 2).cuda()
+    graphs = dg.qm9_shape_dataset(bs, seed=1000)
+    t0 = time.perf_counter()
+    b = CsrBatch([(X, A) for X, A, _ in graphs], targets=torch.stack([t[0] for _, _, t in graphs]))
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t0
+    b.x.requires_grad_(True)
+    crit = torch.nn.MSELoss()
+
+    def step():
+        model.zero_grad(set_to_none=True)
+        b.x.grad = None
+        crit(model.forward_csr(b), b.T).backward()
+
+    sec = timeit(step, steps, warmup)
+    return dict(config="cfg2csr", workload="GNN_lg d=64 order 2 L=5 fwd+bwd on a CsrBatch (no dense dW), 512 QM9-shape",
+                graphs_per_step=bs, ms_per_step=round(sec * 1e3, 4), value=round(bs / sec, 2), unit="graphs/s",
+                dtype="fp32", batch_build_ms=round(build_s * 1e3, 2), image_bytes=int(b.layout.bytes))
+
+
 def run_simple(steps, warmup):
     from models.gnns.model_mnb import GNN_simple
     torch.manual_seed(0)
@@ -150,6 +178,7 @@ def main():
                                  a.warmup),
         "cfg2o3": lambda: run_lg("cfg2o3", "GNN_lg d=64 order 3 L=5 fwd+bwd, 512 QM9-shape", 64, 3, 512, a.steps,
                                  a.warmup),
+        "cfg2csr": lambda: run_lg_csr(a.steps, a.warmup),
         "cfg3": lambda: run_ccn("cfg3", 1, dg.qm9_shape_dataset(256, seed=0),
                                 "CCN_1D(5,1,2,2) fwd+bwd, 256 QM9-shape graphs", a.steps, a.warmup),
         "cfg4": lambda: run_lg("cfg4", "GNN_lg d=128 order 2 L=5 fwd+bwd, 512 QM9-shape (1 GPU of 4096)", 128, 2,
