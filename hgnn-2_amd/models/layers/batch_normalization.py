@@ -37,6 +37,15 @@ class BN(nn.Module):
         self.running_std = torch.zeros(n_features, device=_default_device())
         self.momentum = 0.1
 
+    def __setstate__(self, state):
+        # whole-module checkpoints of the reference (torch.save(model), functions/logs.py:99-111)
+        # pickle the running statistics with their autograd history attached: keep the values only
+        super(BN, self).__setstate__(state)
+        for n in ("running_mean", "running_std"):
+            v = self.__dict__.get(n)
+            if torch.is_tensor(v):
+                self.__dict__[n] = v.detach()
+
     def _apply(self, fn, *args, **kwargs):
         super(BN, self)._apply(fn, *args, **kwargs)
         self.running_mean = fn(self.running_mean)

@@ -217,6 +217,25 @@ int hgnn_net_backward_csr(const hgnn_net_config* cfg, const hgnn_csr_batch* batc
                           const float* d_dout, float* const* grads, float* d_dX, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Device-resident training step (csrc/train.hip): the loss and optimizer of
+ * train_with_mnb (scripts/train_mnb.py:41-91) with no host round trip.
+ *
+ * hgnn_mse_loss: T' = normalize_data(T, mean, std) (functions/utils.py:84-95:
+ * mean only when std < 1e-5), d_stats[0] = MSELoss(out, T'), d_stats[1] = MAE
+ * (utils.evaluation, functions/utils.py:98-102), d_stats[2..3] = RunningAverage
+ * (momentum 0.1, functions/utils.py:134-146) of both, updated in place (zero them
+ * per epoch); d_dout (optional) = dLoss/dout = 2 (out - T') / n.
+ * hgnn_adamax_step: torch.optim.Adamax(lr, (beta1, beta2), eps, weight_decay)
+ * (scripts/main_gnn_qm9.py:185) on n_tensors parameter tensors in one launch per
+ * 64 tensors; step = the 1-based step count of this update.
+ * ---------------------------------------------------------------------- */
+int hgnn_mse_loss(const float* d_out, const float* d_t, int n, float t_mean, float t_std, float* d_stats,
+                  float* d_dout, void* stream);
+int hgnn_adamax_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                     float* const* exp_inf, const int64_t* numel, double lr, double beta1, double beta2,
+                     double eps, double weight_decay, long long step, void* stream);
+
+/* ------------------------------------------------------------------------
  * Covariant compositional networks: CCN_1D / CCN_2D forward + backward.
  *
  * Replaces models/compnets/model_ccn.py:41-64 (CCN_1D.forward) and 93-105

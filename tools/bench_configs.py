@@ -11,6 +11,7 @@ forward" roofline):
   cfg2f  GNN_lg d=64 order 2 L=5, 512 QM9-shape graphs, forward only (train-mode BN)
   cfg2o1 / cfg2o3  the same step with orders 1 / 3
   cfg2csr the config-2 step on a CsrBatch from the native batcher (no dense W -> no dense dW)
+  cfg2train / cfg2train_csr  the whole train_with_mnb step on the device (TrainStep: + MSE + Adamax)
   cfg3   CCN_1D(5, 1, 2, 2), 256 QM9-shape graphs (A + I), per-graph MSE summed
   cfg4   GNN_lg d=128 order 2 L=5, 512 QM9-shape graphs (one GPU's share of 4096)
   cfg5   CCN_2D(5, 1, 2, 2), 64 SBM N=200 graphs (A + I)
@@ -121,6 +122,30 @@ def run_lg_csr(steps, warmup, bs=512):
                 dtype="fp32", batch_build_ms=round(build_s * 1e3, 2), image_bytes=int(b.layout.bytes))
 
 
+def run_train(steps, warmup, bs=512, csr=False):
+    """Full train_with_mnb step on the device: forward, MSE, backward, Adamax (hgnn_amd.train.TrainStep)."""
+    import hgnn_amd.datagen as dg
+    from hgnn_amd.csr import CsrBatch
+    from hgnn_amd.train import TrainStep
+    from models.gnns.model_mnb import GNN_lg
+    torch.manual_seed(0)
+    model = GNN_lg(0, 64, 5, 5, 1, 1, 2).cuda()
+    if csr:
+        graphs = dg.qm9_shape_dataset(bs, seed=1000)
+        batch = CsrBatch([(X, A) for X, A, _ in graphs], targets=torch.stack([t[0] for _, _, t in graphs]))
+    else:
+        batch = lg_batch(bs, 1000)
+        batch[0].requires_grad_(True)   # X, W require grad as in scripts/train_mnb.py:56-57
+        batch[1].requires_grad_(True)
+    step = TrainStep(model, lr=3e-4, t_mean=0.5, t_std=2.0)
+    sec = timeit(lambda: step(batch), steps, warmup)
+    name = "cfg2train_csr" if csr else "cfg2train"
+    return dict(config=name, workload="GNN_lg d=64 order 2 L=5 train step (fwd, MSE, bwd, Adamax) on "
+                + ("a CsrBatch" if csr else "dense inputs (X, W require grad)") + ", 512 QM9-shape",
+                graphs_per_step=bs, ms_per_step=round(sec * 1e3, 4), value=round(bs / sec, 2), unit="graphs/s",
+                dtype="fp32", loss=float(step.stats[0].item()))
+
+
 def run_simple(steps, warmup):
     from models.gnns.model_mnb import GNN_simple
     torch.manual_seed(0)
@@ -179,6 +204,8 @@ def main():
         "cfg2o3": lambda: run_lg("cfg2o3", "GNN_lg d=64 order 3 L=5 fwd+bwd, 512 QM9-shape", 64, 3, 512, a.steps,
                                  a.warmup),
         "cfg2csr": lambda: run_lg_csr(a.steps, a.warmup),
+        "cfg2train": lambda: run_train(a.steps, a.warmup),
+        "cfg2train_csr": lambda: run_train(a.steps, a.warmup, csr=True),
         "cfg3": lambda: run_ccn("cfg3", 1, dg.qm9_shape_dataset(256, seed=0),
                                 "CCN_1D(5,1,2,2) fwd+bwd, 256 QM9-shape graphs", a.steps, a.warmup),
         "cfg4": lambda: run_lg("cfg4", "GNN_lg d=128 order 2 L=5 fwd+bwd, 512 QM9-shape (1 GPU of 4096)", 128, 2,

@@ -4,5 +4,5 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python tools/bench_configs.py --only cfg2csr,cfg2f > gpurun_out/configs.jsonl 2> gpurun_out/configs.err
+timeout -k 10 300 python tools/bench_configs.py --only cfg2train > gpurun_out/configs.jsonl 2> gpurun_out/configs.err
 rc=$?; echo "configs rc=$rc"; cat gpurun_out/configs.jsonl; tail -3 gpurun_out/configs.err
