@@ -51,7 +51,7 @@ struct Program {
     size_t node_off = 0, edge_off = 0, totals = 0, err = 0;
     size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
     int entry_stride_w = 4;
-    size_t dy = 0, dy2 = 0, da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0, dbpart2 = 0;
+    size_t dy = 0, dy2 = 0, da = 0, da2 = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0, dbpart2 = 0;
     bool v2 = false;  // GEMM v2 path (2d % 4 == 0); gemm.hip otherwise
     size_t bytes = 0;
 };
@@ -243,6 +243,7 @@ Program build_program(const hgnn_net_config* c) {
     P.dy = B.take((size_t)max_cap * P.c2 * sizeof(float));
     P.dy2 = B.take((size_t)max_cap * P.c2 * sizeof(float));
     P.da = B.take(max_da * sizeof(float));
+    if (P.v2) P.da2 = B.take(max_da * sizeof(float));  // dA alternates like dY: the side stream's dense dW reads it
     P.slabs = B.take(max_slab * sizeof(float));
     P.bnb_part = B.take((size_t)bn_bwd_tiles(max_cap) * P.c2 * 4 * sizeof(float));
     P.bnb_sums = B.take((size_t)P.c2 * 4 * sizeof(float));
@@ -645,7 +646,13 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     // dW of half i may still read its pair while the main stream runs half i+1.
     bool pending[2] = {false, false};
     int parity = 0;
-    auto fork_dw = [&](const Half& h, int cap, const int* tot, float* dyb, float* dbp) -> int {
+    // The side stream also takes the dense operator gradient (W.requires_grad) of a node
+    // half: it only accumulates into dW, so it leaves the dA -> aggregation-backward chain.
+    // (Measured alternative, not kept: the gather half of the aggregation backward on a third
+    // stream, overlapping the next half -- 268K vs 286K graphs/s: the concurrent memory-bound
+    // kernels only slowed each other.)
+    auto fork_dw = [&](const Half& h, int cap, const int* tot, float* dyb, float* dbp, bool ndw_side,
+                       float* dab) -> int {
         const int kc = dw3_kchunk(cap, P.c2, h.k);
         HGNN_HOST_CHECK(hipEventRecord(side->fork[parity], s));
         HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, side->fork[parity], 0));
@@ -653,6 +660,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         s = side->s;  // TL records its timer events on the stream the kernel runs on
         int r = 0;
         do {
+            if (ndw_side) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, dab, h.kp, false, 1));
             TL(HGNN_K_GEMM_DW, launch_gemm3_dw(dyb, P.c2, at<float>(ws, h.a), h.kp, tot, cap, P.c2, h.k, kc,
                                                at<float>(ws, P.slabs), s));
             TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, kc, P.c2, h.k, P.d, grads[h.pw_lin],
@@ -718,10 +726,10 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         }
 
         if (!ng && !np && !ndw) {
-            if (P.v2) TRY(fork_dw(h, cap, tot, dyb, dbp));
+            if (P.v2) TRY(fork_dw(h, cap, tot, dyb, dbp, false, nullptr));
             continue;
         }
-        float* da = at<float>(ws, P.da);
+        float* da = at<float>(ws, (P.v2 && parity) ? P.da2 : P.da);
         if (P.v2) {
             if (fused_da)
                 TL(HGNN_K_GEMM_DA,
@@ -731,7 +739,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
                                                    h.kp, s));
             // dW starts once dA is done: two MFMA GEMMs side by side only slow each other,
             // dW beside the latency-bound dense-dW / aggregation-backward kernels does not
-            TRY(fork_dw(h, cap, tot, dyb, dbp));
+            TRY(fork_dw(h, cap, tot, dyb, dbp, ndw, da));
         } else {
             GemmDaArgs gd{};
             gd.dy = dyb;
@@ -747,7 +755,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             gd.ldda = h.k;
             TL(HGNN_K_GEMM_DA, launch_gemm_da(gd, s));
         }
-        if (ndw) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, da, h.kp, false, 1));
+        if (ndw && !P.v2) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, da, h.kp, false, 1));
         if (ng) {
             AggBwdArgs ab{};
             ab.total_rows = tot;
