@@ -102,3 +102,49 @@ def ccn_forward(p, X, adj, order, layers):
     else:
         summed = [sum(v.sum(0).sum(0) for v in f) for f in levels]
     return _linear(p, "fc", torch.cat(summed, 0))
+
+
+def ccn2_forward_closed(p, X, adj, layers):
+    """CCN_2D forward for one graph with collapse6to3(T (x) chi_ii) in its O(n^3 C) closed form
+    (utils_ccn.py:281-300, contraction.py:106-121): the same function as
+    ccn_forward(..., order=2) without the d^5 intermediate, so it runs at SBM N = 200 (config 5),
+    which the reference itself cannot (5.65 GB per node).  Pinned against ccn_forward on small
+    graphs by tests/test_oracle.py; vectorised per node, any dtype (fp64 for parity)."""
+    n_nodes = X.shape[0]
+    nbrs = receptive_fields(adj)
+    F = [X[i].view(1, 1, -1).expand(len(nbrs[i]), len(nbrs[i]), -1) for i in range(n_nodes)]
+    levels = [F]
+    for l in range(layers):
+        new = []
+        for i in range(n_nodes):
+            n = len(nbrs[i])
+            rows = []
+            for j in nbrs[i]:
+                pj = torch.tensor(positions(nbrs, i, j))
+                valid = pj >= 0
+                q = pj.clamp(min=0)
+                sub = F[j][q][:, q]                       # (n, n, C) = F_j[p(x)][p(y)]
+                m = (valid.view(-1, 1) & valid.view(1, -1)).to(sub.dtype).unsqueeze(-1)
+                rows.append(sub * m)
+            T = torch.stack(rows, 0)                      # [a][b][c][ch]
+            Sc = T.sum(2)                                 # [a][b]
+            Sa = T.sum(0)                                 # [b][c]
+            q1 = Sc.sum(1)                                # [a]
+            q3 = Sa.sum(1)                                # [b]
+            tot = Sc.sum((0, 1))
+            idx = torch.arange(n)
+            d3 = T[idx, idx, idx].sum(0)
+            eye = torch.eye(n, dtype=T.dtype).unsqueeze(-1)
+            nf = float(n)
+            blocks = [nf * Sc, q1.view(n, 1, -1).expand(n, n, -1), nf * Sa, q3.view(n, 1, -1).expand(n, n, -1),
+                      eye * tot, Sc]
+            blocks += [nf * Sc] * 9
+            blocks += [T[:, idx, idx],                    # q15[x][y] = T[x][y][y]
+                       T[idx, :, idx].transpose(0, 1),    # q16[x][y] = T[y][x][y]
+                       eye * d3]
+            coll = torch.cat(blocks, 2)                   # (n, n, 18 C), channel q * C + ch
+            new.append(Fn.relu(_linear(p, "w{}".format(l + 1), coll)))
+        F = new
+        levels.append(F)
+    summed = [sum(v.sum(0).sum(0) for v in f) for f in levels]
+    return _linear(p, "fc", torch.cat(summed, 0))

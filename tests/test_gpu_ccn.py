@@ -160,3 +160,31 @@ def test_ccn_missing_self_loop_raises():
     A[0, 1] = A[1, 0] = 1.0
     with pytest.raises(RuntimeError, match="self loop"):
         net(torch.randn(4, 5).cuda(), A.cuda())
+
+
+def test_ccn2_sbm200_config5_matches_closed_form_oracle():
+    """Config 5 size (SBM N = 200, degrees up to ~57): the reference cannot run it (d^5 intermediates,
+    SURVEY.md §6), so the batched HIP CCN-2D is checked against the fp64 closed-form oracle
+    (oracle/ref_ccn.py ccn2_forward_closed, itself pinned to the literal restatement on the CPU):
+    outputs, parameter gradients and dX for a batch of 3 SBM-200 graphs."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_2D
+    from oracle import ref_ccn as RC
+    graphs = [(X, A + torch.eye(A.shape[0]), t) for X, A, t in dg.sbm_dataset(3, n=200, seed=0)]
+    net = CCN_2D(5, 1, 2, 2)
+    fu.det_init(net, 55)
+    p64 = {n: v.detach().double().clone().requires_grad_(True) for n, v in net.named_parameters()}
+    net = net.cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    Xr = X.clone().requires_grad_(True)
+    out = net.forward_batch(Xr, A, nb)
+    w = torch.tensor([[1.0], [-0.5], [0.25]])
+    (out * w.cuda()).sum().backward()
+    for b, (x, a, _) in enumerate(graphs):
+        xr = x.double().requires_grad_(True)
+        ref = RC.ccn2_forward_closed(p64, xr, a.double(), 2)
+        _close(out[b], ref, f"sbm200 graph {b}")
+        (ref * w[b].double()).sum().backward()
+        _grad_close(Xr.grad[b, :x.shape[0]], xr.grad, f"sbm200 dX graph {b}")
+    for n, p in net.named_parameters():
+        _grad_close(p.grad, p64[n].grad, f"sbm200 grad {n}")

@@ -164,3 +164,27 @@ def test_oracle_ccn_matches_reference(golden, kind):
         for n, v in p.items():
             g = torch.from_numpy(z[f"{kind}_grad_{k}.{n}"])
             assert torch.allclose(v.grad, g, rtol=1e-4, atol=1e-5 * max(1.0, g.abs().max().item())), (k, n)
+
+
+def test_oracle_ccn2_closed_form_matches_literal(golden):
+    """The closed-form CCN-2D oracle (used at SBM-200 size, config 5, where the literal d^5 one and
+    the reference cannot run) equals the literal restatement -- outputs and every gradient -- on the
+    reference fixture graphs and on random SBM graphs (fp64)."""
+    from oracle import ref_ccn as RC
+    import hgnn_amd.datagen as dg
+    z = golden("ccn")
+    graphs = ccn_graphs(z)[:6] + [(X, A + torch.eye(A.shape[0]), t) for X, A, t in dg.sbm_dataset(2, n=12, seed=9)]
+    for k, (X, A, _) in enumerate(graphs):
+        _, p = ccn_params("2d", k, torch.float64)
+        pa = {n: v.clone().requires_grad_(True) for n, v in p.items()}
+        pb = {n: v.clone().requires_grad_(True) for n, v in p.items()}
+        xa = X.double().requires_grad_(True)
+        xb = X.double().requires_grad_(True)
+        a = RC.ccn_forward(pa, xa, A.double(), 2, 2)
+        b = RC.ccn2_forward_closed(pb, xb, A.double(), 2)
+        assert torch.allclose(a, b, rtol=1e-12, atol=1e-10), (k, a, b)
+        a.sum().backward()
+        b.sum().backward()
+        assert torch.allclose(xa.grad, xb.grad, rtol=1e-10, atol=1e-10)
+        for n in p:
+            assert torch.allclose(pa[n].grad, pb[n].grad, rtol=1e-10, atol=1e-10), n
