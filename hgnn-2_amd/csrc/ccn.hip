@@ -613,19 +613,23 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
     // so node i reduces its own gradient matrices per neighbour a (coalesced, L2-hot) instead of
     // every j gathering them:  G[a] = m_a sum_{b in C_a} dSc[a][b] + sum_{b,z in C_a} dSa[b][z]
     //   + sum_{b in C_a} dD1[a][b] + [a in C_a] (sum_{b in C_a} dD2[a][b] + dd3),  C_a = {x: pos_a(x) >= 0}
+    // dSa of one channel is staged in LDS so the masked row sums read LDS, not scattered HBM rows
     __shared__ unsigned long long vm[CCN_MAXD];
+    __shared__ float sa_l[CCN_MAXD * CCN_MAXD];
     __syncthreads();
     for (int a = wv; a < n; a += 4) {
         const unsigned long long m = __ballot(lane < n && v.pos[o2 + a * n + lane] >= 0);
         if (lane == 0) vm[a] = m;
     }
-    __syncthreads();
-    for (int a = wv; a < n; a += 4) {
-        const unsigned long long ma = vm[a];
-        const bool vb = lane < n && ((ma >> lane) & 1ull);
-        const bool va = (ma >> a) & 1ull;
-        const float mf = (float)__popcll(ma);
-        for (int c = 0; c < cin; ++c) {
+    for (int c = 0; c < cin; ++c) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < n * n; e += 256) sa_l[e] = gd.dSa[(o2 + e) * cin + c];
+        __syncthreads();
+        for (int a = wv; a < n; a += 4) {
+            const unsigned long long ma = vm[a];
+            const bool vb = lane < n && ((ma >> lane) & 1ull);
+            const bool va = (ma >> a) & 1ull;
+            const float mf = (float)__popcll(ma);
             float t = 0.f;
             if (vb) {
                 const long long rab = (o2 + (long long)a * n + lane) * cin + c;
@@ -634,7 +638,7 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
                 while (zs) {
                     const int z = __ffsll((long long)zs) - 1;
                     zs &= zs - 1ull;
-                    t += gd.dSa[(o2 + (long long)lane * n + z) * cin + c];
+                    t += sa_l[lane * n + z];
                 }
             }
             t = wave_sum(t);
