@@ -203,6 +203,9 @@ __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
         store_row<CP>(o + base, a.cp, lane, am);
         store_row<CP>(o + base + a.cp, a.cp, lane, ad);
     }
+    // zero the row padding [K, ldo): the GEMMs run over the padded width
+    const int kk = JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
+    if (lane < a.ldo - kk) o[kk + lane] = 0.f;
 }
 
 static int cpl_of(int c) {

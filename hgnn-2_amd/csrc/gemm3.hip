@@ -67,9 +67,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
     if (m0 >= Mv && !(EPI == E3_DA_BN && blockIdx.x == 0 && blockIdx.y == 0)) return;
     const int K = p.k, N = p.n;
 
-    // The k tail (K % 4 != 0: the padding columns of the aggregate) is zeroed when the
-    // staged registers are written to LDS, not right after the load: masking there
-    // makes the compiler wait for every load at once (vmcnt(0)) and kills the prefetch.
+    // K % 4 == 0 (host-checked): a float4 is wholly inside or outside the k range, so the
+    // loads' range checks are the only masking (the forward GEMM runs over the padded width kp,
+    // whose padding columns are zero in both operands).  A per-element tail select in the
+    // staging doubled the k-loop's instruction count (321 vs 204 per k-step) and cost ~5 us
+    // per launch (tools/gemm_lab.hip).
     float4 ra[AF4], rb[BF4];
     float4 rz[EPI == E3_DA_BN ? AF4 : 1];
     // E3_DA_BN: per-channel affine form of the BN backward, dY = ca dz + cb (y - mu) + ce
@@ -125,40 +127,39 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
         }
         return make_float4(d[0], d[1], d[2], d[3]);
     };
-    auto mask_tail = [](float4 v, int gk, int kend) {
-        if (gk + 3 >= kend) {
-            if (gk >= kend) v.x = 0.f;
-            if (gk + 1 >= kend) v.y = 0.f;
-            if (gk + 2 >= kend) v.z = 0.f;
-            v.w = 0.f;
-        }
-        return v;
+    // Loads are unconditional buffer loads: an out-of-range float4 gets an out-of-bounds offset
+    // and reads 0 in hardware.  A conditional load made the compiler merge the loaded and the
+    // zero value with register moves straight after the load, i.e. a vmcnt(0) in the middle of
+    // the prefetch (seen in the .s of the forward variant); a select at the LDS store moved the
+    // staging arrays to scratch; a pointer select with a zero constant became flat loads.
+    // buffer resources over the valid rows: an out-of-range float4 gets offset OOB and reads 0
+    constexpr unsigned OOB = 0x7ffffff0u;
+    const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.a), 0, Mv * p.lda * 4, 0x00020000);
+    const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.b), 0, N * p.ldb * 4, 0x00020000);
+    const auto rs_z = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(EPI == E3_DA_BN ? p.dz : p.a), 0,
+                                                        Mv * p.lda * 4, 0x00020000);
+    auto ld4 = [](__amdgpu_buffer_rsrc_t r, unsigned off) {
+        return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
     };
     auto load = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < AF4; ++i) {
             const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
             const int gm = m0 + row, gk = k0 + kq;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (gm < Mv && gk < K) v = *reinterpret_cast<const float4*>(p.a + (long long)gm * p.lda + gk);
-            ra[i] = v;
-            if constexpr (EPI == E3_DA_BN) {
-                float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (gm < Mv && gk < K) z = *reinterpret_cast<const float4*>(p.dz + (long long)gm * p.lda + gk);
-                rz[i] = z;
-            }
+            const unsigned off = (gm < Mv && gk < K) ? (unsigned)(gm * p.lda + gk) * 4u : OOB;
+            ra[i] = ld4(rs_a, off);
+            if constexpr (EPI == E3_DA_BN) rz[i] = ld4(rs_z, off);
         }
 #pragma unroll
         for (int i = 0; i < BF4; ++i) {
             const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
             const int gn = n0 + row, gk = k0 + kq;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (gn < N && gk < K) v = *reinterpret_cast<const float4*>(p.b + (long long)gn * p.ldb + gk);
-            rb[i] = v;
+            const unsigned off = (gn < N && gk < K) ? (unsigned)(gn * p.ldb + gk) * 4u : OOB;
+            rb[i] = ld4(rs_b, off);
         }
     };
     auto store = [&](int buf, int k0) {
-        const bool tail = k0 + BK > K;
+        (void)k0;
 #pragma unroll
         for (int i = 0; i < AF4; ++i) {
             const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
@@ -185,13 +186,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
                     }
                 }
             } else {
-                *reinterpret_cast<float4*>(&As[buf][row * LDK + kq]) = tail ? mask_tail(ra[i], k0 + kq, K) : ra[i];
+                *reinterpret_cast<float4*>(&As[buf][row * LDK + kq]) = ra[i];
             }
         }
 #pragma unroll
         for (int i = 0; i < BF4; ++i) {
             const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
-            *reinterpret_cast<float4*>(&Bs[buf][row * LDK + kq]) = tail ? mask_tail(rb[i], k0 + kq, K) : rb[i];
+            *reinterpret_cast<float4*>(&Bs[buf][row * LDK + kq]) = rb[i];
         }
     };
 
@@ -517,6 +518,8 @@ bool gemm3_ok(int lda, int ldb, int ldc, const void* a, const void* b) {
 int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const float* wc, int ldw, int n,
                      const float* bias, int relu_from, float* y, int ldy, float* bn_part, hipStream_t s) {
     if (m_cap <= 0) return 0;
+    if (k % 4 != 0) return HGNN_ERR_UNSUPPORTED;  // pass the padded width (zero padding in both operands)
+    if ((long long)m_cap * lda * 4 >= (1ll << 31) || (long long)n * ldw * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     G3 p{};
     p.a = a;
     p.lda = lda;
@@ -546,6 +549,8 @@ int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int
 int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, int o, const float* wt, int ldw,
                     int kout, float* da, int ldda, hipStream_t s) {
     if (m_cap <= 0) return 0;
+    if (o % 4 != 0) return HGNN_ERR_UNSUPPORTED;
+    if ((long long)m_cap * lddy * 4 >= (1ll << 31) || (long long)kout * ldw * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     G3 p{};
     p.a = dy;
     p.lda = lddy;

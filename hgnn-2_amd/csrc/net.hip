@@ -436,7 +436,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
         TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
 
         if (P.v2) {
-            TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.k, at<float>(ws, h.wc), h.kp,
+            TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<float>(ws, h.wc), h.kp,
                                                  P.c2, at<float>(ws, h.bc), h.relu_from,
                                                  at<float>(ws, P.feats[h.out].y), P.c2,
                                                  c->training ? at<float>(ws, h.part) : nullptr, s));

@@ -237,3 +237,27 @@ def test_csr_batch_path_equals_dense_path(kind, order):
     for (n, m1), (_, m2) in zip(model.named_modules(), twin.named_modules()):
         if hasattr(m1, "running_mean") and torch.is_tensor(getattr(m1, "running_mean")):
             assert torch.equal(m1.running_mean.cpu(), m2.running_mean.cpu()), n
+
+
+def test_gnn_lg_d128_config4_model_vs_oracle_fp64():
+    """Config-4 model width (d = 128: 2d = 256 output channels, two 128-column GEMM tiles, 4-channel
+    lanes in the aggregation) on a 48-graph batch against the fp64 oracle."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_lg
+    graphs = dg.qm9_shape_dataset(48, seed=12)
+    b = _batch(graphs)
+    model = GNN_lg(0, 128, 4, 5, 1, 1, 2).cuda()
+    fu.det_init(model, 128)
+    ref_out, ref_loss, ref_g, ref_dx = _oracle_lg(model, b, 4, 2)
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _cuda(b)
+    X.requires_grad_(True)
+    out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+    torch.nn.MSELoss()(out, T).backward()
+    o = out.detach().cpu().double()
+    assert torch.max(torch.abs(o - ref_out)).item() <= 2e-5 * max(1.0, ref_out.abs().max().item())
+    gmax = max(g.abs().max().item() for g in ref_g.values())
+    for k, p in model.named_parameters():
+        err = (p.grad.cpu().double() - ref_g[k]).abs()
+        assert torch.all(err <= 1e-4 * gmax + 1e-5 * ref_g[k].abs()), (k, err.max().item(), gmax)
+    err = (X.grad.cpu().double() - ref_dx).abs().max().item()
+    assert err <= 1e-4 * max(1.0, ref_dx.abs().max().item())

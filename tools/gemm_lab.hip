@@ -507,6 +507,8 @@ int main() {
         {"edge_fwd", 23296, 128, 640},
         {"edge_dA", 23296, 640, 128},
         {"node_dA", 9728, 640, 128},
+        {"bal256_fwd", 16384, 128, 640},  // exactly 256 tiles of 64 rows: no tail imbalance
+        {"bal512_fwd", 32768, 128, 640},  // 512 tiles: two per CU
     };
     for (const Shape& sh : shapes) {
         const long long na = (long long)sh.M * sh.K, nb = (long long)sh.N * sh.K, nc = (long long)sh.M * sh.N;
@@ -581,6 +583,14 @@ int main() {
                 launch_gemm3_fwd(Abig, sh.K, mv, cap, sh.K, B, sh.K, sh.N, bias, sh.N / 2, C, sh.N, nullptr, s);
             };
             auto lib_da = [&]() { launch_gemm3_da(Abig, sh.K, mv, cap, sh.K, B, sh.K, sh.N, C, sh.N, s); };
+            auto lib_exact = [&]() {
+                launch_gemm3_fwd(Abig, sh.K, nullptr, sh.M, sh.K, B, sh.K, sh.N, bias, sh.N / 2, C, sh.N, nullptr, s);
+            };
+            auto lib_exact_part = [&]() {
+                launch_gemm3_fwd(Abig, sh.K, nullptr, sh.M, sh.K, B, sh.K, sh.N, bias, sh.N / 2, C, sh.N, part, s);
+            };
+            timeit("lib gemm3_fwd (exact M, no m_valid, no part)", lib_exact, 20);
+            timeit("lib gemm3_fwd (exact M, no m_valid, part)", lib_exact_part, 20);
             timeit("lib gemm3_fwd (m_valid, bn_part)", lib_fwd, 20);
             timeit("lib gemm3_fwd (m_valid, no part)", lib_nopart, 20);
             timeit("lib gemm3_da  (m_valid)", lib_da, 20);
