@@ -67,7 +67,7 @@ def _raise_bits(bits):
 
 def check_errors(block=True):
     """Raise if any enqueued forward found an invalid input batch."""
-    if torch.cuda.is_current_stream_capturing():
+    if _capturing():
         return
     keep = []
     bad = 0
@@ -82,8 +82,12 @@ def check_errors(block=True):
         _raise_bits(bad)
 
 
+def _capturing():
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 def _watch_error_word(cfg, ws):
-    if torch.cuda.is_current_stream_capturing():
+    if _capturing():
         # inside a HIP graph capture (bench.py --graph): the batch was validated by the eager
         # warm-up steps; no host-visible check can be part of a replayed graph
         return
