@@ -269,7 +269,7 @@ __global__ void __launch_bounds__(256) k_agg_bwd(AggBwdArgs a) {
     if constexpr (HG) {
         const RowInfo ri = a.g.rows[r];
         const int stride = a.g.stride;
-        constexpr int UB = 2;  // entries in flight (x JT slices each)
+        constexpr int UB = 4;  // entries in flight (x the slices with a nonzero coefficient)
         for (int e0 = 0; e0 < ri.count; e0 += 64) {
             const int n = min(64, ri.count - e0);
             const float4 me = lane_entry(a.g.entries, stride, ri.start + e0, n, lane);
@@ -292,8 +292,18 @@ __global__ void __launch_bounds__(256) k_agg_bwd(AggBwdArgs a) {
 #pragma unroll
                     for (int j = 3; j < JT; ++j) v[u][j] = live ? bcast(mx[j - 3], eu) : 0.f;
                     const float* src = a.ing + (long long)col * a.ldg + a.gofs;
+                    // slices with a zero coefficient are skipped (wave-uniform): I and D live on the
+                    // diagonal entry only and A^k has no diagonal in general, so an entry needs 1-2
+                    // of its J+2 gradient blocks -- about half the gathered bytes
 #pragma unroll
-                    for (int j = 0; j < JT; ++j) load_row<C>(src + j * a.c, a.c, lane, x[u][j]);
+                    for (int j = 0; j < JT; ++j) {
+                        if (v[u][j] != 0.f) {
+                            load_row<C>(src + j * a.c, a.c, lane, x[u][j]);
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < C; ++i) x[u][j][i] = 0.f;
+                        }
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < UB; ++u)
