@@ -16,25 +16,23 @@
 //                                + sum_e Pm * dA[col, m_off + c] + Pd * dA[col, d_off + c].
 #include "kernels.h"
 
+#include <initializer_list>
+
 namespace hgnn {
 
-template <int CPL>
+// Row loads / stores of one wave (lane owns channels lane*CPL ..).  V = the host checked that
+// C == 64*CPL and every row address is aligned for the vector width (the executor's layouts
+// always are), so the vector form is straight-line code; otherwise a guarded scalar form.
+template <int CPL, bool V>
 __device__ __forceinline__ void load_row(const float* __restrict__ p, int C, int lane, float (&x)[CPL]) {
     const int c0 = lane * CPL;
-    constexpr uintptr_t AL = (CPL >= 4 ? 16 : 4 * CPL) - 1;
-    if (C == 64 * CPL && (reinterpret_cast<uintptr_t>(p) & AL) == 0) {
+    if constexpr (V) {
         if constexpr (CPL == 1) {
             x[0] = p[c0];
         } else if constexpr (CPL == 2) {
             const float2 v = *reinterpret_cast<const float2*>(p + c0);
             x[0] = v.x;
             x[1] = v.y;
-        } else if constexpr (CPL == 4) {
-            const float4 v = *reinterpret_cast<const float4*>(p + c0);
-            x[0] = v.x;
-            x[1] = v.y;
-            x[2] = v.z;
-            x[3] = v.w;
         } else {
 #pragma unroll
             for (int i = 0; i < CPL; i += 4) {
@@ -51,11 +49,10 @@ __device__ __forceinline__ void load_row(const float* __restrict__ p, int C, int
     }
 }
 
-template <int CPL>
+template <int CPL, bool V>
 __device__ __forceinline__ void store_row(float* __restrict__ p, int C, int lane, const float (&x)[CPL]) {
     const int c0 = lane * CPL;
-    constexpr uintptr_t AL = (CPL >= 4 ? 16 : 4 * CPL) - 1;
-    if (C == 64 * CPL && (reinterpret_cast<uintptr_t>(p) & AL) == 0) {
+    if constexpr (V) {
         if constexpr (CPL == 1) {
             p[c0] = x[0];
         } else if constexpr (CPL == 2) {
@@ -70,6 +67,17 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, int C, int lane
         for (int i = 0; i < CPL; ++i)
             if (c0 + i < C) p[c0 + i] = x[i];
     }
+}
+
+// Host side of V: channel count fills the lanes exactly, base pointers and every offset /
+// leading dimension keep the vector alignment.
+static bool vec_ok(int cpl, int c, const void* base, std::initializer_list<long long> offs) {
+    if (c != 64 * cpl) return false;
+    const int w = cpl >= 4 ? 4 : cpl;  // floats per vector access
+    if (reinterpret_cast<uintptr_t>(base) % (4 * w)) return false;
+    for (long long o : offs)
+        if (o % w) return false;
+    return true;
 }
 
 // Entry lists are fetched lane-parallel (lane e holds entry e of a 64-entry chunk)
@@ -113,95 +121,112 @@ struct LaneBn {
     }
 };
 
-template <int JT, int CG, int CP>
+template <int JT, int CG, int CP, bool V>
 __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
     const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     if (r >= *a.total_rows) return;
     float* o = a.out + (long long)r * a.ldo;
-    if constexpr (CG > 0) {
-        float acc[JT][CG];
+    constexpr int CGx = CG > 0 ? CG : 1, CPx = CP > 0 ? CP : 1;
+    float acc[JT][CGx], am[CPx], ad[CPx];
 #pragma unroll
-        for (int j = 0; j < JT; ++j)
+    for (int j = 0; j < JT; ++j)
 #pragma unroll
-            for (int i = 0; i < CG; ++i) acc[j][i] = 0.f;
-        const RowInfo ri = a.g.rows[r];
-        const int stride = a.g.stride;
-        LaneBn<CG> bn;
-        bn.init(a.gbn, a.cg, lane);
-        for (int e0 = 0; e0 < ri.count; e0 += 64) {
-            const int n = min(64, ri.count - e0);
+        for (int i = 0; i < CGx; ++i) acc[j][i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPx; ++i) am[i] = ad[i] = 0.f;
+    // The G and P chains (row info -> entry chunk -> feature gathers) run interleaved: both
+    // row infos, then both entry chunks, then the gathers of both lists in one batch, so a
+    // row costs ~3 dependent memory round trips instead of 6.
+    RowInfo rg{0, 0}, rp{0, 0};
+    if constexpr (CG > 0) rg = a.g.rows[r];
+    if constexpr (CP > 0) rp = a.p.rows[r];
+    LaneBn<CGx> bng;
+    LaneBn<CPx> bnp;
+    if constexpr (CG > 0) bng.init(a.gbn, a.cg, lane);
+    if constexpr (CP > 0) bnp.init(a.pbn, a.cp, lane);
+    const int stride = a.g.stride;
+    const int nmax = max(rg.count, rp.count);
+    for (int e0 = 0; e0 < nmax; e0 += 64) {
+        const int ng = min(64, max(0, rg.count - e0)), np = min(64, max(0, rp.count - e0));
+        float4 mg = make_float4(0.f, 0.f, 0.f, 0.f), mp = mg;
+        float mx[JT > 3 ? JT - 3 : 1];
+        if constexpr (CG > 0) {
             // JT <= 3: one float4 per entry; larger JT reads the extra coefficients below
-            const float4 me = lane_entry(a.g.entries, stride, ri.start + e0, n, lane);
-            float mx[JT > 3 ? JT - 3 : 1];
+            mg = lane_entry(a.g.entries, stride, rg.start + e0, ng, lane);
             if constexpr (JT > 3) {
 #pragma unroll
                 for (int j = 3; j < JT; ++j)
-                    mx[j - 3] = lane < n ? a.g.entries[(long long)(ri.start + e0 + lane) * stride + 1 + j] : 0.f;
+                    mx[j - 3] = lane < ng ? a.g.entries[(long long)(rg.start + e0 + lane) * stride + 1 + j] : 0.f;
             }
-            for (int e = 0; e < n; e += AGG_U) {
-                float x[AGG_U][CG];
-                float v[AGG_U][JT];
+        }
+        if constexpr (CP > 0) mp = lane_entry(a.p.entries, 4, rp.start + e0, np, lane);
+        const int nn = max(ng, np);
+        for (int e = 0; e < nn; e += AGG_U) {
+            float xg[AGG_U][CGx], v[AGG_U][JT], xp[AGG_U][CPx], vm[AGG_U], vd[AGG_U];
+            if constexpr (CG > 0) {
 #pragma unroll
                 for (int u = 0; u < AGG_U; ++u) {
-                    const int eu = min(e + u, n - 1);
-                    const int col = __builtin_amdgcn_readlane(__float_as_int(me.x), eu);
-                    const bool live = e + u < n;
-                    v[u][0] = live ? bcast(me.y, eu) : 0.f;
-                    if constexpr (JT > 1) v[u][1] = live ? bcast(me.z, eu) : 0.f;
-                    if constexpr (JT > 2) v[u][2] = live ? bcast(me.w, eu) : 0.f;
+                    // dead slots re-read the last live row with zero coefficients (no branch)
+                    const int eu = max(0, min(e + u, ng - 1));
+                    const int col = __builtin_amdgcn_readlane(__float_as_int(mg.x), eu);
+                    const bool live = e + u < ng;
+                    v[u][0] = live ? bcast(mg.y, eu) : 0.f;
+                    if constexpr (JT > 1) v[u][1] = live ? bcast(mg.z, eu) : 0.f;
+                    if constexpr (JT > 2) v[u][2] = live ? bcast(mg.w, eu) : 0.f;
 #pragma unroll
                     for (int j = 3; j < JT; ++j) v[u][j] = live ? bcast(mx[j - 3], eu) : 0.f;
-                    load_row<CG>(a.xg + (long long)col * a.cg, a.cg, lane, x[u]);
-                }
+                    if (ng > 0) load_row<CG, V>(a.xg + (long long)col * a.cg, a.cg, lane, xg[u]);
+                    else
 #pragma unroll
-                for (int u = 0; u < AGG_U; ++u) bn.apply(x[u]);
+                        for (int i = 0; i < CG; ++i) xg[u][i] = 0.f;
+                }
+            }
+            if constexpr (CP > 0) {
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u) {
+                    const int eu = max(0, min(e + u, np - 1));
+                    const int col = __builtin_amdgcn_readlane(__float_as_int(mp.x), eu);
+                    const bool live = e + u < np;
+                    vm[u] = live ? bcast(mp.y, eu) : 0.f;
+                    vd[u] = live ? bcast(mp.z, eu) : 0.f;
+                    if (np > 0) load_row<CP, V>(a.xp + (long long)col * a.cp, a.cp, lane, xp[u]);
+                    else
+#pragma unroll
+                        for (int i = 0; i < CP; ++i) xp[u][i] = 0.f;
+                }
+            }
+            if constexpr (CG > 0) {
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u) bng.apply(xg[u]);
 #pragma unroll
                 for (int u = 0; u < AGG_U; ++u)
 #pragma unroll
                     for (int j = 0; j < JT; ++j)
 #pragma unroll
-                        for (int i = 0; i < CG; ++i) acc[j][i] = fmaf(v[u][j], x[u][i], acc[j][i]);
+                        for (int i = 0; i < CG; ++i) acc[j][i] = fmaf(v[u][j], xg[u][i], acc[j][i]);
             }
-        }
+            if constexpr (CP > 0) {
 #pragma unroll
-        for (int j = 0; j < JT; ++j) store_row<CG>(o + j * a.cg, a.cg, lane, acc[j]);
-    }
-    if constexpr (CP > 0) {
-        float am[CP], ad[CP];
-#pragma unroll
-        for (int i = 0; i < CP; ++i) am[i] = ad[i] = 0.f;
-        const RowInfo ri = a.p.rows[r];
-        LaneBn<CP> bn;
-        bn.init(a.pbn, a.cp, lane);
-        for (int e0 = 0; e0 < ri.count; e0 += 64) {
-            const int n = min(64, ri.count - e0);
-            const float4 me = lane_entry(a.p.entries, 4, ri.start + e0, n, lane);
-            for (int e = 0; e < n; e += AGG_U) {
-                float x[AGG_U][CP], vm[AGG_U], vd[AGG_U];
-#pragma unroll
-                for (int u = 0; u < AGG_U; ++u) {
-                    const int eu = min(e + u, n - 1);
-                    const int col = __builtin_amdgcn_readlane(__float_as_int(me.x), eu);
-                    const bool live = e + u < n;
-                    vm[u] = live ? bcast(me.y, eu) : 0.f;
-                    vd[u] = live ? bcast(me.z, eu) : 0.f;
-                    load_row<CP>(a.xp + (long long)col * a.cp, a.cp, lane, x[u]);
-                }
-#pragma unroll
-                for (int u = 0; u < AGG_U; ++u) bn.apply(x[u]);
+                for (int u = 0; u < AGG_U; ++u) bnp.apply(xp[u]);
 #pragma unroll
                 for (int u = 0; u < AGG_U; ++u)
 #pragma unroll
                     for (int i = 0; i < CP; ++i) {
-                        am[i] = fmaf(vm[u], x[u][i], am[i]);
-                        ad[i] = fmaf(vd[u], x[u][i], ad[i]);
+                        am[i] = fmaf(vm[u], xp[u][i], am[i]);
+                        ad[i] = fmaf(vd[u], xp[u][i], ad[i]);
                     }
             }
         }
+    }
+    if constexpr (CG > 0) {
+#pragma unroll
+        for (int j = 0; j < JT; ++j) store_row<CG, V>(o + j * a.cg, a.cg, lane, acc[j]);
+    }
+    if constexpr (CP > 0) {
         const int base = JT * a.cg;
-        store_row<CP>(o + base, a.cp, lane, am);
-        store_row<CP>(o + base + a.cp, a.cp, lane, ad);
+        store_row<CP, V>(o + base, a.cp, lane, am);
+        store_row<CP, V>(o + base + a.cp, a.cp, lane, ad);
     }
     // zero the row padding [K, ldo): the GEMMs run over the padded width
     const int kk = JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
@@ -217,14 +242,24 @@ static int cpl_of(int c) {
     return -1;
 }
 
+template <int JT, int CG, int CP>
+static void agg_fwd_v(const AggFwdArgs& a, dim3 g, hipStream_t s) {
+    const int kk = JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
+    const bool v = vec_ok(CG, a.cg, a.xg, {}) && (CP == 0 || vec_ok(CP, a.cp, a.xp, {})) &&
+                   vec_ok(CG, a.cg, a.out, {a.ldo, (long long)kk}) &&
+                   (CP == 0 || vec_ok(CP, a.cp, a.out, {a.ldo, (long long)JT * a.cg, (long long)a.cp}));
+    if (v) hipLaunchKernelGGL((k_agg_fwd<JT, CG, CP, true>), g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_agg_fwd<JT, CG, CP, false>), g, dim3(256), 0, s, a);
+}
+
 template <int JT, int CG>
 static int agg_fwd_cp(const AggFwdArgs& a, dim3 g, hipStream_t s) {
     switch (cpl_of(a.xp ? a.cp : 0)) {
-        case 0: hipLaunchKernelGGL((k_agg_fwd<JT, CG, 0>), g, dim3(256), 0, s, a); break;
-        case 1: hipLaunchKernelGGL((k_agg_fwd<JT, CG, 1>), g, dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_agg_fwd<JT, CG, 2>), g, dim3(256), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_agg_fwd<JT, CG, 4>), g, dim3(256), 0, s, a); break;
-        case 8: hipLaunchKernelGGL((k_agg_fwd<JT, CG, 8>), g, dim3(256), 0, s, a); break;
+        case 0: agg_fwd_v<JT, CG, 0>(a, g, s); break;
+        case 1: agg_fwd_v<JT, CG, 1>(a, g, s); break;
+        case 2: agg_fwd_v<JT, CG, 2>(a, g, s); break;
+        case 4: agg_fwd_v<JT, CG, 4>(a, g, s); break;
+        case 8: agg_fwd_v<JT, CG, 8>(a, g, s); break;
         default: return 2;
     }
     HGNN_LAUNCH_CHECK();
@@ -253,124 +288,203 @@ int launch_agg_fwd(const AggFwdArgs& a, hipStream_t s) {
     }
 }
 
-template <int JT, int C, bool HG, bool HP>
-__global__ void __launch_bounds__(256) k_agg_bwd(AggBwdArgs a) {
-    const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    const int lane = threadIdx.x & 63;
-    if (r >= *a.total_rows) return;
+// Backward gathers.  The G gather (transposed operator lists, output = the gradient of the
+// half's own features) and the P gather (transposed Pm/Pd lists, output = the other kind's
+// features) write different tensors; launch_agg_bwd_pair runs both in one grid (blocks
+// [0, gb) gather G, the rest P), so neither runs alone on a partly filled chip.
+template <int JT, int C, bool V>
+__device__ __forceinline__ void agg_bwd_g(const AggBwdArgs& a, int r, int lane) {
     float acc[C];
     float* o = a.out + (long long)r * a.ldo;
     if (a.accumulate) {
-        load_row<C>(o, a.c, lane, acc);
+        load_row<C, V>(o, a.c, lane, acc);
     } else {
 #pragma unroll
         for (int i = 0; i < C; ++i) acc[i] = 0.f;
     }
-    if constexpr (HG) {
-        const RowInfo ri = a.g.rows[r];
-        const int stride = a.g.stride;
-        constexpr int UB = 4;  // entries in flight (x the slices with a nonzero coefficient)
-        for (int e0 = 0; e0 < ri.count; e0 += 64) {
-            const int n = min(64, ri.count - e0);
-            const float4 me = lane_entry(a.g.entries, stride, ri.start + e0, n, lane);
-            float mx[JT > 3 ? JT - 3 : 1];
-            if constexpr (JT > 3) {
+    const RowInfo ri = a.g.rows[r];
+    const int stride = a.g.stride;
+    constexpr int UB = 4;  // entries in flight (x the slices with a nonzero coefficient)
+    for (int e0 = 0; e0 < ri.count; e0 += 64) {
+        const int n = min(64, ri.count - e0);
+        const float4 me = lane_entry(a.g.entries, stride, ri.start + e0, n, lane);
+        float mx[JT > 3 ? JT - 3 : 1];
+        if constexpr (JT > 3) {
 #pragma unroll
-                for (int j = 3; j < JT; ++j)
-                    mx[j - 3] = lane < n ? a.g.entries[(long long)(ri.start + e0 + lane) * stride + 1 + j] : 0.f;
-            }
-            for (int e = 0; e < n; e += UB) {
-                float x[UB][JT][C], v[UB][JT];
+            for (int j = 3; j < JT; ++j)
+                mx[j - 3] = lane < n ? a.g.entries[(long long)(ri.start + e0 + lane) * stride + 1 + j] : 0.f;
+        }
+        for (int e = 0; e < n; e += UB) {
+            float x[UB][JT][C], v[UB][JT];
 #pragma unroll
-                for (int u = 0; u < UB; ++u) {
-                    const int eu = min(e + u, n - 1);
-                    const int col = __builtin_amdgcn_readlane(__float_as_int(me.x), eu);
-                    const bool live = e + u < n;
-                    v[u][0] = live ? bcast(me.y, eu) : 0.f;
-                    if constexpr (JT > 1) v[u][1] = live ? bcast(me.z, eu) : 0.f;
-                    if constexpr (JT > 2) v[u][2] = live ? bcast(me.w, eu) : 0.f;
+            for (int u = 0; u < UB; ++u) {
+                const int eu = min(e + u, n - 1);
+                const int col = __builtin_amdgcn_readlane(__float_as_int(me.x), eu);
+                const bool live = e + u < n;
+                v[u][0] = live ? bcast(me.y, eu) : 0.f;
+                if constexpr (JT > 1) v[u][1] = live ? bcast(me.z, eu) : 0.f;
+                if constexpr (JT > 2) v[u][2] = live ? bcast(me.w, eu) : 0.f;
 #pragma unroll
-                    for (int j = 3; j < JT; ++j) v[u][j] = live ? bcast(mx[j - 3], eu) : 0.f;
-                    const float* src = a.ing + (long long)col * a.ldg + a.gofs;
-                    // slices with a zero coefficient are skipped (wave-uniform): I and D live on the
-                    // diagonal entry only and A^k has no diagonal in general, so an entry needs 1-2
-                    // of its J+2 gradient blocks -- about half the gathered bytes
+                for (int j = 3; j < JT; ++j) v[u][j] = live ? bcast(mx[j - 3], eu) : 0.f;
+                const float* src = a.ing + (long long)col * a.ldg + a.gofs;
+                // slices with a zero coefficient are skipped (wave-uniform): I and D live on the
+                // diagonal entry only and A^k has no diagonal in general, so an entry needs 1-2
+                // of its J+2 gradient blocks -- about half the gathered bytes
 #pragma unroll
-                    for (int j = 0; j < JT; ++j) {
-                        if (v[u][j] != 0.f) {
-                            load_row<C>(src + j * a.c, a.c, lane, x[u][j]);
-                        } else {
+                for (int j = 0; j < JT; ++j) {
+                    if (v[u][j] != 0.f) {
+                        load_row<C, V>(src + j * a.c, a.c, lane, x[u][j]);
+                    } else {
 #pragma unroll
-                            for (int i = 0; i < C; ++i) x[u][j][i] = 0.f;
-                        }
+                        for (int i = 0; i < C; ++i) x[u][j][i] = 0.f;
                     }
                 }
-#pragma unroll
-                for (int u = 0; u < UB; ++u)
-#pragma unroll
-                    for (int j = 0; j < JT; ++j)
-#pragma unroll
-                        for (int i = 0; i < C; ++i) acc[i] = fmaf(v[u][j], x[u][j][i], acc[i]);
             }
+#pragma unroll
+            for (int u = 0; u < UB; ++u)
+#pragma unroll
+                for (int j = 0; j < JT; ++j)
+#pragma unroll
+                    for (int i = 0; i < C; ++i) acc[i] = fmaf(v[u][j], x[u][j][i], acc[i]);
         }
     }
-    if constexpr (HP) {
-        const RowInfo ri = a.p.rows[r];
-        for (int e0 = 0; e0 < ri.count; e0 += 64) {
-            const int n = min(64, ri.count - e0);
-            const float4 me = lane_entry(a.p.entries, 4, ri.start + e0, n, lane);
-            for (int e = 0; e < n; e += AGG_U) {
-                float xm[AGG_U][C], xd[AGG_U][C], vm[AGG_U], vd[AGG_U];
+    store_row<C, V>(o, a.c, lane, acc);
+}
+
+template <int C, bool V>
+__device__ __forceinline__ void agg_bwd_p(const AggBwdArgs& a, int r, int lane) {
+    float acc[C];
+    float* o = a.out + (long long)r * a.ldo;
+    if (a.accumulate) {
+        load_row<C, V>(o, a.c, lane, acc);
+    } else {
 #pragma unroll
-                for (int u = 0; u < AGG_U; ++u) {
-                    const int eu = min(e + u, n - 1);
-                    const int col = __builtin_amdgcn_readlane(__float_as_int(me.x), eu);
-                    const bool live = e + u < n;
-                    vm[u] = live ? bcast(me.y, eu) : 0.f;
-                    vd[u] = live ? bcast(me.z, eu) : 0.f;
-                    const float* src = a.inp + (long long)col * a.ldp;
-                    load_row<C>(src + a.pofs_m, a.c, lane, xm[u]);
-                    load_row<C>(src + a.pofs_d, a.c, lane, xd[u]);
-                }
+        for (int i = 0; i < C; ++i) acc[i] = 0.f;
+    }
+    const RowInfo ri = a.p.rows[r];
+    for (int e0 = 0; e0 < ri.count; e0 += 64) {
+        const int n = min(64, ri.count - e0);
+        const float4 me = lane_entry(a.p.entries, 4, ri.start + e0, n, lane);
+        for (int e = 0; e < n; e += AGG_U) {
+            float xm[AGG_U][C], xd[AGG_U][C], vm[AGG_U], vd[AGG_U];
 #pragma unroll
-                for (int u = 0; u < AGG_U; ++u)
-#pragma unroll
-                    for (int i = 0; i < C; ++i) acc[i] = fmaf(vd[u], xd[u][i], fmaf(vm[u], xm[u][i], acc[i]));
+            for (int u = 0; u < AGG_U; ++u) {
+                const int eu = min(e + u, n - 1);
+                const int col = __builtin_amdgcn_readlane(__float_as_int(me.x), eu);
+                const bool live = e + u < n;
+                vm[u] = live ? bcast(me.y, eu) : 0.f;
+                vd[u] = live ? bcast(me.z, eu) : 0.f;
+                const float* src = a.inp + (long long)col * a.ldp;
+                load_row<C, V>(src + a.pofs_m, a.c, lane, xm[u]);
+                load_row<C, V>(src + a.pofs_d, a.c, lane, xd[u]);
             }
+#pragma unroll
+            for (int u = 0; u < AGG_U; ++u)
+#pragma unroll
+                for (int i = 0; i < C; ++i) acc[i] = fmaf(vd[u], xd[u][i], fmaf(vm[u], xm[u][i], acc[i]));
         }
     }
-    store_row<C>(o, a.c, lane, acc);
+    store_row<C, V>(o, a.c, lane, acc);
+}
+
+// MODE 1: G only (ga); 2: P only (pa); 3: blocks [0, gb) G on ga, the rest P on pa.
+template <int JT, int CG, int CP, bool V, int MODE>
+__global__ void __launch_bounds__(256) k_agg_bwd(AggBwdArgs ga, AggBwdArgs pa, int gb) {
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    if (MODE == 1 || (MODE == 3 && (int)blockIdx.x < gb)) {
+        if constexpr (MODE != 2) {
+            const int r = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wv);
+            if (r >= *ga.total_rows) return;
+            agg_bwd_g<JT, CG, V>(ga, r, lane);
+        }
+    } else {
+        if constexpr (MODE != 1) {
+            const int r = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - (MODE == 3 ? gb : 0)) * 4 + wv);
+            if (r >= *pa.total_rows) return;
+            agg_bwd_p<CP, V>(pa, r, lane);
+        }
+    }
+}
+
+static bool bwd_vec_g(int cpl, const AggBwdArgs& a) {
+    return vec_ok(cpl, a.c, a.ing, {a.ldg, a.gofs}) && vec_ok(cpl, a.c, a.out, {a.ldo});
+}
+static bool bwd_vec_p(int cpl, const AggBwdArgs& a) {
+    return vec_ok(cpl, a.c, a.inp, {a.ldp, a.pofs_m, a.pofs_d}) && vec_ok(cpl, a.c, a.out, {a.ldo});
 }
 
 template <int JT, int C>
-static int agg_bwd_parts(const AggBwdArgs& a, dim3 g, hipStream_t s) {
-    const bool hg = a.ing != nullptr, hp = a.inp != nullptr;
-    if (hg && hp) hipLaunchKernelGGL((k_agg_bwd<JT, C, true, true>), g, dim3(256), 0, s, a);
-    else if (hg) hipLaunchKernelGGL((k_agg_bwd<JT, C, true, false>), g, dim3(256), 0, s, a);
-    else if (hp) hipLaunchKernelGGL((k_agg_bwd<JT, C, false, true>), g, dim3(256), 0, s, a);
-    else return 1;
+static int agg_bwd_single(const AggBwdArgs& a, hipStream_t s) {
+    const dim3 g(ceil_div(a.cap_rows, 4));
+    if (a.ing) {
+        if (bwd_vec_g(C, a)) hipLaunchKernelGGL((k_agg_bwd<JT, C, C, true, 1>), g, dim3(256), 0, s, a, a, 0);
+        else hipLaunchKernelGGL((k_agg_bwd<JT, C, C, false, 1>), g, dim3(256), 0, s, a, a, 0);
+    } else {
+        if (bwd_vec_p(C, a)) hipLaunchKernelGGL((k_agg_bwd<3, C, C, true, 2>), g, dim3(256), 0, s, a, a, 0);
+        else hipLaunchKernelGGL((k_agg_bwd<3, C, C, false, 2>), g, dim3(256), 0, s, a, a, 0);
+    }
     HGNN_LAUNCH_CHECK();
     return 0;
 }
 
 template <int JT>
-static int agg_bwd_c(const AggBwdArgs& a, dim3 g, hipStream_t s) {
+static int agg_bwd_c(const AggBwdArgs& a, hipStream_t s) {
     switch (cpl_of(a.c)) {
-        case 1: return agg_bwd_parts<JT, 1>(a, g, s);
-        case 2: return agg_bwd_parts<JT, 2>(a, g, s);
-        case 4: return agg_bwd_parts<JT, 4>(a, g, s);
-        case 8: return agg_bwd_parts<JT, 8>(a, g, s);
+        case 1: return agg_bwd_single<JT, 1>(a, s);
+        case 2: return agg_bwd_single<JT, 2>(a, s);
+        case 4: return agg_bwd_single<JT, 4>(a, s);
+        case 8: return agg_bwd_single<JT, 8>(a, s);
         default: return 2;
     }
 }
 
 int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s) {
     if (a.cap_rows <= 0) return 0;
-    const dim3 g(ceil_div(a.cap_rows, 4));
+    if ((a.ing != nullptr) == (a.inp != nullptr)) return 1;  // exactly one of the two gathers
     switch (a.jtot) {
-        case 3: return agg_bwd_c<3>(a, g, s);
-        case 4: return agg_bwd_c<4>(a, g, s);
-        case 5: return agg_bwd_c<5>(a, g, s);
+        case 3: return agg_bwd_c<3>(a, s);
+        case 4: return agg_bwd_c<4>(a, s);
+        case 5: return agg_bwd_c<5>(a, s);
+        default: return 2;
+    }
+}
+
+template <int JT, int C>
+static int agg_bwd_pair_c(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t s) {
+    const int gb = ceil_div(ga.cap_rows, 4), pb = ceil_div(pa.cap_rows, 4);
+    hipLaunchKernelGGL((k_agg_bwd<JT, C, C, true, 3>), dim3(gb + pb), dim3(256), 0, s, ga, pa, gb);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int JT>
+static int agg_bwd_pair_j(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t s) {
+    switch (cpl_of(ga.c)) {
+        case 1: return agg_bwd_pair_c<JT, 1>(ga, pa, s);
+        case 2: return agg_bwd_pair_c<JT, 2>(ga, pa, s);
+        case 4: return agg_bwd_pair_c<JT, 4>(ga, pa, s);
+        case 8: return agg_bwd_pair_c<JT, 8>(ga, pa, s);
+        default: return 2;
+    }
+}
+
+int launch_agg_bwd_pair(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t s) {
+    // one grid for both gathers when they share the lane layout and the vector path;
+    // otherwise two launches
+    const int cpl = cpl_of(ga.c);
+    const bool pair = ga.ing && !ga.inp && pa.inp && !pa.ing && ga.cap_rows > 0 && pa.cap_rows > 0 &&
+                      cpl > 0 && cpl == cpl_of(pa.c) && ga.jtot == pa.jtot && bwd_vec_g(cpl, ga) &&
+                      bwd_vec_p(cpl, pa);
+    if (!pair) {
+        int r = launch_agg_bwd(ga, s);
+        if (r) return r;
+        return launch_agg_bwd(pa, s);
+    }
+    switch (ga.jtot) {
+        case 3: return agg_bwd_pair_j<3>(ga, pa, s);
+        case 4: return agg_bwd_pair_j<4>(ga, pa, s);
+        case 5: return agg_bwd_pair_j<5>(ga, pa, s);
         default: return 2;
     }
 }

@@ -105,7 +105,10 @@ struct AggBwdArgs {
     int ldo;
     int accumulate;
 };
-int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s);
+int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s);  // exactly one of ing / inp
+// the G gather of ga and the P gather of pa (different outputs) in one grid when they
+// share the lane layout, else two launches
+int launch_agg_bwd_pair(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t s);
 
 // ---------------------------------------------------------------- GEMM (fp32 MFMA)
 // Y = A . W^T + bias, relu on cols >= relu_from, BN partials over valid rows.

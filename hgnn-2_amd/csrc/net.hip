@@ -604,40 +604,41 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
                                   da, s));
         if (need_dw) TL(HGNN_K_DW_DENSE, dw_dense(P.last_gin, da, P.k_last, true, 0));
         const int cg = P.feats[P.last_gin].c;
-        if (needs_grad(P.last_gin)) {
-            AggBwdArgs ab{};
-            ab.total_rows = tot_n;
-            ab.cap_rows = P.cap_n;
-            ab.g = src.v[S_WT];
-            ab.ing = da;
-            ab.ldg = P.k_last;
-            ab.gofs = 0;
-            ab.jtot = P.jt;
-            ab.c = cg;
-            ab.out = at<float>(ws, P.feats[P.last_gin].grad);
-            ab.ldo = cg;
-            ab.accumulate = init[P.last_gin];
-            TL(HGNN_K_AGG_BWD, launch_agg_bwd(ab, s));
-            init[P.last_gin] = 1;
+        const bool lg = needs_grad(P.last_gin), lp = needs_grad(P.last_pin);
+        AggBwdArgs gab{}, pab{};
+        if (lg) {
+            gab.total_rows = tot_n;
+            gab.cap_rows = P.cap_n;
+            gab.g = src.v[S_WT];
+            gab.ing = da;
+            gab.ldg = P.k_last;
+            gab.gofs = 0;
+            gab.jtot = P.jt;
+            gab.c = cg;
+            gab.out = at<float>(ws, P.feats[P.last_gin].grad);
+            gab.ldo = cg;
+            gab.accumulate = init[P.last_gin];
         }
-        if (needs_grad(P.last_pin)) {
+        if (lp) {
             const int cp = P.feats[P.last_pin].c;
-            AggBwdArgs ab{};
-            ab.total_rows = tot_e;
-            ab.cap_rows = P.cap_e;
-            ab.p = src.v[S_PE];
-            ab.inp = da;
-            ab.ldp = P.k_last;
-            ab.pofs_m = P.jt * cg;
-            ab.pofs_d = P.jt * cg + cp;
-            ab.jtot = P.jt;
-            ab.c = cp;
-            ab.out = at<float>(ws, P.feats[P.last_pin].grad);
-            ab.ldo = cp;
-            ab.accumulate = init[P.last_pin];
-            TL(HGNN_K_AGG_BWD, launch_agg_bwd(ab, s));
-            init[P.last_pin] = 1;
+            pab.total_rows = tot_e;
+            pab.cap_rows = P.cap_e;
+            pab.p = src.v[S_PE];
+            pab.inp = da;
+            pab.ldp = P.k_last;
+            pab.pofs_m = P.jt * cg;
+            pab.pofs_d = P.jt * cg + cp;
+            pab.jtot = P.jt;
+            pab.c = cp;
+            pab.out = at<float>(ws, P.feats[P.last_pin].grad);
+            pab.ldo = cp;
+            pab.accumulate = init[P.last_pin];
         }
+        if (lg && lp) TL(HGNN_K_AGG_BWD, launch_agg_bwd_pair(gab, pab, s));
+        else if (lg) TL(HGNN_K_AGG_BWD, launch_agg_bwd(gab, s));
+        else if (lp) TL(HGNN_K_AGG_BWD, launch_agg_bwd(pab, s));
+        if (lg) init[P.last_gin] = 1;
+        if (lp) init[P.last_pin] = 1;
     }
 
     SideStream* side = nullptr;
@@ -756,40 +757,40 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             TL(HGNN_K_GEMM_DA, launch_gemm_da(gd, s));
         }
         if (ndw && !P.v2) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, da, h.kp, false, 1));
+        AggBwdArgs gab{}, pab{};
         if (ng) {
-            AggBwdArgs ab{};
-            ab.total_rows = tot;
-            ab.cap_rows = cap;
-            ab.g = src.v[h.edge ? S_WLT : S_WT];
-            ab.ing = da;
-            ab.ldg = h.kp;
-            ab.gofs = 0;
-            ab.jtot = P.jt;
-            ab.c = h.cg;
-            ab.out = at<float>(ws, P.feats[h.gin].grad);
-            ab.ldo = h.cg;
-            ab.accumulate = init[h.gin];
-            TL(HGNN_K_AGG_BWD, launch_agg_bwd(ab, s));
-            init[h.gin] = 1;
+            gab.total_rows = tot;
+            gab.cap_rows = cap;
+            gab.g = src.v[h.edge ? S_WLT : S_WT];
+            gab.ing = da;
+            gab.ldg = h.kp;
+            gab.gofs = 0;
+            gab.jtot = P.jt;
+            gab.c = h.cg;
+            gab.out = at<float>(ws, P.feats[h.gin].grad);
+            gab.ldo = h.cg;
+            gab.accumulate = init[h.gin];
         }
         if (np) {
             const bool other_edge = !h.edge;
-            AggBwdArgs ab{};
-            ab.total_rows = other_edge ? tot_e : tot_n;
-            ab.cap_rows = other_edge ? P.cap_e : P.cap_n;
-            ab.p = src.v[h.edge ? S_PN : S_PE];
-            ab.inp = da;
-            ab.ldp = h.kp;
-            ab.pofs_m = P.jt * h.cg;
-            ab.pofs_d = P.jt * h.cg + h.cp;
-            ab.jtot = P.jt;
-            ab.c = h.cp;
-            ab.out = at<float>(ws, P.feats[h.pin].grad);
-            ab.ldo = h.cp;
-            ab.accumulate = init[h.pin];
-            TL(HGNN_K_AGG_BWD, launch_agg_bwd(ab, s));
-            init[h.pin] = 1;
+            pab.total_rows = other_edge ? tot_e : tot_n;
+            pab.cap_rows = other_edge ? P.cap_e : P.cap_n;
+            pab.p = src.v[h.edge ? S_PN : S_PE];
+            pab.inp = da;
+            pab.ldp = h.kp;
+            pab.pofs_m = P.jt * h.cg;
+            pab.pofs_d = P.jt * h.cg + h.cp;
+            pab.jtot = P.jt;
+            pab.c = h.cp;
+            pab.out = at<float>(ws, P.feats[h.pin].grad);
+            pab.ldo = h.cp;
+            pab.accumulate = init[h.pin];
         }
+        if (ng && np) TL(HGNN_K_AGG_BWD, launch_agg_bwd_pair(gab, pab, s));
+        else if (ng) TL(HGNN_K_AGG_BWD, launch_agg_bwd(gab, s));
+        else if (np) TL(HGNN_K_AGG_BWD, launch_agg_bwd(pab, s));
+        if (ng) init[h.gin] = 1;
+        if (np) init[h.pin] = 1;
     }
     for (int p = 0; p < 2; ++p)
         if (pending[p]) HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[p], 0));
