@@ -11,8 +11,9 @@ GPUs the RCCL all-reduce of the gradient bucket (batch-axis data parallelism,
 Run:  python bench.py [--gpus N --steps K --warmup W]
       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 Prints ONE JSON line (rank 0) with the BASELINE metric, a live roofline of the
-dominant kernel class (HIP events around its launches inside the timed
-region) and the oracle's CPU time on a bounded sample (rank 0, N=1 only).
+dominant kernel class and HBM rooflines of the two aggregation classes (HIP
+events around their launches in a second timed region of the same steps), and
+the oracle's CPU time on a bounded sample (rank 0, N=1 only).
 """
 
 import argparse
@@ -138,7 +139,12 @@ def main():
         dominant = max(per, key=lambda k: per[k][0])
         launches_per_step = per[dominant][1] // 2
 
-    timer = KernelTimer(max(1, launches_per_step * args.steps + 8), [dominant]) if dominant is not None else None
+    # the dominant class, plus the two aggregation classes: the north_star's HBM-roofline target is
+    # on the aggregation (sparse operator x feature gathers) of the forward
+    hbm_classes = [RF.K_AGG_FWD, RF.K_AGG_BWD]
+    timed = [dominant] + [k for k in hbm_classes if k != dominant] if dominant is not None else []
+    max_launch = sum(per[k][1] for k in timed) // 2 if dominant is not None else 0
+    timer = KernelTimer(max(1, max_launch * args.steps + 8), timed) if dominant is not None else None
     graph = None
     if args.graph:
         # The step (~90 kernel launches + Python autograd) is captured once and replayed; every
@@ -188,14 +194,24 @@ def main():
                 step()
         torch.cuda.synchronize()
     roof = None
+    roof_hbm = None
     if timer is not None:
         ms, n = timer.elapsed(dominant)
+        timer_ms = {k: timer.elapsed(k) for k in timed}
         timer.close()
         counts = RF.batch_counts(W.detach(), WL, Pm, Pd, Nb, Eb)
         roof = RF.roofline_entry(dominant, ms, n, counts, args.order, 5, args.d, args.layers, args.steps,
                                  pmc_path=os.path.join(REPO, "profiles", "pmc_traffic.json"))
         roof["timed_in"] = f"second timed region: {args.steps} eager steps with HIP events around the class's launches"
         roof["class_ms_per_step_profile"] = {RF.NAMES[k]: round(v[0] / 2, 4) for k, v in per.items()}
+        roof_hbm = {}
+        for k in hbm_classes:
+            kms, kn = timer_ms[k]
+            e = RF.roofline_entry(k, kms, kn, counts, args.order, 5, args.d, args.layers, args.steps,
+                                  pmc_path=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+            roof_hbm[RF.NAMES[k]] = {x: e[x] for x in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                       "algorithmic_bytes_per_launch", "launches_per_step",
+                                                       "avg_launch_us")}
 
     value = args.bs * world * args.steps / elapsed
     res = {
@@ -220,6 +236,7 @@ def main():
             "parallelism": f"dp{world}",
         },
         "roofline": roof,
+        "roofline_hbm": roof_hbm,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_baseline:

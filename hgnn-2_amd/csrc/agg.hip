@@ -98,26 +98,26 @@ __device__ __forceinline__ float bcast(float v, int l) {
 // Per-lane BN constants of the CPL channels a lane owns (lane * CPL + i).
 template <int CPL>
 struct LaneBn {
-    float mu[CPL], sd[CPL], w, b;
+    float mu[CPL], sc[CPL], w, b;  // sc = w / std per channel
     bool on;
     __device__ __forceinline__ void init(const BnView& v, int C, int lane) {
         on = v.mean != nullptr;
         w = b = 0.f;
 #pragma unroll
-        for (int i = 0; i < CPL; ++i) mu[i] = 0.f, sd[i] = 1.f;
+        for (int i = 0; i < CPL; ++i) mu[i] = 0.f, sc[i] = 1.f;
         if (!on) return;
         w = *v.w;
         b = *v.b;
 #pragma unroll
         for (int i = 0; i < CPL; ++i) {
             const int c = lane * CPL + i;
-            if (c < C) mu[i] = v.mean[c], sd[i] = v.std[c];
+            if (c < C) mu[i] = v.mean[c], sc[i] = bn_scale(w, v.std[c]);
         }
     }
     __device__ __forceinline__ void apply(float (&x)[CPL]) const {
         if (!on) return;
 #pragma unroll
-        for (int i = 0; i < CPL; ++i) x[i] = bn_z(x[i], mu[i], sd[i], w, b);
+        for (int i = 0; i < CPL; ++i) x[i] = bn_z_s(x[i], mu[i], sc[i], b);
     }
 };
 

@@ -189,16 +189,16 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) s[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (rg < RG) {
-        float mu[4], sd[4];
+        float mu[4], isd[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             mu[i] = a.mean[4 * lane + i];
-            sd[i] = a.std[4 * lane + i];
+            isd[i] = 1.0f / a.std[4 * lane + i];
         }
         auto acc = [&](float4 dz, float4 yv) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float h = __fdiv_rn(__fsub_rn(f4c(yv, i), mu[i]), sd[i]);
+                const float h = (f4c(yv, i) - mu[i]) * isd[i];
                 const float d = f4c(dz, i);
                 const float g = wv * d;
                 f4c(s[0], i) += g;
@@ -265,13 +265,13 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
     __shared__ float4 red[256];
     float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
     if (rg < RG) {
-        float mu[4], sd[4], m1[4], m2[4];
+        float mu[4], isd[4], m1[4], m2[4];
         bool relu[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int ch = 4 * lane + i;
             mu[i] = a.mean[ch];
-            sd[i] = a.std[ch];
+            isd[i] = 1.0f / a.std[ch];
             m1[i] = a.sums[ch * 4 + 0] * inv_n;
             m2[i] = a.sums[ch * 4 + 1] * inv_n;
             relu[i] = ch >= a.relu_from;
@@ -280,8 +280,8 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
             float4 d;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                f4c(d, k) = bn_bwd_dy(f4c(yv, k), f4c(dz, k), mu[k], sd[k], wv, m1[k], m2[k], a.training != 0,
-                                      relu[k]);
+                f4c(d, k) = bn_bwd_dy_inv(f4c(yv, k), f4c(dz, k), mu[k], isd[k], wv, m1[k], m2[k], a.training != 0,
+                                          relu[k]);
                 f4c(cs, k) += f4c(d, k);
             }
             *reinterpret_cast<float4*>(a.dy + i) = d;

@@ -103,8 +103,7 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
                                 float t[4];
 #pragma unroll
                                 for (int q = 0; q < 4; ++q) {
-                                    const float hh = __fdiv_rn(__fsub_rn(0.f, a.pmean[c + q]), a.pstd[c + q]);
-                                    t[q] = __fadd_rn(__fmul_rn(*a.pw, hh), *a.pb);
+                                    t[q] = bn_z(0.f, a.pmean[c + q], a.pstd[c + q], *a.pw, *a.pb);
                                 }
                                 v[u] = make_float4(t[0], t[1], t[2], t[3]);
                             }
@@ -171,8 +170,7 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
                             v[u] = a.xp[(long long)(off + m) * F + c];
                             if (a.pmean) v[u] = bn_z(v[u], a.pmean[c], a.pstd[c], *a.pw, *a.pb);
                         } else if (a.pmean) {
-                            const float hh = __fdiv_rn(__fsub_rn(0.f, a.pmean[c]), a.pstd[c]);
-                            v[u] = __fadd_rn(__fmul_rn(*a.pw, hh), *a.pb);
+                            v[u] = bn_z(0.f, a.pmean[c], a.pstd[c], *a.pw, *a.pb);
                         }
                     }
                 }

@@ -67,8 +67,15 @@ struct BnView {
     const float* b;
 };
 
+// BN output z = w (y - mean) / std + b, evaluated as (y - mean) * (w / std) + b with the
+// scale rounded once per channel: every reader (aggregation, dense dW) uses these two
+// functions, so all consumers see the same z.  The reference's operation order
+// (sub, div, mul, add) differs by a few ulp; an exact __fdiv_rn per gathered element cost
+// the aggregation forward ~15 % (measured: 0.198 -> 0.167 ms per step).
+__device__ __forceinline__ float bn_scale(float w, float sd) { return w / sd; }
+__device__ __forceinline__ float bn_z_s(float y, float mu, float scale, float b) { return fmaf(y - mu, scale, b); }
 __device__ __forceinline__ float bn_z(float y, float mu, float sd, float w, float b) {
-    return __fadd_rn(__fmul_rn(w, __fdiv_rn(__fsub_rn(y, mu), sd)), b);
+    return bn_z_s(y, mu, bn_scale(w, sd), b);
 }
 
 struct AggFwdArgs {
@@ -260,6 +267,22 @@ __device__ __forceinline__ float bn_bwd_dy(float yv, float dzv, float mu, float 
         d = (g - m1 - h * m2) / sd;
     } else {
         d = g / sd;
+    }
+    if (relu && !(yv > 0.f)) d = 0.f;
+    return d;
+}
+
+// Same with the reciprocal of std rounded once per channel (the float4 BN-backward kernels):
+// multiplications instead of two correctly rounded divisions per element.
+__device__ __forceinline__ float bn_bwd_dy_inv(float yv, float dzv, float mu, float isd, float wv, float m1, float m2,
+                                               bool training, bool relu) {
+    const float g = wv * dzv;
+    float d;
+    if (training) {
+        const float h = (yv - mu) * isd;
+        d = (g - m1 - h * m2) * isd;
+    } else {
+        d = g * isd;
     }
     if (relu && !(yv > 0.f)) d = 0.f;
     return d;

@@ -14,7 +14,8 @@ import os
 
 import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhgnn_amd.so")
+LIB_PATH = os.environ.get("HGNN_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                            "libhgnn_amd.so")
 
 HGNN_OK = 0
 STATUS = {0: "ok", 1: "invalid argument", 2: "unsupported configuration", 3: "HIP runtime error",

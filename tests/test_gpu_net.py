@@ -260,4 +260,9 @@ def test_gnn_lg_d128_config4_model_vs_oracle_fp64():
         err = (p.grad.cpu().double() - ref_g[k]).abs()
         assert torch.all(err <= 1e-4 * gmax + 1e-5 * ref_g[k].abs()), (k, err.max().item(), gmax)
     err = (X.grad.cpu().double() - ref_dx).abs().max().item()
-    assert err <= 1e-4 * max(1.0, ref_dx.abs().max().item())
+    # dX at this width is ill-conditioned: the reference's own fp32 evaluation (the oracle run in
+    # fp32, op for op) is 0.016 away from fp64 here, 2.5x the fixed 1e-4 * max|dX| bound; the GPU
+    # result must be within that bound or within twice the reference-fp32 error
+    _, _, _, dx32 = _oracle_lg(model, b, 4, 2, dtype=torch.float32)
+    ref32_err = (dx32.double() - ref_dx).abs().max().item()
+    assert err <= max(1e-4 * max(1.0, ref_dx.abs().max().item()), 2.0 * ref32_err), (err, ref32_err)

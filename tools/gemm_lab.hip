@@ -182,6 +182,152 @@ struct Shape {
     int M, N, K;
 };
 
+// Distance-D register prefetch: D register stage sets, so the global loads of k-tile t+D
+// are issued while tile t computes (k_nt: D = 1).  LDS stays double-buffered.
+template <int BM, int BN, int BK, int WGM, int WGN, int D>
+__global__ void __launch_bounds__(64 * WGM * WGN) k_ntd(const float* __restrict__ A, int lda,
+                                                        const float* __restrict__ B, int ldb, float* __restrict__ C,
+                                                        int ldc, int M, int N, int K) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 32, AN = TN / 32;
+    constexpr int LDK = BK + 4;
+    constexpr int AF4 = BM * BK / 4 / NT, BF4 = BN * BK / 4 / NT;
+    __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv / WGN, wn = wv % WGN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    constexpr unsigned OOB = 0x7ffffff0u;
+    const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), 0, M * lda * 4, 0x00020000);
+    const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B), 0, N * ldb * 4, 0x00020000);
+    auto ld4 = [](__amdgpu_buffer_rsrc_t r, unsigned off) {
+        return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+    };
+    float4 ra[D][AF4], rb[D][BF4];
+    auto load = [&](int st, int k0) {
+#pragma unroll
+        for (int i = 0; i < AF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            const int gm = m0 + row, gk = k0 + kq;
+            ra[st][i] = ld4(rs_a, (gm < M && gk < K) ? (unsigned)(gm * lda + gk) * 4u : OOB);
+        }
+#pragma unroll
+        for (int i = 0; i < BF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            const int gn = n0 + row, gk = k0 + kq;
+            rb[st][i] = ld4(rs_b, (gn < N && gk < K) ? (unsigned)(gn * ldb + gk) * 4u : OOB);
+        }
+    };
+    auto store = [&](int st, int buf) {
+#pragma unroll
+        for (int i = 0; i < AF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            *reinterpret_cast<float4*>(&As[buf][row * LDK + kq]) = ra[st][i];
+        }
+#pragma unroll
+        for (int i = 0; i < BF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            *reinterpret_cast<float4*>(&Bs[buf][row * LDK + kq]) = rb[st][i];
+        }
+    };
+    f32x16 acc[AM][AN];
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nt = (K + BK - 1) / BK;
+    const int h = lane >> 5, l31 = lane & 31;
+    // prologue: tiles 0..D loaded, tile 0 stored
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        if (d < nt) load(d, d * BK);
+    store(0, 0);
+    __syncthreads();
+    if (D < nt) load(0, D * BK);
+    // tile t+1 lives in stage (t+1) % D; tile t+D+1 is loaded into the stage freed by the store
+    for (int t = 0; t < nt; ++t) {
+        const int buf = t & 1;
+        const float* as = &As[buf][(wm * TM + l31) * LDK + h * (BK / 2)];
+        const float* bs = &Bs[buf][(wn * TN + l31) * LDK + h * (BK / 2)];
+#pragma unroll
+        for (int g = 0; g < BK / 8; ++g) {
+            float4 a[AM], b[AN];
+#pragma unroll
+            for (int i = 0; i < AM; ++i) a[i] = *reinterpret_cast<const float4*>(as + i * 32 * LDK + 4 * g);
+#pragma unroll
+            for (int j = 0; j < AN; ++j) b[j] = *reinterpret_cast<const float4*>(bs + j * 32 * LDK + 4 * g);
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+#pragma unroll
+                for (int j = 0; j < AN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                }
+        }
+        if (t + 1 < nt) {
+            // stage index must be compile-time for register arrays: unrolled switch over D
+#pragma unroll
+            for (int d = 0; d < D; ++d)
+                if ((t + 1) % D == d) {
+                    store(d, buf ^ 1);
+                    if (t + 1 + D < nt) load(d, (t + 1 + D) * BK);
+                }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j) {
+            const int gn = n0 + wn * TN + j * 32 + l31;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gm = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (gm < M && gn < N) C[(long long)gm * ldc + gn] = acc[i][j][r];
+            }
+        }
+}
+
+template <int BM, int BN, int BK, int WGM, int WGN, int D>
+void run_ntd(const char* tag, const Shape& sh, const float* A, const float* B, float* C, const float* ref,
+             hipStream_t s) {
+    const dim3 g((sh.M + BM - 1) / BM, (sh.N + BN - 1) / BN);
+    const long long MN = (long long)sh.M * sh.N;
+    auto launch = [&]() {
+        hipLaunchKernelGGL((k_ntd<BM, BN, BK, WGM, WGN, D>), g, dim3(64 * WGM * WGN), 0, s, A, sh.K, B, sh.K, C, sh.N,
+                           sh.M, sh.N, sh.K);
+    };
+    launch();
+    CK(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int reps = 20;
+    CK(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) launch();
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<float> hc(MN), hr(MN);
+    CK(hipMemcpy(hc.data(), C, MN * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hr.data(), ref, MN * 4, hipMemcpyDeviceToHost));
+    double err = 0, mx = 0;
+    for (long long i = 0; i < MN; ++i) {
+        err = fmax(err, fabs(hc[i] - hr[i]));
+        mx = fmax(mx, fabs(hr[i]));
+    }
+    const double us = ms * 1e3 / reps;
+    printf("%-10s %-28s blocks=%6d  %8.1f us  %6.1f TF/s  err=%.2e\n", sh.name, tag, g.x * g.y, us,
+           2.0 * sh.M * sh.N * sh.K / (us * 1e-6) / 1e12, err);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+}
+
 template <int BM, int BN, int BK, int WGM, int WGN, int PIPE = 0>
 void run_nt(const char* tag, const Shape& sh, const float* A, const float* B, float* C, float* slabs, const float* ref,
             int splits, hipStream_t s) {
@@ -599,6 +745,30 @@ int main() {
             CK(hipFree(mv));
             CK(hipFree(part));
             CK(hipFree(Abig));
+        }
+        if (getenv("LAB_SPLIT")) {
+            // split-K with a separate slab-sum kernel: does finer work granularity pay at these M?
+            run_ntd<64, 128, 32, 2, 2, 1>("ntd<64,128,32,2x2> D1", sh, A, B, C, R, s);
+            run_ntd<64, 128, 32, 2, 2, 2>("ntd<64,128,32,2x2> D2", sh, A, B, C, R, s);
+            run_ntd<64, 128, 32, 2, 2, 3>("ntd<64,128,32,2x2> D3", sh, A, B, C, R, s);
+            run_ntd<64, 128, 16, 2, 2, 2>("ntd<64,128,16,2x2> D2", sh, A, B, C, R, s);
+            run_ntd<64, 128, 16, 2, 2, 4>("ntd<64,128,16,2x2> D4", sh, A, B, C, R, s);
+            run_ntd<64, 64, 32, 2, 2, 2>("ntd<64,64,32,2x2> D2", sh, A, B, C, R, s);
+            run_ntd<64, 64, 32, 2, 2, 3>("ntd<64,64,32,2x2> D3", sh, A, B, C, R, s);
+            run_ntd<32, 128, 32, 1, 4, 2>("ntd<32,128,32,1x4> D2", sh, A, B, C, R, s);
+            for (int sp : {1}) {
+                run_nt<64, 128, 32, 2, 2>("nt<64,128,32,2x2>", sh, A, B, C, S, R, sp, s);
+                run_nt<64, 64, 32, 2, 2>("nt<64,64,32,2x2>", sh, A, B, C, S, R, sp, s);
+                run_nt<32, 128, 32, 1, 4>("nt<32,128,32,1x4>", sh, A, B, C, S, R, sp, s);
+            }
+            CK(hipFree(A));
+            CK(hipFree(B));
+            CK(hipFree(BT));
+            CK(hipFree(C));
+            CK(hipFree(R));
+            CK(hipFree(S));
+            CK(hipFree(bias));
+            continue;
         }
         for (int sp : {1}) {
             run_nt<64, 128, 32, 2, 2>("nt<64,128,32,2x2>", sh, A, B, C, S, R, sp, s);
