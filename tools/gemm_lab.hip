@@ -184,7 +184,7 @@ struct Shape {
 
 // Distance-D register prefetch: D register stage sets, so the global loads of k-tile t+D
 // are issued while tile t computes (k_nt: D = 1).  LDS stays double-buffered.
-template <int BM, int BN, int BK, int WGM, int WGN, int D>
+template <int BM, int BN, int BK, int WGM, int WGN, int D, int ORD = 0, int MID = 0>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_ntd(const float* __restrict__ A, int lda,
                                                         const float* __restrict__ B, int ldb, float* __restrict__ C,
                                                         int ldc, int M, int N, int K) {
@@ -251,32 +251,47 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_ntd(const float* __restrict_
         const int buf = t & 1;
         const float* as = &As[buf][(wm * TM + l31) * LDK + h * (BK / 2)];
         const float* bs = &Bs[buf][(wn * TN + l31) * LDK + h * (BK / 2)];
+        auto next = [&]() {
+            if (t + 1 < nt) {
+                // stage index must be compile-time for register arrays: unrolled switch over D
+#pragma unroll
+                for (int d = 0; d < D; ++d)
+                    if ((t + 1) % D == d) {
+                        store(d, buf ^ 1);
+                        if (t + 1 + D < nt) load(d, (t + 1 + D) * BK);
+                    }
+            }
+        };
 #pragma unroll
         for (int g = 0; g < BK / 8; ++g) {
+            if (MID && g == BK / 16) next();  // next tile's LDS store in the middle of the MFMAs
             float4 a[AM], b[AN];
 #pragma unroll
             for (int i = 0; i < AM; ++i) a[i] = *reinterpret_cast<const float4*>(as + i * 32 * LDK + 4 * g);
 #pragma unroll
             for (int j = 0; j < AN; ++j) b[j] = *reinterpret_cast<const float4*>(bs + j * 32 * LDK + 4 * g);
+            if constexpr (ORD == 0) {
 #pragma unroll
-            for (int i = 0; i < AM; ++i)
+                for (int i = 0; i < AM; ++i)
 #pragma unroll
-                for (int j = 0; j < AN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
-                }
+                    for (int j = 0; j < AN; ++j) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                    }
+            } else {
+                // step-major: consecutive MFMAs on different accumulators
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int i = 0; i < AM; ++i)
+#pragma unroll
+                        for (int j = 0; j < AN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
+            }
         }
-        if (t + 1 < nt) {
-            // stage index must be compile-time for register arrays: unrolled switch over D
-#pragma unroll
-            for (int d = 0; d < D; ++d)
-                if ((t + 1) % D == d) {
-                    store(d, buf ^ 1);
-                    if (t + 1 + D < nt) load(d, (t + 1 + D) * BK);
-                }
-        }
+        if (!MID) next();
         __syncthreads();
     }
 #pragma unroll
@@ -292,13 +307,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_ntd(const float* __restrict_
         }
 }
 
-template <int BM, int BN, int BK, int WGM, int WGN, int D>
+template <int BM, int BN, int BK, int WGM, int WGN, int D, int ORD = 0, int MID = 0>
 void run_ntd(const char* tag, const Shape& sh, const float* A, const float* B, float* C, const float* ref,
              hipStream_t s) {
     const dim3 g((sh.M + BM - 1) / BM, (sh.N + BN - 1) / BN);
     const long long MN = (long long)sh.M * sh.N;
     auto launch = [&]() {
-        hipLaunchKernelGGL((k_ntd<BM, BN, BK, WGM, WGN, D>), g, dim3(64 * WGM * WGN), 0, s, A, sh.K, B, sh.K, C, sh.N,
+        hipLaunchKernelGGL((k_ntd<BM, BN, BK, WGM, WGN, D, ORD, MID>), g, dim3(64 * WGM * WGN), 0, s, A, sh.K, B, sh.K, C, sh.N,
                            sh.M, sh.N, sh.K);
     };
     launch();
@@ -324,6 +339,363 @@ void run_ntd(const char* tag, const Shape& sh, const float* A, const float* B, f
     const double us = ms * 1e3 / reps;
     printf("%-10s %-28s blocks=%6d  %8.1f us  %6.1f TF/s  err=%.2e\n", sh.name, tag, g.x * g.y, us,
            2.0 * sh.M * sh.N * sh.K / (us * 1e-6) / 1e12, err);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+}
+
+// ---- fp32 GEMM on bf16 MFMA with a 3-way operand split ("bf16x6"): x = hi + mid + lo
+// (each bf16 round-to-nearest of the remainder, exact to ~2^-24), product terms
+// hh + hm + mh + hl + lh + mm (the dropped ones are <= 2^-23 relative), accumulated in fp32.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3(float4 v, bf16x4_t& h, bf16x4_t& m, bf16x4_t& l) {
+    const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const __bf16 hi = (__bf16)x[i];
+        const float r1 = x[i] - (float)hi;
+        const __bf16 mi = (__bf16)r1;
+        const float r2 = r1 - (float)mi;
+        h[i] = hi;
+        m[i] = mi;
+        l[i] = (__bf16)r2;
+    }
+}
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ void __launch_bounds__(64 * WGM * WGN) k_x6(const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                                       int ldb, float* __restrict__ C, int ldc, int M, int N, int K) {
+    constexpr int BK = 32, BKP = BK + 8;  // 80-B LDS rows: conflict-free ds_read_b128
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 32, AN = TN / 32;
+    constexpr int AF4 = BM * BK / 4 / NT, BF4 = BN * BK / 4 / NT;
+    static_assert(AF4 >= 1 && BF4 >= 1 && AM >= 1 && AN >= 1, "shape");
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][3][BM * BKP];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][3][BN * BKP];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv / WGN, wn = wv % WGN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    constexpr unsigned OOB = 0x7ffffff0u;
+    const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), 0, M * lda * 4, 0x00020000);
+    const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B), 0, N * ldb * 4, 0x00020000);
+    auto ld4 = [](__amdgpu_buffer_rsrc_t r, unsigned off) {
+        return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+    };
+    float4 ra[AF4], rb[BF4];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < AF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            const int gm = m0 + row, gk = k0 + kq;
+            ra[i] = ld4(rs_a, (gm < M && gk < K) ? (unsigned)(gm * lda + gk) * 4u : OOB);
+        }
+#pragma unroll
+        for (int i = 0; i < BF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            const int gn = n0 + row, gk = k0 + kq;
+            rb[i] = ld4(rs_b, (gn < N && gk < K) ? (unsigned)(gn * ldb + gk) * 4u : OOB);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < AF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            bf16x4_t h, m, l;
+            split3(ra[i], h, m, l);
+            *reinterpret_cast<bf16x4_t*>(&As[buf][0][row * BKP + kq]) = h;
+            *reinterpret_cast<bf16x4_t*>(&As[buf][1][row * BKP + kq]) = m;
+            *reinterpret_cast<bf16x4_t*>(&As[buf][2][row * BKP + kq]) = l;
+        }
+#pragma unroll
+        for (int i = 0; i < BF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            bf16x4_t h, m, l;
+            split3(rb[i], h, m, l);
+            *reinterpret_cast<bf16x4_t*>(&Bs[buf][0][row * BKP + kq]) = h;
+            *reinterpret_cast<bf16x4_t*>(&Bs[buf][1][row * BKP + kq]) = m;
+            *reinterpret_cast<bf16x4_t*>(&Bs[buf][2][row * BKP + kq]) = l;
+        }
+    };
+    f32x16 acc[AM][AN];
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nt = (K + BK - 1) / BK;
+    const int h = lane >> 5, l31 = lane & 31;
+    load(0);
+    store(0);
+    __syncthreads();
+    if (nt > 1) load(BK);
+    for (int t = 0; t < nt; ++t) {
+        const int buf = t & 1;
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+            bf16x8_t fa[3][AM], fb[3][AN];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+#pragma unroll
+                for (int i = 0; i < AM; ++i)
+                    fa[p][i] = *reinterpret_cast<const bf16x8_t*>(&As[buf][p][(wm * TM + i * 32 + l31) * BKP + ks * 16 + 8 * h]);
+#pragma unroll
+                for (int j = 0; j < AN; ++j)
+                    fb[p][j] = *reinterpret_cast<const bf16x8_t*>(&Bs[buf][p][(wn * TN + j * 32 + l31) * BKP + ks * 16 + 8 * h]);
+            }
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+#pragma unroll
+                for (int j = 0; j < AN; ++j) {
+                    // small terms first
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[2][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2][i], fb[0][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[1][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[0][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+                }
+        }
+        if (t + 1 < nt) {
+            store(buf ^ 1);
+            if (t + 2 < nt) load((t + 2) * BK);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j) {
+            const int gn = n0 + wn * TN + j * 32 + l31;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gm = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (gm < M && gn < N) C[(long long)gm * ldc + gn] = acc[i][j][r];
+            }
+        }
+}
+
+template <int BM, int BN, int WGM, int WGN>
+void run_x6(const char* tag, const Shape& sh, const float* A, const float* B, float* C, const float* ref,
+            hipStream_t s) {
+    const dim3 g((sh.M + BM - 1) / BM, (sh.N + BN - 1) / BN);
+    const long long MN = (long long)sh.M * sh.N;
+    auto launch = [&]() {
+        hipLaunchKernelGGL((k_x6<BM, BN, WGM, WGN>), g, dim3(64 * WGM * WGN), 0, s, A, sh.K, B, sh.K, C, sh.N, sh.M,
+                           sh.N, sh.K);
+    };
+    launch();
+    CK(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int reps = 20;
+    CK(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) launch();
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<float> hc(MN), hr(MN);
+    CK(hipMemcpy(hc.data(), C, MN * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hr.data(), ref, MN * 4, hipMemcpyDeviceToHost));
+    double err = 0, mx = 0;
+    for (long long i = 0; i < MN; ++i) {
+        err = fmax(err, fabs(hc[i] - hr[i]));
+        mx = fmax(mx, fabs(hr[i]));
+    }
+    const double us = ms * 1e3 / reps;
+    printf("%-10s %-28s blocks=%6d  %8.1f us  %6.1f TF/s(fp32-eq)  err=%.2e (max|ref| %.1f)\n", sh.name, tag, g.x * g.y,
+           us, 2.0 * sh.M * sh.N * sh.K / (us * 1e-6) / 1e12, err, mx);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+}
+
+// v2: BK templated, register prefetch distance D, B optionally pre-split in global
+// (3 bf16 planes [3][N][K], written once per weight update), LDS double-buffered.
+__global__ void k_split_planes(const float* __restrict__ x, __bf16* __restrict__ planes, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float v = x[i];
+    const __bf16 hi = (__bf16)v;
+    const float r1 = v - (float)hi;
+    const __bf16 mi = (__bf16)r1;
+    planes[i] = hi;
+    planes[n + i] = mi;
+    planes[2 * n + i] = (__bf16)(r1 - (float)mi);
+}
+
+template <int BM, int BN, int BK, int WGM, int WGN, int D, bool PREB>
+__global__ void __launch_bounds__(64 * WGM * WGN) k_x6b(const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                                        const __bf16* __restrict__ Bp, int ldb, float* __restrict__ C,
+                                                        int ldc, int M, int N, int K) {
+    constexpr int BKP = BK + 8;
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 32, AN = TN / 32;
+    constexpr int AF4 = BM * BK / 4 / NT, BF4 = BN * BK / 4 / NT;
+    static_assert(AF4 >= 1 && BF4 >= 1 && AM >= 1 && AN >= 1, "shape");
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][3][BM * BKP];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][3][BN * BKP];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv / WGN, wn = wv % WGN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    constexpr unsigned OOB = 0x7ffffff0u;
+    const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), 0, M * lda * 4, 0x00020000);
+    const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B), 0, N * ldb * 4, 0x00020000);
+    const long long np = (long long)N * ldb;  // plane size (elements)
+    const auto rs_p = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(Bp), 0, (int)(3 * np * 2), 0x00020000);
+    auto ld4 = [](__amdgpu_buffer_rsrc_t r, unsigned off) {
+        return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+    };
+    auto ld2 = [](__amdgpu_buffer_rsrc_t r, unsigned off) {
+        return __builtin_bit_cast(bf16x4_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+    };
+    float4 ra[D][AF4], rb[D][PREB ? 1 : BF4];
+    bf16x4_t rp[D][PREB ? 3 : 1][PREB ? BF4 : 1];
+    auto load = [&](int st, int k0) {
+#pragma unroll
+        for (int i = 0; i < AF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            const int gm = m0 + row, gk = k0 + kq;
+            ra[st][i] = ld4(rs_a, (gm < M && gk < K) ? (unsigned)(gm * lda + gk) * 4u : OOB);
+        }
+#pragma unroll
+        for (int i = 0; i < BF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            const int gn = n0 + row, gk = k0 + kq;
+            const bool ok = gn < N && gk < K;
+            if constexpr (PREB) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    rp[st][q][i] = ld2(rs_p, ok ? (unsigned)(q * np + gn * ldb + gk) * 2u : OOB);
+            } else {
+                rb[st][i] = ld4(rs_b, ok ? (unsigned)(gn * ldb + gk) * 4u : OOB);
+            }
+        }
+    };
+    auto store = [&](int st, int buf) {
+#pragma unroll
+        for (int i = 0; i < AF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            bf16x4_t h, m, l;
+            split3(ra[st][i], h, m, l);
+            *reinterpret_cast<bf16x4_t*>(&As[buf][0][row * BKP + kq]) = h;
+            *reinterpret_cast<bf16x4_t*>(&As[buf][1][row * BKP + kq]) = m;
+            *reinterpret_cast<bf16x4_t*>(&As[buf][2][row * BKP + kq]) = l;
+        }
+#pragma unroll
+        for (int i = 0; i < BF4; ++i) {
+            const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+            if constexpr (PREB) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4_t*>(&Bs[buf][q][row * BKP + kq]) = rp[st][q][i];
+            } else {
+                bf16x4_t h, m, l;
+                split3(rb[st][i], h, m, l);
+                *reinterpret_cast<bf16x4_t*>(&Bs[buf][0][row * BKP + kq]) = h;
+                *reinterpret_cast<bf16x4_t*>(&Bs[buf][1][row * BKP + kq]) = m;
+                *reinterpret_cast<bf16x4_t*>(&Bs[buf][2][row * BKP + kq]) = l;
+            }
+        }
+    };
+    f32x16 acc[AM][AN];
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nt = (K + BK - 1) / BK;
+    const int h = lane >> 5, l31 = lane & 31;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        if (d < nt) load(d, d * BK);
+    store(0, 0);
+    __syncthreads();
+    if (D < nt) load(0, D * BK);
+    for (int t = 0; t < nt; ++t) {
+        const int buf = t & 1;
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+            bf16x8_t fa[3][AM], fb[3][AN];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+#pragma unroll
+                for (int i = 0; i < AM; ++i)
+                    fa[p][i] = *reinterpret_cast<const bf16x8_t*>(&As[buf][p][(wm * TM + i * 32 + l31) * BKP + ks * 16 + 8 * h]);
+#pragma unroll
+                for (int j = 0; j < AN; ++j)
+                    fb[p][j] = *reinterpret_cast<const bf16x8_t*>(&Bs[buf][p][(wn * TN + j * 32 + l31) * BKP + ks * 16 + 8 * h]);
+            }
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+#pragma unroll
+                for (int j = 0; j < AN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[2][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2][i], fb[0][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[1][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[0][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+                }
+        }
+        if (t + 1 < nt) {
+#pragma unroll
+            for (int d = 0; d < D; ++d)
+                if ((t + 1) % D == d) {
+                    store(d, buf ^ 1);
+                    if (t + 1 + D < nt) load(d, (t + 1 + D) * BK);
+                }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j) {
+            const int gn = n0 + wn * TN + j * 32 + l31;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gm = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (gm < M && gn < N) C[(long long)gm * ldc + gn] = acc[i][j][r];
+            }
+        }
+}
+
+template <int BM, int BN, int BK, int WGM, int WGN, int D, bool PREB>
+void run_x6b(const char* tag, const Shape& sh, const float* A, const float* B, float* C, const float* ref,
+             hipStream_t s) {
+    const dim3 g((sh.M + BM - 1) / BM, (sh.N + BN - 1) / BN);
+    const long long MN = (long long)sh.M * sh.N, NB = (long long)sh.N * sh.K;
+    __bf16* Bp;
+    CK(hipMalloc(&Bp, 3 * NB * 2));
+    hipLaunchKernelGGL(k_split_planes, dim3((NB + 255) / 256), dim3(256), 0, s, B, Bp, NB);
+    auto launch = [&]() {
+        hipLaunchKernelGGL((k_x6b<BM, BN, BK, WGM, WGN, D, PREB>), g, dim3(64 * WGM * WGN), 0, s, A, sh.K, B, Bp, sh.K,
+                           C, sh.N, sh.M, sh.N, sh.K);
+    };
+    launch();
+    CK(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int reps = 20;
+    CK(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) launch();
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<float> hc(MN), hr(MN);
+    CK(hipMemcpy(hc.data(), C, MN * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hr.data(), ref, MN * 4, hipMemcpyDeviceToHost));
+    double err = 0;
+    for (long long i = 0; i < MN; ++i) err = fmax(err, fabs(hc[i] - hr[i]));
+    const double us = ms * 1e3 / reps;
+    printf("%-10s %-32s blocks=%6d  %8.1f us  %6.1f TF/s(fp32-eq)  err=%.2e\n", sh.name, tag, g.x * g.y, us,
+           2.0 * sh.M * sh.N * sh.K / (us * 1e-6) / 1e12, err);
+    CK(hipFree(Bp));
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
 }
@@ -749,13 +1121,17 @@ int main() {
         if (getenv("LAB_SPLIT")) {
             // split-K with a separate slab-sum kernel: does finer work granularity pay at these M?
             run_ntd<64, 128, 32, 2, 2, 1>("ntd<64,128,32,2x2> D1", sh, A, B, C, R, s);
-            run_ntd<64, 128, 32, 2, 2, 2>("ntd<64,128,32,2x2> D2", sh, A, B, C, R, s);
-            run_ntd<64, 128, 32, 2, 2, 3>("ntd<64,128,32,2x2> D3", sh, A, B, C, R, s);
-            run_ntd<64, 128, 16, 2, 2, 2>("ntd<64,128,16,2x2> D2", sh, A, B, C, R, s);
-            run_ntd<64, 128, 16, 2, 2, 4>("ntd<64,128,16,2x2> D4", sh, A, B, C, R, s);
-            run_ntd<64, 64, 32, 2, 2, 2>("ntd<64,64,32,2x2> D2", sh, A, B, C, R, s);
-            run_ntd<64, 64, 32, 2, 2, 3>("ntd<64,64,32,2x2> D3", sh, A, B, C, R, s);
-            run_ntd<32, 128, 32, 1, 4, 2>("ntd<32,128,32,1x4> D2", sh, A, B, C, R, s);
+            run_ntd<64, 64, 32, 2, 2, 1, 0, 0>("ntd<64,64,32,2x2> D1", sh, A, B, C, R, s);
+            run_x6<64, 64, 2, 2>("x6<64,64,2x2>", sh, A, B, C, R, s);
+            run_x6b<64, 64, 32, 2, 2, 1, true>("x6b<64,64,32> D1 preB", sh, A, B, C, R, s);
+            run_x6b<64, 64, 32, 2, 2, 2, true>("x6b<64,64,32> D2 preB", sh, A, B, C, R, s);
+            run_x6b<64, 64, 32, 2, 2, 2, false>("x6b<64,64,32> D2", sh, A, B, C, R, s);
+            run_x6b<64, 64, 64, 2, 2, 1, true>("x6b<64,64,64> D1 preB", sh, A, B, C, R, s);
+            run_x6b<64, 64, 64, 2, 2, 2, true>("x6b<64,64,64> D2 preB", sh, A, B, C, R, s);
+            run_x6b<64, 64, 16, 2, 2, 2, true>("x6b<64,64,16> D2 preB", sh, A, B, C, R, s);
+            run_x6b<64, 64, 16, 2, 2, 4, true>("x6b<64,64,16> D4 preB", sh, A, B, C, R, s);
+            run_x6b<128, 64, 32, 2, 2, 2, true>("x6b<128,64,32> D2 preB", sh, A, B, C, R, s);
+            run_x6b<64, 128, 32, 2, 2, 2, true>("x6b<64,128,32> D2 preB", sh, A, B, C, R, s);
             for (int sp : {1}) {
                 run_nt<64, 128, 32, 2, 2>("nt<64,128,32,2x2>", sh, A, B, C, S, R, sp, s);
                 run_nt<64, 64, 32, 2, 2>("nt<64,64,32,2x2>", sh, A, B, C, S, R, sp, s);
