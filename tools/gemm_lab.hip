@@ -184,7 +184,7 @@ struct Shape {
 
 // Distance-D register prefetch: D register stage sets, so the global loads of k-tile t+D
 // are issued while tile t computes (k_nt: D = 1).  LDS stays double-buffered.
-template <int BM, int BN, int BK, int WGM, int WGN, int D, int ORD = 0, int MID = 0>
+template <int BM, int BN, int BK, int WGM, int WGN, int D, int ORD = 0, int MID = 0, int PROBE = 0>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_ntd(const float* __restrict__ A, int lda,
                                                         const float* __restrict__ B, int ldb, float* __restrict__ C,
                                                         int ldc, int M, int N, int K) {
@@ -257,8 +257,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_ntd(const float* __restrict_
 #pragma unroll
                 for (int d = 0; d < D; ++d)
                     if ((t + 1) % D == d) {
-                        store(d, buf ^ 1);
-                        if (t + 1 + D < nt) load(d, (t + 1 + D) * BK);
+                        if (PROBE != 2) {
+                            store(d, buf ^ 1);
+                            if (t + 1 + D < nt) load(d, (t + 1 + D) * BK);
+                        }
                     }
             }
         };
@@ -270,7 +272,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_ntd(const float* __restrict_
             for (int i = 0; i < AM; ++i) a[i] = *reinterpret_cast<const float4*>(as + i * 32 * LDK + 4 * g);
 #pragma unroll
             for (int j = 0; j < AN; ++j) b[j] = *reinterpret_cast<const float4*>(bs + j * 32 * LDK + 4 * g);
-            if constexpr (ORD == 0) {
+            if constexpr (PROBE == 1) {
+#pragma unroll
+                for (int i = 0; i < AM; ++i)
+#pragma unroll
+                    for (int j = 0; j < AN; ++j) acc[i][j][0] += a[i].x * b[j].y + a[i].z * b[j].w;
+            } else if constexpr (ORD == 0) {
 #pragma unroll
                 for (int i = 0; i < AM; ++i)
 #pragma unroll
@@ -307,13 +314,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_ntd(const float* __restrict_
         }
 }
 
-template <int BM, int BN, int BK, int WGM, int WGN, int D, int ORD = 0, int MID = 0>
+template <int BM, int BN, int BK, int WGM, int WGN, int D, int ORD = 0, int MID = 0, int PROBE = 0>
 void run_ntd(const char* tag, const Shape& sh, const float* A, const float* B, float* C, const float* ref,
              hipStream_t s) {
     const dim3 g((sh.M + BM - 1) / BM, (sh.N + BN - 1) / BN);
     const long long MN = (long long)sh.M * sh.N;
     auto launch = [&]() {
-        hipLaunchKernelGGL((k_ntd<BM, BN, BK, WGM, WGN, D, ORD, MID>), g, dim3(64 * WGM * WGN), 0, s, A, sh.K, B, sh.K, C, sh.N,
+        hipLaunchKernelGGL((k_ntd<BM, BN, BK, WGM, WGN, D, ORD, MID, PROBE>), g, dim3(64 * WGM * WGN), 0, s, A, sh.K, B, sh.K, C, sh.N,
                            sh.M, sh.N, sh.K);
     };
     launch();
@@ -1120,18 +1127,10 @@ int main() {
         }
         if (getenv("LAB_SPLIT")) {
             // split-K with a separate slab-sum kernel: does finer work granularity pay at these M?
-            run_ntd<64, 128, 32, 2, 2, 1>("ntd<64,128,32,2x2> D1", sh, A, B, C, R, s);
-            run_ntd<64, 64, 32, 2, 2, 1, 0, 0>("ntd<64,64,32,2x2> D1", sh, A, B, C, R, s);
+            run_ntd<64, 64, 32, 2, 2, 1>("ntd<64,64,32,2x2> D1", sh, A, B, C, R, s);
+            run_ntd<64, 64, 32, 2, 2, 1, 0, 0, 1>("ntd<64,64> PROBE staging-only", sh, A, B, C, R, s);
+            run_ntd<64, 64, 32, 2, 2, 1, 0, 0, 2>("ntd<64,64> PROBE mfma+lds-only", sh, A, B, C, R, s);
             run_x6<64, 64, 2, 2>("x6<64,64,2x2>", sh, A, B, C, R, s);
-            run_x6b<64, 64, 32, 2, 2, 1, true>("x6b<64,64,32> D1 preB", sh, A, B, C, R, s);
-            run_x6b<64, 64, 32, 2, 2, 2, true>("x6b<64,64,32> D2 preB", sh, A, B, C, R, s);
-            run_x6b<64, 64, 32, 2, 2, 2, false>("x6b<64,64,32> D2", sh, A, B, C, R, s);
-            run_x6b<64, 64, 64, 2, 2, 1, true>("x6b<64,64,64> D1 preB", sh, A, B, C, R, s);
-            run_x6b<64, 64, 64, 2, 2, 2, true>("x6b<64,64,64> D2 preB", sh, A, B, C, R, s);
-            run_x6b<64, 64, 16, 2, 2, 2, true>("x6b<64,64,16> D2 preB", sh, A, B, C, R, s);
-            run_x6b<64, 64, 16, 2, 2, 4, true>("x6b<64,64,16> D4 preB", sh, A, B, C, R, s);
-            run_x6b<128, 64, 32, 2, 2, 2, true>("x6b<128,64,32> D2 preB", sh, A, B, C, R, s);
-            run_x6b<64, 128, 32, 2, 2, 2, true>("x6b<64,128,32> D2 preB", sh, A, B, C, R, s);
             for (int sp : {1}) {
                 run_nt<64, 128, 32, 2, 2>("nt<64,128,32,2x2>", sh, A, B, C, S, R, sp, s);
                 run_nt<64, 64, 32, 2, 2>("nt<64,64,32,2x2>", sh, A, B, C, S, R, sp, s);
