@@ -303,6 +303,7 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
     __shared__ int sp[CCN_MAXD * CCN_MAXD];
     __shared__ unsigned long long vmask[CCN_MAXD];  // bit x of vmask[a]: x in C_a
     __shared__ float sred[2][4][C2_CMAX];           // per-wave partial q1-total and d3
+    __shared__ int s_j[CCN_MAXD], s_dj[CCN_MAXD], s_oj[CCN_MAXD];  // neighbour a: node, degree, 2D row offset
     const int i = blockIdx.x;
     if (i >= *total_nodes) return;
     const int n = v.deg[i];
@@ -311,6 +312,12 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
     const int* ni = v.nbr + (long long)i * v.nmax;
     const long long o2 = v.off2[i], o1 = v.off1[i];
     for (int e = threadIdx.x; e < n * n; e += 256) sp[e] = v.pos[o2 + e];
+    if (threadIdx.x < n) {
+        const int j = ni[threadIdx.x];
+        s_j[threadIdx.x] = j;
+        s_dj[threadIdx.x] = v.deg[j];
+        s_oj[threadIdx.x] = v.off2[j];
+    }
     __syncthreads();
     for (int a = wv; a < n; a += 4) {
         const unsigned long long m = __ballot(lane < n && sp[a * n + lane] >= 0);
@@ -342,21 +349,38 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
                 d2[c] = (vb && va) ? xj : 0.f;
             }
         } else {
-            const int dj = v.deg[j];
-            const float* row = fin + ((long long)v.off2[j] + (long long)(vb ? pb : 0) * dj) * cin;
+            const int dj = s_dj[a];
+            const float* row = fin + ((long long)s_oj[a] + (long long)(vb ? pb : 0) * dj) * cin;
+            // the common neighbours z (wave-uniform) in batches of 4: all loads of a batch in flight
+            // before any is used (a one-at-a-time walk paid one memory latency per z); same order of
+            // summation
             unsigned long long zs = ma;
             while (zs) {
-                const int z = __ffsll((long long)zs) - 1;
-                zs &= zs - 1ull;
-                const int pz = sp[a * n + z];
-                if (vb) {
+                int zz[4];
 #pragma unroll
-                    for (int c = 0; c < C2_CMAX; ++c) {
-                        if (c >= cin) break;
-                        const float t = row[(long long)pz * cin + c];
-                        sc[c] += t;
-                        if (z == lane) d1[c] = t;
-                        if (z == a) d2[c] = t;
+                for (int u = 0; u < 4; ++u) {
+                    zz[u] = zs ? __ffsll((long long)zs) - 1 : -1;
+                    zs &= zs ? zs - 1ull : 0ull;
+                }
+                float t[4][C2_CMAX];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int pz = zz[u] >= 0 ? sp[a * n + zz[u]] : 0;  // valid row: loads need no mask
+#pragma unroll
+                    for (int c = 0; c < C2_CMAX; ++c) t[u][c] = c < cin ? row[(long long)pz * cin + c] : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int z = zz[u];
+                    if (z < 0) break;
+                    if (vb) {
+#pragma unroll
+                        for (int c = 0; c < C2_CMAX; ++c) {
+                            if (c >= cin) break;
+                            sc[c] += t[u][c];
+                            if (z == lane) d1[c] = t[u][c];
+                            if (z == a) d2[c] = t[u][c];
+                        }
                     }
                 }
             }
@@ -395,26 +419,41 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
         float sa[C2_CMAX];
 #pragma unroll
         for (int c = 0; c < C2_CMAX; ++c) sa[c] = 0.f;
-        for (int a = 0; a < n; ++a) {
-            const unsigned long long ma = vmask[a];
-            if (!((ma >> b) & 1ull)) continue;           // wave-uniform: b not in C_a
-            const bool vz = lane < n && ((ma >> lane) & 1ull);
-            if (level0) {
-                const int j = ni[a];
+        // the neighbours a with b in C_a, ascending, in batches of 4 (loads first, then the sums)
+        unsigned long long as = __ballot(lane < n && ((vmask[lane < n ? lane : 0] >> b) & 1ull));
+        while (as) {
+            int aa[4];
 #pragma unroll
-                for (int c = 0; c < C2_CMAX; ++c) {
-                    if (c >= cin) break;
-                    if (vz) sa[c] += X[(long long)j * cin + c];
+            for (int u = 0; u < 4; ++u) {
+                aa[u] = as ? __ffsll((long long)as) - 1 : -1;
+                as &= as ? as - 1ull : 0ull;
+            }
+            float t[4][C2_CMAX];
+            bool vz[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int a = aa[u] >= 0 ? aa[u] : 0;
+                const unsigned long long ma = vmask[a];
+                vz[u] = aa[u] >= 0 && lane < n && ((ma >> lane) & 1ull);
+                const float* q;
+                if (level0) {
+                    q = X + (long long)s_j[a] * cin;
+                } else {
+                    const int pb = max(sp[a * n + b], 0), pz = vz[u] ? sp[a * n + lane] : 0;
+                    q = fin + ((long long)s_oj[a] + (long long)pb * s_dj[a] + pz) * cin;
                 }
-            } else if (vz) {
-                const int j = ni[a];
-                const int dj = v.deg[j];
-                const int pb = sp[a * n + b], pz = sp[a * n + lane];
-                const float* q = fin + ((long long)v.off2[j] + (long long)pb * dj + pz) * cin;
 #pragma unroll
-                for (int c = 0; c < C2_CMAX; ++c) {
-                    if (c >= cin) break;
-                    sa[c] += q[c];
+                for (int c = 0; c < C2_CMAX; ++c) t[u][c] = c < cin ? q[c] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (aa[u] < 0) break;
+                if (vz[u]) {
+#pragma unroll
+                    for (int c = 0; c < C2_CMAX; ++c) {
+                        if (c >= cin) break;
+                        sa[c] += t[u][c];
+                    }
                 }
             }
         }
@@ -678,60 +717,103 @@ __global__ void __launch_bounds__(256) k_ccn2_dx0(CcnPlanView v, const int* tota
 // read F_j[u][w] (+ readout); level 0: dX[j] = sum over (u, w) (+ d_j^2 dsum0).  As in the forward,
 // F_j[u][w] is read by T_i only where u, w are both common neighbours of i and j: wave per row u,
 // lane w, walking the neighbours a with u in C_a (wave-uniform), lanes gathering where w in C_a.
+template <int C, int NB>
 __global__ void __launch_bounds__(256) k_ccn2_bwd_gather(CcnPlanView v, const int* total_nodes, C2Grad gd, int cin,
                                                          const float* __restrict__ dsum, int dsum_ld, int dsum_off,
                                                          int level0, float* __restrict__ dout) {
+    // C: channel bound of this instantiation (cin <= C); NB: neighbours gathered per batch
     __shared__ int sp[CCN_MAXD * CCN_MAXD];
     __shared__ unsigned long long vmask[CCN_MAXD];
     __shared__ float red[4][C2_CMAX];
+    __shared__ int s_i[CCN_MAXD], s_di[CCN_MAXD], s_oi[CCN_MAXD], s_aj[CCN_MAXD];  // neighbour a of j
     const int j = blockIdx.x;
     if (j >= *total_nodes) return;
     const int n = v.deg[j];
-    if (n > CCN_MAXD || cin > C2_CMAX) return;
+    if (n > CCN_MAXD || cin > C) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long o2 = v.off2[j];
     const int* nj = v.nbr + (long long)j * v.nmax;
     const int sj = v.selfpos[j];
     const int g = v.graph[j];
     for (int e = threadIdx.x; e < n * n; e += 256) sp[e] = v.pos[o2 + e];
+    if (threadIdx.x < n) {
+        const int i = nj[threadIdx.x];
+        s_i[threadIdx.x] = i;
+        s_di[threadIdx.x] = v.deg[i];
+        s_oi[threadIdx.x] = v.off2[i];
+    }
     __syncthreads();
     for (int a = wv; a < n; a += 4) {
         const unsigned long long m = __ballot(lane < n && sp[a * n + lane] >= 0);
-        if (lane == 0) vmask[a] = m;
+        if (lane == 0) {
+            vmask[a] = m;
+            s_aj[a] = sp[a * n + sj];  // position of j in N(i_a)
+        }
     }
     __syncthreads();
-    float rd[C2_CMAX], part[C2_CMAX];
+    float rd[C], part[C];
 #pragma unroll
-    for (int c = 0; c < C2_CMAX; ++c) {
+    for (int c = 0; c < C; ++c) {
         rd[c] = (dsum && c < cin) ? dsum[(long long)g * dsum_ld + dsum_off + c] : 0.f;
         part[c] = 0.f;
     }
     for (int u = wv; u < n; u += 4) {
-        float acc[C2_CMAX];
+        float acc[C];
 #pragma unroll
-        for (int c = 0; c < C2_CMAX; ++c) acc[c] = 0.f;
-        for (int a = 0; a < n; ++a) {
-            const unsigned long long ma = vmask[a];
-            if (!((ma >> u) & 1ull)) continue;          // wave-uniform: u not in C_a
-            if (!(lane < n && ((ma >> lane) & 1ull))) continue;
-            const int b = sp[a * n + u], z = sp[a * n + lane];
-            const int i = nj[a];
-            const int aj = sp[a * n + sj];
-            const int di = v.deg[i];
-            const long long oi = v.off2[i];
-            const long long rab = (oi + (long long)aj * di + b) * cin, rbz = (oi + (long long)b * di + z) * cin;
+        for (int c = 0; c < C; ++c) acc[c] = 0.f;
+        // the neighbours a with u in C_a, ascending, NB at a time: every load of a batch is in flight
+        // before the sums (the per-a walk paid ~3 dependent memory latencies per a: 2.2 -> 0.7 ms per
+        // launch at config 5)
+        unsigned long long as = __ballot(lane < n && ((vmask[lane < n ? lane : 0] >> u) & 1ull));
+        while (as) {
+            int aa[NB];
 #pragma unroll
-            for (int c = 0; c < C2_CMAX; ++c) {
-                if (c >= cin) break;
-                float t = gd.dSc[rab + c] + gd.dSa[rbz + c];
-                if (z == b) t += gd.dD1[rab + c];
-                if (z == aj) t += gd.dD2[rab + c];
-                if (aj == b && b == z) t += gd.dd3[(long long)i * cin + c];
-                acc[c] += t;
+            for (int q = 0; q < NB; ++q) {
+                aa[q] = as ? __ffsll((long long)as) - 1 : -1;
+                as &= as ? as - 1ull : 0ull;
+            }
+            float tsc[NB][C], tsa[NB][C], td1[NB][C], td2[NB][C], td3[NB][C];
+            int zb[NB], zz[NB], zaj[NB];
+            bool vz[NB];
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+                const int a = aa[q] >= 0 ? aa[q] : 0;
+                vz[q] = aa[q] >= 0 && lane < n && ((vmask[a] >> lane) & 1ull);
+                const int b = max(sp[a * n + u], 0), z = vz[q] ? sp[a * n + lane] : 0;
+                const int aj = s_aj[a], di = s_di[a], i = s_i[a];
+                const long long oi = s_oi[a];
+                const long long rab = (oi + (long long)aj * di + b) * cin, rbz = (oi + (long long)b * di + z) * cin;
+                zb[q] = b;
+                zz[q] = z;
+                zaj[q] = aj;
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const bool ok = c < cin;
+                    tsc[q][c] = ok ? gd.dSc[rab + c] : 0.f;
+                    tsa[q][c] = ok ? gd.dSa[rbz + c] : 0.f;
+                    td1[q][c] = ok ? gd.dD1[rab + c] : 0.f;
+                    td2[q][c] = ok ? gd.dD2[rab + c] : 0.f;
+                    td3[q][c] = ok ? gd.dd3[(long long)i * cin + c] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+                if (aa[q] < 0) break;
+                if (!vz[q]) continue;
+                const int b = zb[q], z = zz[q], aj = zaj[q];
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    if (c >= cin) break;
+                    float t = tsc[q][c] + tsa[q][c];
+                    if (z == b) t += td1[q][c];
+                    if (z == aj) t += td2[q][c];
+                    if (aj == b && b == z) t += td3[q][c];
+                    acc[c] += t;
+                }
             }
         }
 #pragma unroll
-        for (int c = 0; c < C2_CMAX; ++c) {
+        for (int c = 0; c < C; ++c) {
             if (c >= cin) break;
             if (level0) part[c] += acc[c];
             else if (lane < n) dout[(o2 + (long long)u * n + lane) * cin + c] = acc[c] + rd[c];
@@ -739,7 +821,7 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_gather(CcnPlanView v, const in
     }
     if (level0) {
 #pragma unroll
-        for (int c = 0; c < C2_CMAX; ++c) {
+        for (int c = 0; c < C; ++c) {
             if (c >= cin) break;
             const float t = wave_sum(part[c]);
             if (lane == 0) red[wv][c] = t;
@@ -1282,8 +1364,12 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                 hipLaunchKernelGGL(k_ccn2_dx0, dim3(nb4), dim3(256), 0, s, v, tot, P<float>(W, L.g0), cin, dsum, nf,
                                    dst);
             else
-                hipLaunchKernelGGL(k_ccn2_bwd_gather, dim3(nb1), dim3(256), 0, s, v, tot, gd, cin, dsum, nf, doff,
-                                   lvl0, dst);
+                if (cin <= 2)
+                    hipLaunchKernelGGL((k_ccn2_bwd_gather<2, 4>), dim3(nb1), dim3(256), 0, s, v, tot, gd, cin, dsum,
+                                       nf, doff, lvl0, dst);
+                else
+                    hipLaunchKernelGGL((k_ccn2_bwd_gather<C2_CMAX, 1>), dim3(nb1), dim3(256), 0, s, v, tot, gd, cin,
+                                       dsum, nf, doff, lvl0, dst);
         }
         HGNN_LAUNCH_CHECK();
         float* t = dF;
