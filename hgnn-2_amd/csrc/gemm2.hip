@@ -397,6 +397,24 @@ size_t dw2_slab_floats(int r_cap, int o, int k) {
 __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ slabs, const int* r_valid,
                                                     int kchunk, int M, int N, int split, float* dw0, float* dw1,
                                                     const float* __restrict__ dbpart, float* db0, float* db1) {
+    const int nwb = (M * N + 255) / 256;
+    if ((int)blockIdx.x >= nwb) {
+        // trailing blocks: the bias gradient of output channel o (k_db_reduce's work, same order)
+        __shared__ double red[4];
+        const int o = blockIdx.x - nwb;
+        const int tv = ceil_div(*r_valid, 64);
+        double s = 0.0;
+        for (int t = threadIdx.x; t < tv; t += 256) s += (double)dbpart[(long long)t * M + o];
+        s = wave_sum_d(s);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const double t = red[0] + red[1] + red[2] + red[3];
+            if (o < split) db0[o] = (float)t;
+            else db1[o - split] = (float)t;
+        }
+        return;
+    }
     const int idx = blockIdx.x * 256 + threadIdx.x;
     const int rows = *r_valid;
     if (idx < M * N) {
@@ -418,31 +436,12 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
     }
 }
 
-// bias gradient: one block per output channel sums the per-tile column sums of dY
-__global__ void __launch_bounds__(256) k_db_reduce(const int* r_valid, int M, int split,
-                                                   const float* __restrict__ dbpart, float* db0, float* db1) {
-    __shared__ double red[4];
-    const int o = blockIdx.x;
-    const int tv = ceil_div(*r_valid, 64);
-    double s = 0.0;
-    for (int t = threadIdx.x; t < tv; t += 256) s += (double)dbpart[(long long)t * M + o];
-    s = wave_sum_d(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const double t = red[0] + red[1] + red[2] + red[3];
-        if (o < split) db0[o] = (float)t;
-        else db1[o - split] = (float)t;
-    }
-}
-
 int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int k, int split, float* dw0,
                       float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s) {
     const int total = o * k;
-    hipLaunchKernelGGL(k_dw_reduce2, dim3(ceil_div(total, 256)), dim3(256), 0, s, slabs, r_valid, kchunk, o, k,
-                       split, dw0, dw1, dbpart, db0, db1);
-    HGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_db_reduce, dim3(o), dim3(256), 0, s, r_valid, o, split, dbpart, db0, db1);
+    // one launch: ceil(o k / 256) blocks of slab sums, then o blocks of bias sums
+    hipLaunchKernelGGL(k_dw_reduce2, dim3(ceil_div(total, 256) + (dbpart ? o : 0)), dim3(256), 0, s, slabs, r_valid,
+                       kchunk, o, k, split, dw0, dw1, dbpart, db0, db1);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -96,7 +96,7 @@ CLASS_KERNELS = {
     K_GEMM_DA: ("k_gemm3<", "k_gemm2_da"),
     K_AGG_BWD: ("k_agg_bwd",),
     K_DW_DENSE: ("k_dw_dense",),
-    K_DW_REDUCE: ("k_dw_reduce", "k_db_reduce"),
+    K_DW_REDUCE: ("k_dw_reduce",),
 }
 
 
