@@ -14,6 +14,6 @@ for r in $(seq 1 ${REPS:-2}); do
     out=gpurun_out/ab3.json
     env $c timeout -k 10 300 python bench.py --steps ${STEPS:-50} --warmup 5 --cpu-baseline 0 ${BENCH_ARGS:-} > $out 2> gpurun_out/ab.err
     rc=$?; if [ $rc -ne 0 ]; then tail -5 gpurun_out/ab.err; exit $rc; fi
-    python -c "import json,sys; d=json.loads(open('$out').read().strip().splitlines()[-1]); p=d['roofline']['class_ms_per_step_profile']; print('%-28s'%sys.argv[1][-28:], d['value'], d['ms_per_step'], ' '.join('%s %.3f' % (k, p[k]) for k in ('agg_fwd','gemm_fwd','bn_bwd','gemm_da','agg_bwd','gemm_dw')))" "$c"
+    python -c "import json,sys; d=json.loads(open('$out').read().strip().splitlines()[-1]); p=d['roofline']['class_ms_per_step_profile']; print('%-28s'%sys.argv[1][-28:], d['value'], d['ms_per_step'], ' '.join('%s %.3f' % (k, p[k]) for k in ('struct','agg_fwd','gemm_fwd','bn_bwd','gemm_da','agg_bwd','gemm_dw')))" "$c"
   done
 done
