@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-bs", type=int, default=512)
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--roofline", type=int, default=1)
+    ap.add_argument("--fwd-line", type=int, default=1, help="also time the forward alone (cfg2f)")
     ap.add_argument("--graph", type=int, default=0,
                     help="capture the step (forward + backward) in a HIP graph and replay it; measured on the box: "
                          "293.6 K vs 293.7 K graphs/s eager -- the step is GPU-bound, so off by default")
@@ -60,28 +61,70 @@ def make_batch(bs, seed):
     return list(prepare_batch(data, 0, 1))
 
 
-def cpu_baseline(args, batch_cpu, model):
-    """Oracle (CPU restatement of the reference, oracle/ref_mnb.py) fwd+bwd on a bounded sample."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args, batch_cpu, model, gpu_res):
+    """Oracle (CPU restatement of the reference, oracle/ref_mnb.py) on the same batch and weights:
+    one warm-up fwd+bwd on a small batch, then one timed step of the full batch with forward and
+    backward timed apart.  Its outputs double as the parity check of the GPU step
+    (SURVEY.md §8 c policy, oracle/parity.py): fp32 oracle (the reference's op order) for outputs,
+    loss and every gradient, plus an fp64 forward (batched leg) as the second output leg."""
+    from oracle import parity as PP
     from oracle import ref_mnb as R
     b = [t.clone() for t in batch_cpu]
-    if args.cpu_bs < args.bs:
-        b = make_batch(args.cpu_bs, 4242)
     X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = b
-    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     threads = torch.get_num_threads()
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
-        st = R.bn_states(args.layers, 2 * args.d)
-        Xr = X.clone().requires_grad_(True)
-        Wr = W.clone().requires_grad_(True)
-        out = R.gnn_lg(p, [Xr, XL, Wr, WL, Pm, Pd], Nb, mask, Eb, mask_lg, args.layers, args.order, st, True)
-        torch.nn.MSELoss()(out, T).backward()
-    dt = time.perf_counter() - t0
-    n = X.shape[0] * args.cpu_steps
-    return {"value": round(n / dt, 3), "unit": "graphs/s", "cores": threads, "kind": "port",
-            "sample": f"{args.cpu_steps} fwd+bwd step(s) of {X.shape[0]} QM9-shape graphs, d={args.d}, "
-                      f"L={args.layers}, order {args.order}, on oracle/ref_mnb.py (torch CPU, {threads} threads); "
-                      f"{dt:.1f} s"}
+
+    def run(bb, dtype=torch.float32, fast=False, grads=True):
+        X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = bb
+        p = {k: v.to(dtype).requires_grad_(grads) for k, v in sd.items()}
+        st = R.bn_states(args.layers, 2 * args.d, dtype=dtype)
+        Xr = X.to(dtype).requires_grad_(grads)
+        Wr = W.to(dtype).requires_grad_(grads)
+        t0 = time.perf_counter()
+        with torch.set_grad_enabled(grads):
+            out = R.gnn_lg(p, [Xr, XL.to(dtype), Wr, WL.to(dtype), Pm.to(dtype), Pd.to(dtype)], Nb, mask.to(dtype),
+                           Eb, mask_lg.to(dtype), args.layers, args.order, st, True, fast=fast)
+            loss = torch.nn.MSELoss()(out, T.to(dtype))
+        t1 = time.perf_counter()
+        if grads:
+            loss.backward()
+        t2 = time.perf_counter()
+        g = {k: v.grad for k, v in p.items()} if grads else None
+        return out.detach(), loss.item(), g, (Xr.grad, Wr.grad), t1 - t0, t2 - t1
+
+    run(make_batch(32, 4243))  # warm-up: allocator, thread pool, conv kernels
+    out32, loss32, g32, (dx32, dw32), t_f, t_b = run(b)
+    out64 = run(b, torch.float64, fast=True, grads=False)[0]
+    n = X.shape[0]
+    res = {"value": round(n / (t_f + t_b), 3), "unit": "graphs/s", "cores": threads, "kind": "port",
+           "cpu_model": _cpu_model(), "forward_s": round(t_f, 3), "backward_s": round(t_b, 3),
+           "sample": f"1 warm-up step on 32 graphs, then 1 timed fwd+bwd step of {n} QM9-shape graphs, "
+                     f"d={args.d}, L={args.layers}, order {args.order}, on oracle/ref_mnb.py (the reference's "
+                     f"dense per-graph loops; torch CPU, {threads} threads); {t_f + t_b:.1f} s"}
+    outp = PP.outputs_two_leg(gpu_res["out"], out32, out64)
+    gr = PP.grads_global(gpu_res["grads"], g32)
+    gx = PP.grads_global({"dX": gpu_res["dX"], "dW": gpu_res["dW"]}, {"dX": dx32, "dW": dw32})
+    dloss = abs(gpu_res["loss"] - loss32)
+    par = {"vs": "oracle fp32 (reference op order) on the bench batch and weights; outputs also vs fp64",
+           "max_abs_out_vs_ref32": outp["max_abs_vs_ref32"], "bound_out_ref32": outp["bound_ref32"],
+           "max_abs_out_vs_ref64": outp["max_abs_vs_ref64"], "bound_out_ref64": outp["bound_ref64"],
+           "abs_loss_diff": dloss,
+           "max_grad_err_over_bound": round(gr["worst_err_over_bound"], 4), "worst_grad": gr["worst_tensor"],
+           "max_input_grad_err_over_bound": round(gx["worst_err_over_bound"], 4),
+           "n_param_grads": len(g32)}
+    par["pass"] = bool(outp["pass"] and gr["pass"] and gx["pass"] and dloss <= 1e-5 * max(1.0, abs(loss32)))
+    return res, par
 
 
 def main():
@@ -109,14 +152,17 @@ def main():
     crit = torch.nn.MSELoss()
     from hgnn_amd.dp import GradAllReduce
     allreduce = GradAllReduce(params)
+    last_out = [None]
 
     def compute():
         for p in params:
             p.grad = None
         X.grad = None
+        W.grad = None  # the reference rebuilds W every batch: no accumulation into an old W.grad
         out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
         loss = crit(out, T)
         loss.backward()
+        last_out[0] = out
         return loss
 
     def step():
@@ -218,6 +264,41 @@ def main():
                                                        "algorithmic_bytes_per_launch", "launches_per_step",
                                                        "avg_launch_us")}
 
+    # forward-only line (config "cfg2f"): the north star's HBM target is stated on the batched
+    # LG-GNN forward.  Train-mode BN (batch statistics), no autograd graph kept.
+    roof_fwd = None
+    if args.fwd_line:
+        from hgnn_amd.net import KernelTimer as KT
+
+        def fwd():
+            with torch.no_grad():
+                model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+        for _ in range(3):
+            fwd()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fwd()
+        torch.cuda.synchronize()
+        fms = (time.perf_counter() - t0) * 1e3 / args.steps
+        with KT(4096, [RF.K_AGG_FWD]) as tf:
+            for _ in range(args.steps):
+                fwd()
+            torch.cuda.synchronize()
+            ams, an = tf.elapsed(RF.K_AGG_FWD)
+        tf.close()
+        counts_f = RF.batch_counts(W.detach(), WL, Pm, Pd, Nb, Eb)
+        ffl, fby = RF.forward_work(counts_f, args.order, 5, args.d, args.layers)
+        agg = RF.roofline_entry(RF.K_AGG_FWD, ams, an, counts_f, args.order, 5, args.d, args.layers, args.steps)
+        roof_fwd = {"workload": f"forward only (train-mode BN), {args.bs} graphs", "ms_per_forward": round(fms, 4),
+                    "graphs_per_s": round(args.bs / fms * 1e3, 1),
+                    "algorithmic_flops": ffl, "algorithmic_bytes": fby,
+                    "achieved_tflops": round(ffl / fms / 1e9, 3),
+                    "frac_mfma": round(ffl / fms / 1e9 / RF.PEAK_FP32_MFMA_TFS, 4),
+                    "achieved_gbs": round(fby / fms / 1e6, 2),
+                    "frac_hbm": round(fby / fms / 1e6 / RF.PEAK_HBM_GBS, 4),
+                    "agg_fwd": {x: agg[x] for x in ("achieved", "unit", "frac", "launches_per_step", "avg_launch_us")}}
+
     value = args.bs * world * args.steps / elapsed
     res = {
         "metric": METRIC,
@@ -242,14 +323,23 @@ def main():
         },
         "roofline": roof,
         "roofline_hbm": roof_hbm,
+        "roofline_fwd": roof_fwd,
         "cpu_baseline": None,
+        "parity": None,
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(args, batch_cpu, model)
+        # one more GPU step on the same batch: its outputs / grads are checked against the oracle
+        loss = compute()
+        gpu_res = {"loss": loss.item(), "out": last_out[0].detach().cpu(),
+                   "grads": {k: p.grad.detach().cpu() for k, p in model.named_parameters()},
+                   "dX": X.grad.detach().cpu(), "dW": W.grad.detach().cpu()}
+        res["cpu_baseline"], res["parity"] = cpu_baseline(args, batch_cpu, model, gpu_res)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if res.get("parity") is not None and not res["parity"]["pass"]:
+        sys.exit("bench: GPU step breaches the SURVEY.md §8 c parity policy (see the 'parity' object)")
 
 
 if __name__ == "__main__":

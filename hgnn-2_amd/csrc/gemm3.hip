@@ -482,7 +482,8 @@ size_t dw3_slab_floats(int r_cap, int o, int k) {
 int launch_gemm3_da_bn(const BnBwdArgs& bn, const int* m_valid, int m_cap, int o, const float* wt, int ldw, int kout,
                        float* da, int ldda, hipStream_t s) {
     if (m_cap <= 0) return 0;
-    if (o > 512 || o % 4 != 0 || bn.c != o) return 2;
+    if (o > 512 || o % 4 != 0 || bn.c != o) return HGNN_ERR_UNSUPPORTED;
+    if ((long long)m_cap * o * 4 >= (1ll << 31) || (long long)kout * ldw * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     G3 p{};
     p.a = bn.y;
     p.lda = o;

@@ -169,7 +169,7 @@ struct GemmDwArgs {
 int launch_gemm_dw(const GemmDwArgs& g, hipStream_t s);
 size_t gemm_dw_slab_floats(int r_cap, int o, int k);
 
-// ---------------------------------------------------------------- GEMM v2 (gemm2.hip)
+// ---------------------------------------------------------------- GEMM (gemm3.hip, repack.hip)
 struct RepackItem {
     const float* wl;   // linear conv weight (d, K)
     const float* wr;   // ReLU conv weight (d, K)
@@ -196,17 +196,9 @@ int dw3_kchunk(int r_cap, int o, int k);
 size_t dw3_slab_floats(int r_cap, int o, int k);
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
                     int kchunk, float* slabs, hipStream_t s);
-int launch_gemm2_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const float* wt, int n,
-                     const float* bias, int relu_from, float* y, int ldy, float* bn_part, hipStream_t s);
-int launch_gemm2_da(const float* dy, int lddy, const int* m_valid, int m_cap, int o, const float* w0,
-                    const float* w1, int split, int ldw, int k, float* da, int ldda, hipStream_t s);
-int launch_gemm2_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o,
-                    int k, int kchunk, float* slabs, hipStream_t s);
 // slabs -> dW (split rows) ; bias grads from the BN-backward per-tile column sums of dY
 int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int k, int split, float* dw0,
                       float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s);
-int dw2_kchunk(int r_cap, int o, int k);
-size_t dw2_slab_floats(int r_cap, int o, int k);
 
 // ---------------------------------------------------------------- BN
 struct BnFwdArgs {

@@ -1,7 +1,8 @@
 // Network executor: GNN_lg / GNN_simple forward and backward as one enqueue.
 //
 // The reference runs every layer as Python-level torch ops with per-graph
-// Python loops (models/gnns/model_mnb.py:166-174, 232-237; layers_mnb.py).
+// Python loops (models/gnns/model_mnb.py:58-66 GNN_simple.forward, 124-129
+// GNN_lg.forward, order switch 102-119; models/layers/layers_mnb.py).
 // Here the network is a fixed "program" of half-layers derived from the
 // config: each half = aggregate (agg_fwd) -> fused Conv1d pair GEMM with
 // bias/ReLU/BN-partials epilogue -> BN finalize -> BN apply.  The last layer is
@@ -252,6 +253,17 @@ Program build_program(const hgnn_net_config* c) {
     return P;
 }
 
+// The GEMMs address each operand through a 32-bit buffer resource: every operand the
+// program hands them must stay under 2 GB (checked before anything is enqueued).
+bool fits_32bit(const Program& P) {
+    const long long lim = (1ll << 31) - 1;
+    for (const Half& h : P.halves) {
+        const long long cap = h.edge ? P.cap_e : P.cap_n;
+        if (cap * h.kp * 4 > lim || cap * P.c2 * 4 > lim || (long long)P.c2 * h.kp * 4 > lim) return false;
+    }
+    return (long long)P.cap_n * P.k_last * 4 <= lim;
+}
+
 template <typename T>
 T* at(void* ws, size_t off) {
     return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
@@ -359,6 +371,7 @@ struct Timer {
 int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
                 const float* const* prm, float* const* run, void* ws, float* out, hipStream_t s, Timer* tm) {
     const Program P = build_program(c);
+    if (!fits_32bit(P)) return HGNN_ERR_UNSUPPORTED;
     const bool lg = c->kind == 1;
     const Src src = make_src(P, ws, csr);
     BatchMeta m = src.m;
@@ -511,11 +524,16 @@ struct SideStream {
     hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
 };
 
-static int side_stream(SideStream** out) {
+static int side_stream(hipStream_t main_s, SideStream** out) {
     thread_local SideStream ss;
-    int dev = 0;
-    HGNN_HOST_CHECK(hipGetDevice(&dev));
+    // the device the caller's stream belongs to, not the thread's current device: the side
+    // stream's kernels read and write the main stream's buffers
+    hipDevice_t dev = 0;
+    HGNN_HOST_CHECK(hipStreamGetDevice(main_s, &dev));
     if (ss.dev != dev) {
+        int cur = 0;
+        HGNN_HOST_CHECK(hipGetDevice(&cur));
+        HGNN_HOST_CHECK(hipSetDevice(dev));
         if (ss.s) {
             (void)hipStreamDestroy(ss.s);
             for (int i = 0; i < 2; ++i) {
@@ -530,6 +548,7 @@ static int side_stream(SideStream** out) {
             HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming));
         }
         ss.dev = dev;
+        HGNN_HOST_CHECK(hipSetDevice(cur));
     }
     *out = &ss;
     return 0;
@@ -551,6 +570,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
                  const float* const* prm, void* ws, const float* dout, float* const* grads, float* dX, float* dW,
                  hipStream_t s, Timer* tm) {
     const Program P = build_program(c);
+    if (!fits_32bit(P)) return HGNN_ERR_UNSUPPORTED;
     const Src src = make_src(P, ws, csr);
     BatchMeta m = src.m;
     const int* tot_n = m.totals;
@@ -642,7 +662,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     }
 
     SideStream* side = nullptr;
-    if (P.v2) TRY(side_stream(&side));
+    if (P.v2) TRY(side_stream(s, &side));
     // dY and the bias partials alternate between two buffers, so the side stream's
     // dW of half i may still read its pair while the main stream runs half i+1.
     bool pending[2] = {false, false};
@@ -839,7 +859,8 @@ int hgnn_net_bn_count(const hgnn_net_config* cfg) {
 
 size_t hgnn_net_workspace_bytes(const hgnn_net_config* cfg) {
     if (!valid_config(cfg)) return 0;
-    return build_program(cfg).bytes;
+    const Program P = build_program(cfg);
+    return fits_32bit(P) ? P.bytes : 0;
 }
 
 uint32_t* hgnn_net_error_word(const hgnn_net_config* cfg, void* workspace) {

@@ -234,10 +234,11 @@ class _NetFn(torch.autograd.Function):
         cfg.need_dw = 1 if dW is not None else 0
         args = (ctypes.byref(cfg), ctypes.byref(ctx.inp), L.ptr_array(ctx.params), ctypes.c_void_p(ctx.ws.data_ptr()),
                 ctypes.c_void_p(dout.data_ptr()), L.ptr_array(grads), L.ptr(dX), L.ptr(dW), L.stream_handle(X.device))
-        if _timer is not None:
-            st = L.lib().hgnn_net_backward_timed(*args, ctypes.c_void_p(_timer.handle))
-        else:
-            st = L.lib().hgnn_net_backward(*args)
+        with torch.cuda.device(X.device):
+            if _timer is not None:
+                st = L.lib().hgnn_net_backward_timed(*args, ctypes.c_void_p(_timer.handle))
+            else:
+                st = L.lib().hgnn_net_backward(*args)
         L.check(st, "network backward")
         return (None, None, dX, dW, *grads)
 
@@ -272,23 +273,40 @@ def run_net(spec, X, W, N_batch, mask, XL=None, WL=None, Pm=None, Pd=None, E_bat
             raise RuntimeError("hgnn_amd: mask_lg must be (bs, Emax, Emax) and E_batch (bs,)")
     else:
         Eb = None
-    ks, k_last = expected_k(spec.kind, spec.order, f_in, spec.d, spec.n_layers, W.shape[3])
+    params = _checked_params(spec, f_in, W.shape[3], dev)
+    tensors = (XL, WL, Pm, Pd, Nb, Eb, mask, mask_lg)
+    with torch.cuda.device(dev):
+        return _NetFn.apply(spec, tensors, X, W, *params)
+
+
+def _checked_params(spec, f_in, jt, dev):
+    """Every parameter's shape against the widths the executor will read (the C ABI gets bare
+    pointers: a mismatch would be an out-of-bounds device read), dtype and device."""
+    lg = spec.kind == 1
+    ks, k_last = expected_k(spec.kind, spec.order, f_in, spec.d, spec.n_layers, jt)
     params = list(spec.params)
     per = 12 if lg else 6
+    if len(params) != per * len(ks) + 2:
+        raise RuntimeError(f"hgnn_amd: expected {per * len(ks) + 2} parameters, got {len(params)}")
     for l, kk in enumerate(ks):
         convs = [(0, kk[0]), (2, kk[0])] + ([(6, kk[1]), (8, kk[1])] if lg else [])
         for off, k in convs:
             w = params[l * per + off]
             if w.shape != (spec.d, k, 1):
                 raise RuntimeError(f"hgnn_amd: layer {l} conv weight {tuple(w.shape)} != ({spec.d}, {k}, 1)")
+            if params[l * per + off + 1].shape != (spec.d,):
+                raise RuntimeError(f"hgnn_amd: layer {l} conv bias {tuple(params[l * per + off + 1].shape)}")
+        for off in ((4, 5, 10, 11) if lg else (4, 5)):
+            if params[l * per + off].numel() != 1:
+                raise RuntimeError(f"hgnn_amd: layer {l} BN affine parameters must be scalars")
     if params[-2].shape != (spec.dim_out, k_last, 1):
         raise RuntimeError(f"hgnn_amd: fc weight {tuple(params[-2].shape)} != ({spec.dim_out}, {k_last}, 1)")
+    if params[-1].shape != (spec.dim_out,):
+        raise RuntimeError(f"hgnn_amd: fc bias {tuple(params[-1].shape)} != ({spec.dim_out},)")
     for p in params:
         if p.device != dev or p.dtype != torch.float32:
             raise RuntimeError("hgnn_amd: parameters must be float32 on the input device (call model.cuda())")
-    params = [p if p.is_contiguous() else p.contiguous() for p in params]
-    tensors = (XL, WL, Pm, Pd, Nb, Eb, mask, mask_lg)
-    return _NetFn.apply(spec, tensors, X, W, *params)
+    return [p if p.is_contiguous() else p.contiguous() for p in params]
 
 
 def _csr_config(spec, batch):
@@ -335,10 +353,11 @@ class _NetCsrFn(torch.autograd.Function):
             if ctx.needs_input_grad[2] else None
         cfg.need_dx = 1 if dX is not None else 0
         cfg.need_dw = 0
-        L.check(L.lib().hgnn_net_backward_csr(ctypes.byref(cfg), ctypes.byref(batch.view), L.ptr_array(ctx.params),
+        with torch.cuda.device(batch.device):
+            st = L.lib().hgnn_net_backward_csr(ctypes.byref(cfg), ctypes.byref(batch.view), L.ptr_array(ctx.params),
                                               ctypes.c_void_p(ctx.ws.data_ptr()), ctypes.c_void_p(dout.data_ptr()),
-                                              L.ptr_array(grads), L.ptr(dX), L.stream_handle(batch.device)),
-                "network backward (csr)")
+                                              L.ptr_array(grads), L.ptr(dX), L.stream_handle(batch.device))
+        L.check(st, "network backward (csr)")
         return (None, None, dX, *grads)
 
 
@@ -349,11 +368,6 @@ def run_net_csr(spec, batch):
         raise RuntimeError("hgnn_amd: the CSR batch must be on the GPU (CsrBatch(..., device='cuda'))")
     if spec.kind == 1 and not batch.dual:
         raise RuntimeError("hgnn_amd: GNN_lg needs a CSR batch built with dual=True")
-    ks, k_last = expected_k(spec.kind, spec.order, batch.f_in, spec.d, spec.n_layers, batch.j_tot)
-    params = [p if p.is_contiguous() else p.contiguous() for p in spec.params]
-    if params[-2].shape != (spec.dim_out, k_last, 1):
-        raise RuntimeError(f"hgnn_amd: fc weight {tuple(params[-2].shape)} != ({spec.dim_out}, {k_last}, 1)")
-    for p in params:
-        if p.device != batch.device or p.dtype != torch.float32:
-            raise RuntimeError("hgnn_amd: parameters must be float32 on the batch's device")
-    return _NetCsrFn.apply(spec, batch, batch.x, *params)
+    params = _checked_params(spec, batch.f_in, batch.j_tot, batch.device)
+    with torch.cuda.device(batch.device):
+        return _NetCsrFn.apply(spec, batch, batch.x, *params)

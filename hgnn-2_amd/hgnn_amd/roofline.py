@@ -84,16 +84,40 @@ def class_work(kcls, counts, order, f_in, d, n_layers, jt=3):
     return fl, by
 
 
+def forward_work(counts, order, f_in, d, n_layers, jt=3):
+    """(flops, compulsory bytes) of one LG-GNN forward (SURVEY.md §8 d 'LG-GNN forward bytes / FLOPs'):
+    every layer reads its input features once and writes its pre-BN output once; the structure
+    (CSR of W, WL, Pm, Pd: 4 (rows + 1) + 8 nnz) is read by every layer; weights once."""
+    halves, k_last = lg_halves(order, f_in, d, n_layers, jt)
+    c2 = 2 * d
+    N, M = counts["nodes"], counts["edges"]
+    by = 0.0
+    cn, ce = f_in, 1
+    for _ in range(n_layers - 1):
+        by += 4.0 * (cn * N + ce * M + c2 * (N + M))
+        cn, ce = c2, c2
+    by += 4.0 * (c2 * (N + M)) + 4.0
+    S = (4.0 * (N + 1) + 8.0 * counts["nnz_w"] + 4.0 * (M + 1) + 8.0 * counts["nnz_wl"] +
+         2 * (4.0 * (N + 1) + 8.0 * counts["nnz_p"]))
+    by += n_layers * S
+    params = sum(c2 * (k + 1) for _, k, _, _ in halves) + k_last + 1
+    by += 4.0 * params
+    fl = class_work(K_GEMM_FWD, counts, order, f_in, d, n_layers, jt)[0]
+    fl += class_work(K_AGG_FWD, counts, order, f_in, d, n_layers, jt)[0]
+    fl += 2.0 * N * k_last
+    return fl, by
+
+
 # kernel-name predicates of each class (rocprofv3 names of csrc/*.hip), for the PMC traffic join
 CLASS_KERNELS = {
     K_STRUCT: ("k_plan", "k_extract", "k_pack_nodes", "k_pack_edges", "k_repack", "k_unpack_nodes"),
     K_AGG_FWD: ("k_agg_fwd",),
-    K_GEMM_FWD: ("k_gemm3<", "k_gemm2<"),
+    K_GEMM_FWD: ("k_gemm3<", "k_gemm_fwd"),
     K_BN_FWD: ("k_bn_finalize", "k_bn_apply"),
     K_READOUT: ("k_readout",),
     K_BN_BWD: ("k_bn_bwd",),
-    K_GEMM_DW: ("k_gemm3_tn", "k_gemm2_dw"),
-    K_GEMM_DA: ("k_gemm3<", "k_gemm2_da"),
+    K_GEMM_DW: ("k_gemm3_tn", "k_gemm_dw"),
+    K_GEMM_DA: ("k_gemm3<", "k_gemm_da"),
     K_AGG_BWD: ("k_agg_bwd",),
     K_DW_DENSE: ("k_dw_dense",),
     K_DW_REDUCE: ("k_dw_reduce",),

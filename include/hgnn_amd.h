@@ -59,8 +59,8 @@ const char* hgnn_status_string(int status);
 /* ------------------------------------------------------------------------
  * Network executor: GNN_lg.forward / GNN_simple.forward + autograd backward.
  *
- * Replaces models/gnns/model_mnb.py:166-174 (GNN_simple.forward) and
- * models/gnns/model_mnb.py:232-237 (GNN_lg.forward) with every layer
+ * Replaces models/gnns/model_mnb.py:58-66 (GNN_simple.forward) and
+ * models/gnns/model_mnb.py:124-129 (GNN_lg.forward) with every layer
  * (models/layers/layers_mnb.py:52-69, 88-95, 189-225, 256-290, 322-358,
  * 379-388), BN (models/layers/batch_normalization.py:34-108) and the
  * aggregation ops graph_oper / P_multi (layers_mnb.py:391-434) fused into one
@@ -69,7 +69,7 @@ const char* hgnn_status_string(int status);
  * ---------------------------------------------------------------------- */
 typedef struct hgnn_net_config {
     int32_t kind;      /* 0 = GNN_simple, 1 = GNN_lg                              */
-    int32_t order;     /* GNN_lg update order 1, 2, 3 (model_mnb.py:210-227)      */
+    int32_t order;     /* GNN_lg update order 1, 2, 3 (model_mnb.py:102-119)      */
     int32_t bs;        /* graphs in the batch                                     */
     int32_t nmax;      /* padded node count Nmax (X.shape[2])                     */
     int32_t emax;      /* padded edge-slot count Emax (XL.shape[2]); 0 for simple */

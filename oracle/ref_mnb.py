@@ -146,6 +146,22 @@ def p_multi(P, X):
     return out
 
 
+def graph_oper_fast(A, X):
+    """graph_oper as one batched contraction (same sums, other fp order); the fast oracle leg that
+    keeps the full-size parity tests cheap.  tests/test_oracle.py pins it to graph_oper."""
+    bs, N, _, J = A.shape
+    return torch.einsum("bnmj,bfm->bjfn", A, X).reshape(bs, J * X.shape[1], N)
+
+
+def p_multi_fast(P, X):
+    """p_multi as one bmm (see graph_oper_fast)."""
+    return torch.bmm(X, P.transpose(1, 2))
+
+
+def _ops(fast):
+    return (graph_oper_fast, p_multi_fast) if fast else (graph_oper, p_multi)
+
+
 def mask_embedding(H, mask):
     bs, N = mask.shape[0], mask.shape[1]
     return H * mask[:, :, 0].view(bs, 1, N).repeat(1, H.shape[1], 1)
@@ -176,14 +192,16 @@ def conv(x, p, name):
 
 
 # --------------------------------------------------------------------------- models
-def _lg_node(p, pre, X, XL_like, W, Pm, Pd, N_batch, mask, st, training):
-    x1 = torch.cat((graph_oper(W, X), p_multi(Pm, XL_like), p_multi(Pd, XL_like)), 1)
+def _lg_node(p, pre, X, XL_like, W, Pm, Pd, N_batch, mask, st, training, fast=False):
+    go, pm = _ops(fast)
+    x1 = torch.cat((go(W, X), pm(Pm, XL_like), pm(Pd, XL_like)), 1)
     zb = torch.cat((conv(x1, p, pre + "cv2"), F.relu(conv(x1, p, pre + "cv1"))), 1)
     return bn(zb, N_batch, mask, p[pre + "bn1.weight"], p[pre + "bn1.bias"], st[pre + "bn1"], training)
 
 
-def _lg_edge(p, pre, XL, X_like, WL, Pm, Pd, E_batch, mask_lg, st, training):
-    xd = torch.cat((graph_oper(WL, XL), p_multi(Pm.transpose(2, 1), X_like), p_multi(Pd.transpose(2, 1), X_like)), 1)
+def _lg_edge(p, pre, XL, X_like, WL, Pm, Pd, E_batch, mask_lg, st, training, fast=False):
+    go, pm = _ops(fast)
+    xd = torch.cat((go(WL, XL), pm(Pm.transpose(2, 1), X_like), pm(Pd.transpose(2, 1), X_like)), 1)
     zd = torch.cat((conv(xd, p, pre + "cv4"), F.relu(conv(xd, p, pre + "cv3"))), 1)
     return bn(zd, E_batch, mask_lg, p[pre + "bn2.weight"], p[pre + "bn2.bias"], st[pre + "bn2"], training)
 
@@ -196,33 +214,36 @@ def bn_states(n_layers, c, kind="lg", dtype=torch.float32):
     return st
 
 
-def gnn_lg(p, state, N_batch, mask, E_batch, mask_lg, n_layers, order, st, training=True):
-    """GNN_lg.forward (model_mnb.py:232-237) on a parameter dict with state_dict names."""
+def gnn_lg(p, state, N_batch, mask, E_batch, mask_lg, n_layers, order, st, training=True, fast=False):
+    """GNN_lg.forward (model_mnb.py:124-129, order switch 102-119) on a parameter dict with
+    state_dict names.  fast=True: batched contractions instead of the per-graph loops."""
     X, XL, W, WL, Pm, Pd = state
     for l in range(n_layers - 1):
         pre = f"layer{l}."
         if order == 1:
-            Z = _lg_node(p, pre, X, XL, W, Pm, Pd, N_batch, mask, st, training)
-            ZL = _lg_edge(p, pre, XL, Z, WL, Pm, Pd, E_batch, mask_lg, st, training)
+            Z = _lg_node(p, pre, X, XL, W, Pm, Pd, N_batch, mask, st, training, fast)
+            ZL = _lg_edge(p, pre, XL, Z, WL, Pm, Pd, E_batch, mask_lg, st, training, fast)
         elif order == 2:
-            ZL = _lg_edge(p, pre, XL, X, WL, Pm, Pd, E_batch, mask_lg, st, training)
-            Z = _lg_node(p, pre, X, ZL, W, Pm, Pd, N_batch, mask, st, training)
+            ZL = _lg_edge(p, pre, XL, X, WL, Pm, Pd, E_batch, mask_lg, st, training, fast)
+            Z = _lg_node(p, pre, X, ZL, W, Pm, Pd, N_batch, mask, st, training, fast)
         else:
-            Z = _lg_node(p, pre, X, XL, W, Pm, Pd, N_batch, mask, st, training)
-            ZL = _lg_edge(p, pre, XL, X, WL, Pm, Pd, E_batch, mask_lg, st, training)
+            Z = _lg_node(p, pre, X, XL, W, Pm, Pd, N_batch, mask, st, training, fast)
+            ZL = _lg_edge(p, pre, XL, X, WL, Pm, Pd, E_batch, mask_lg, st, training, fast)
         X, XL = Z, ZL
-    x1 = torch.cat((graph_oper(W, X), p_multi(Pm, XL), p_multi(Pd, XL)), 1)
+    go, pm = _ops(fast)
+    x1 = torch.cat((go(W, X), pm(Pm, XL), pm(Pd, XL)), 1)
     y = torch.sum(conv(x1, p, "layerlast.fc"), dim=2)
     return y.view(y.shape[0], -1)
 
 
-def gnn_simple(p, state, N_batch, mask, n_layers, st, training=True):
-    """GNN_simple.forward (model_mnb.py:166-174)."""
+def gnn_simple(p, state, N_batch, mask, n_layers, st, training=True, fast=False):
+    """GNN_simple.forward (model_mnb.py:58-66)."""
     X, W = state
+    go, _ = _ops(fast)
     for l in range(n_layers - 1):
         pre = f"layer{l}."
-        x1 = graph_oper(W, X)
+        x1 = go(W, X)
         zb = torch.cat((F.relu(conv(x1, p, pre + "cv2")), F.relu(conv(x1, p, pre + "cv1"))), 1)
         X = bn(zb, N_batch, mask, p[pre + "bn1.weight"], p[pre + "bn1.bias"], st[pre + "bn1"], training)
-    y = torch.sum(conv(graph_oper(W, X), p, "layerlast.fc"), dim=2)
+    y = torch.sum(conv(go(W, X), p, "layerlast.fc"), dim=2)
     return y.view(y.shape[0], -1)

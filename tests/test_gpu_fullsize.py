@@ -1,0 +1,121 @@
+"""GPU parity at the BASELINE.json sizes (SURVEY.md §8 c policy, oracle/parity.py).
+
+* config 2 at its real size: GNN_lg order 2, d=64, L=5 on the 512-graph QM9-shape batch;
+* config 4's per-rank share: GNN_lg d=128, L=5 on 512 graphs;
+* the executor's J > 1 instantiations (J+2 = 4 and 5 operator slices,
+  functions/operators.py:25-29) for every order and for GNN_simple.
+
+Outputs: two legs -- the reference-order fp32 oracle (per-graph torch.mm loops,
+oracle/ref_mnb.py, forward only) and the fp64 oracle.  Gradients: against the
+fp64 oracle, batched leg (oracle/ref_mnb.py graph_oper_fast, pinned to the loop
+leg by tests/test_oracle.py::test_oracle_fast_leg_equals_loop_leg).
+"""
+
+import pytest
+import torch
+
+import fixture_util as fu
+from oracle import parity as PP
+from oracle import ref_mnb as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(graphs, J=1):
+    from functions.batching import prepare_batch
+    from functions.operators import graph_operators
+    data = [[X, A, t, *graph_operators([X, A], J, True)] for X, A, t in graphs]
+    return list(prepare_batch(data, 0, J))
+
+
+def _oracle(model, b, L, order, dtype, fast, grads=True, kind="lg"):
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = b
+    p = {k: v.detach().cpu().to(dtype).requires_grad_(grads) for k, v in model.state_dict().items()}
+    st = R.bn_states(L, 2 * model.n_features, kind=kind, dtype=dtype)
+    Xo = X.to(dtype).requires_grad_(grads)
+    Wo = W.to(dtype).requires_grad_(grads)
+    with torch.set_grad_enabled(grads):
+        if kind == "lg":
+            out = R.gnn_lg(p, [Xo, XL.to(dtype), Wo, WL.to(dtype), Pm.to(dtype), Pd.to(dtype)], Nb,
+                           mask.to(dtype), Eb, mask_lg.to(dtype), L, order, st, True, fast=fast)
+        else:
+            out = R.gnn_simple(p, [Xo, Wo], Nb, mask.to(dtype), L, st, True, fast=fast)
+        loss = torch.nn.MSELoss()(out, T.to(dtype))
+        if not grads:
+            return out.detach(), loss.item(), None, None, None
+        loss.backward()
+    return out.detach(), loss.item(), {k: v.grad for k, v in p.items()}, Xo.grad, Wo.grad
+
+
+def _gpu(model, b, kind="lg"):
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = [t.cuda() for t in b]
+    X.requires_grad_(True)
+    W.requires_grad_(True)
+    out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg) if kind == "lg" else model([X, W], Nb, mask)
+    loss = torch.nn.MSELoss()(out, T)
+    loss.backward()
+    torch.cuda.synchronize()
+    return out.detach(), loss.item(), {k: p.grad for k, p in model.named_parameters()}, X.grad, W.grad
+
+
+def _check(model, b, L, order, kind="lg", dx_relax=False):
+    out, loss, g, dx, dw = _gpu(model, b, kind)
+    r32, l32, _, _, _ = _oracle(model, b, L, order, torch.float32, fast=False, grads=False, kind=kind)
+    r64, l64, g64, dx64, dw64 = _oracle(model, b, L, order, torch.float64, fast=True, kind=kind)
+    o = PP.outputs_two_leg(out, r32, r64)
+    assert o["pass"], o
+    assert abs(loss - l32) <= 1e-5 * max(1.0, abs(l32)), (loss, l32)
+    gr = PP.grads_global(g, g64)
+    assert gr["pass"], gr
+    dwr = PP.grads_global({"dW": dw}, {"dW": dw64})
+    assert dwr["pass"], dwr
+    err = (dx.cpu().double() - dx64).abs().max().item()
+    bound = 1e-4 * max(1.0, dx64.abs().max().item())
+    if dx_relax and err > bound:
+        # dX at d = 128 is ill-conditioned (tests/test_gpu_net.py::test_gnn_lg_d128_config4_model_vs_oracle_fp64):
+        # accept twice the reference's own fp32 error (fp32 oracle, batched leg)
+        _, _, _, dx32, _ = _oracle(model, b, L, order, torch.float32, fast=True, kind=kind)
+        bound = max(bound, 2.0 * (dx32.double() - dx64).abs().max().item())
+    assert err <= bound, (err, bound)
+    return o, gr
+
+
+def test_config2_full_batch_512_vs_oracle():
+    """The headline workload itself: 512 QM9-shape graphs, GNN_lg(0, 64, 5, 5, 1, 1, 2)."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_lg
+    b = _batch(dg.qm9_shape_dataset(512, seed=1000))
+    model = GNN_lg(0, 64, 5, 5, 1, 1, 2).cuda()
+    fu.det_init(model, 2)
+    _check(model, b, 5, 2)
+
+
+def test_config4_rank_share_d128_512_vs_oracle():
+    """Config 4's per-GPU share: GNN_lg d = 128 (2d = 256 channels), L = 5, 512 graphs."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_lg
+    b = _batch(dg.qm9_shape_dataset(512, seed=1004))
+    model = GNN_lg(0, 128, 5, 5, 1, 1, 2).cuda()
+    fu.det_init(model, 4)
+    _check(model, b, 5, 2, dx_relax=True)
+
+
+@pytest.mark.parametrize("J,order", [(2, 1), (2, 2), (2, 3), (3, 2)])
+def test_executor_more_operator_slices_vs_oracle(J, order):
+    """J = 2 / 3: W = [I, D, A, A^2(, A^4)] (functions/operators.py:25-29) -> the jtot 4 / 5 kernels."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_lg
+    b = _batch(dg.qm9_shape_dataset(64, seed=60 + 10 * J + order), J=J)
+    assert b[1].shape[3] == J + 2
+    model = GNN_lg(0, 16, 4, 5, 1, J, order).cuda()
+    fu.det_init(model, 20 + J)
+    _check(model, b, 4, order)
+
+
+def test_gnn_simple_j2_vs_oracle():
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_simple
+    b = _batch(dg.sbm_dataset(24, n=50, seed=5), J=2)
+    model = GNN_simple(0, 8, 6, 5, 1, 2).cuda()
+    fu.det_init(model, 61)
+    _check(model, b, 6, 0, kind="simple")

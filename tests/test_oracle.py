@@ -109,6 +109,40 @@ def test_oracle_gnn_simple_matches_reference(golden):
             assert np.all(np.abs(g - z[k]) <= 1e-4 * gmax + 1e-5 * np.abs(z[k])), k
 
 
+@pytest.mark.parametrize("order,J", [(1, 1), (2, 1), (3, 1), (2, 2)])
+def test_oracle_fast_leg_equals_loop_leg(order, J):
+    """The batched leg (graph_oper_fast / p_multi_fast), which the full-size GPU parity tests use
+    as their fp64 anchor, computes the same function as the reference-order loop leg."""
+    import hgnn_amd.datagen as dg
+    from functions.batching import prepare_batch
+    from functions.operators import graph_operators
+    graphs = dg.qm9_shape_dataset(12, seed=70 + order)
+    data = [[X, A, t, *graph_operators([X, A], J, True)] for X, A, t in graphs]
+    b = prepare_batch(data, 0, J)
+    res = []
+    for fast in (False, True):
+        X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = [t.double() if t.is_floating_point() else t for t in b]
+        p = oracle_params((0, 8, 4, 5, 1, J, order), 31, dtype=torch.float64)
+        st = R.bn_states(4, 16, dtype=torch.float64)
+        X.requires_grad_(True)
+        out = R.gnn_lg(p, [X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg, 4, order, st, True, fast=fast)
+        torch.nn.MSELoss()(out, T).backward()
+        res.append((out.detach(), {k: v.grad for k, v in p.items()}, X.grad))
+    (o0, g0, x0), (o1, g1, x1) = res
+    assert torch.allclose(o0, o1, rtol=1e-12, atol=1e-12)
+    for k in g0:
+        assert torch.allclose(g0[k], g1[k], rtol=1e-10, atol=1e-12), k
+    assert torch.allclose(x0, x1, rtol=1e-10, atol=1e-12)
+    s0 = R.bn_states(4, 4, kind="simple", dtype=torch.float64)
+    s1 = R.bn_states(4, 4, kind="simple", dtype=torch.float64)
+    ps = oracle_params((0, 2, 4, 5, 1, J), 32, kind="simple", dtype=torch.float64)
+    X = b[0].double()
+    W = b[1].double()
+    a = R.gnn_simple(ps, [X, W], b[9], b[7].double(), 4, s0, True)
+    c = R.gnn_simple(ps, [X, W], b[9], b[7].double(), 4, s1, True, fast=True)
+    assert torch.allclose(a, c, rtol=1e-12, atol=1e-12)
+
+
 # --------------------------------------------------------------------------- CCN
 def ccn_params(kind, k, dtype=torch.float32):
     """Fixture weights: det_init(net, 300 + k) on a CCN of the fixtures' shape (5 -> 1, h=2, L=2)."""

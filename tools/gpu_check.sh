@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 STEPS=${STEPS:-20}
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
   rc=$?
   echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
