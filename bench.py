@@ -82,15 +82,15 @@ def cpu_baseline(args, batch_cpu, model, gpu_res):
     from oracle import ref_mnb as R
     b = [t.clone() for t in batch_cpu]
     X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = b
-    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}  # leaves of their own
     threads = torch.get_num_threads()
 
     def run(bb, dtype=torch.float32, fast=False, grads=True):
         X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = bb
-        p = {k: v.to(dtype).requires_grad_(grads) for k, v in sd.items()}
+        p = {k: v.to(dtype).detach().clone().requires_grad_(grads) for k, v in sd.items()}
         st = R.bn_states(args.layers, 2 * args.d, dtype=dtype)
-        Xr = X.to(dtype).requires_grad_(grads)
-        Wr = W.to(dtype).requires_grad_(grads)
+        Xr = X.to(dtype).detach().clone().requires_grad_(grads)
+        Wr = W.to(dtype).detach().clone().requires_grad_(grads)
         t0 = time.perf_counter()
         with torch.set_grad_enabled(grads):
             out = R.gnn_lg(p, [Xr, XL.to(dtype), Wr, WL.to(dtype), Pm.to(dtype), Pd.to(dtype)], Nb, mask.to(dtype),

@@ -196,7 +196,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
         }
     };
 
-    f32x16 acc[AM][AN];
+    // Each BK-deep k tile is summed by the MFMAs into a fresh accumulator (tacc) and added to
+    // acc afterwards: fma chains of BK instead of K (640) terms.  Measured on the box: the
+    // one-chain version's outputs were 1.0-1.5x twice the reference fp32 error against fp64
+    // (SURVEY §8 c second leg) on the bs=128 / bs=512 d=128 tests; the split costs 16 VALU adds
+    // per 16 MFMAs.
+    f32x16 acc[AM][AN], tacc[AM][AN];
 #pragma unroll
     for (int i = 0; i < AM; ++i)
 #pragma unroll
@@ -215,6 +220,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
         const float* as = &As[buf][(wm * TM + l31) * LDK + h * (BK / 2)];
         const float* bs = &Bs[buf][(wn * TN + l31) * LDK + h * (BK / 2)];
 #pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int j = 0; j < AN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) tacc[i][j][r] = 0.f;
+#pragma unroll
         for (int g = 0; g < BK / 8; ++g) {
             float4 a[AM], b[AN];
 #pragma unroll
@@ -225,12 +236,16 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
             for (int i = 0; i < AM; ++i)
 #pragma unroll
                 for (int j = 0; j < AN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, tacc[i][j], 0, 0, 0);
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, tacc[i][j], 0, 0, 0);
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, tacc[i][j], 0, 0, 0);
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, tacc[i][j], 0, 0, 0);
                 }
         }
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int j = 0; j < AN; ++j) acc[i][j] += tacc[i][j];
         if (t + 1 < nt) {
             store(buf ^ 1, (t + 1) * BK);
             if (t + 2 < nt) load((t + 2) * BK);
