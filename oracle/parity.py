@@ -16,7 +16,7 @@ def _t(x):
     return x.detach().to("cpu", torch.float64)
 
 
-def outputs_two_leg(gpu, ref32, ref64=None):
+def outputs_two_leg(gpu, ref32, ref64=None, factor=2.0):
     g, r32 = _t(gpu), _t(ref32)
     scale = max(1.0, r32.abs().max().item())
     e32 = (g - r32).abs().max().item() if g.numel() else 0.0
@@ -25,7 +25,7 @@ def outputs_two_leg(gpu, ref32, ref64=None):
     if ref64 is not None:
         r64 = _t(ref64)
         e64 = (g - r64).abs().max().item() if g.numel() else 0.0
-        b64 = 2 * ((r32 - r64).abs().max().item() if g.numel() else 0.0) + 1e-6
+        b64 = factor * ((r32 - r64).abs().max().item() if g.numel() else 0.0) + 1e-6
         res.update({"max_abs_vs_ref64": e64, "bound_ref64": b64})
         ok = ok and e64 <= b64
     res["pass"] = bool(ok)
