@@ -200,6 +200,41 @@ int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const in
 int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int k, int split, float* dw0,
                       float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s);
 
+// ---------------------------------------------------------------- fused aggregation + GEMM (fused.hip)
+// One K segment of the virtual aggregate: ns coefficient slices of a cs-channel feature matrix
+// gathered through a row list; B(n, s, c) = b[n * b_n + s * b_s + c] is the matching block of
+// the GEMM's second operand.
+struct FusedSeg {
+    StructView list;      // row lists over the job's output rows
+    const float* src;     // gathered rows [src_rows][ld]
+    long long ld;
+    int cs, ns;           // channels (multiple of 16), slices (entry coefficients 1 .. ns)
+    BnView bn;            // BN applied on load (mean == nullptr: none)
+    const float* b;
+    long long b_n, b_s;
+};
+struct FusedJob {
+    const int* total_rows;  // device row count of the output
+    int cap_rows, blocks;   // blocks: set by launch_fused
+    FusedSeg seg[2];
+    int nseg;
+    int n;                  // output columns
+    float* out;
+    int ldo, accumulate;    // FEPI_ACC: out (+)= product
+    const float* bias;      // FEPI_FWD: bias, ReLU from column relu_from, BN partials
+    int relu_from;
+    float* bn_part;
+    float* a_out;           // FEPI_FWD, optional: the aggregate [rows][lda_out] (for dW)
+    int lda_out;
+};
+struct FusedArgs {
+    FusedJob job[2];        // job[1].nseg == 0: one job (blocks of job 1 follow job 0's)
+};
+enum { FEPI_FWD = 0, FEPI_ACC = 1 };
+bool fused_ok(const FusedJob& j);
+int fused_blocks(int cap_rows);
+int launch_fused(FusedArgs a, int epi, hipStream_t s);
+
 // ---------------------------------------------------------------- BN
 struct BnFwdArgs {
     const float* part;     // [tiles][c][3]

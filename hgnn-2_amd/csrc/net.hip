@@ -54,6 +54,7 @@ struct Program {
     int entry_stride_w = 4;
     size_t dy = 0, dy2 = 0, da = 0, da2 = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0, dbpart2 = 0;
     bool v2 = false;  // GEMM v2 path (2d % 4 == 0); gemm.hip otherwise
+    bool fused = false;  // fused aggregation + GEMM (fused.hip): 2d % 16 == 0, 2d <= 256
     size_t bytes = 0;
 };
 
@@ -79,6 +80,18 @@ bool valid_config(const hgnn_net_config* c) {
     if (capn * c->nmax > (1ll << 31) - 1) return false;
     if (cape * (c->emax > c->nmax ? c->emax : c->nmax) > (1ll << 31) - 1) return false;
     return true;
+}
+
+// HGNN_FUSED=0 selects the unfused kernels (aggregation -> [rows][K] buffer -> GEMM; dA GEMM ->
+// transposed aggregation) for A/B runs; the parity tests run both.
+static bool fused_enabled() {
+    const char* e = getenv("HGNN_FUSED");
+    return !(e && e[0] == '0');
+}
+
+// A half whose aggregation is gathered inside the GEMM (both input widths multiples of 16).
+static bool fused_fwd_half(const Program& P, const Half& h) {
+    return P.fused && h.cg % 16 == 0 && (h.pin < 0 || h.cp % 16 == 0);
 }
 
 Program build_program(const hgnn_net_config* c) {
@@ -220,6 +233,7 @@ Program build_program(const hgnn_net_config* c) {
     size_t max_da = 0, max_slab = 0;
     int max_cap = 0;
     P.v2 = (P.c2 % 4) == 0;
+    P.fused = P.v2 && P.c2 % 16 == 0 && P.c2 <= 256 && fused_enabled();
     for (auto& h : P.halves) {
         const int cap = h.edge ? P.cap_e : P.cap_n;
         h.kp = P.v2 ? (h.k + 3) / 4 * 4 : h.k;
@@ -430,6 +444,46 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
     for (const Half& h : P.halves) {
         const int cap = h.edge ? P.cap_e : P.cap_n;
         const int* tot = h.edge ? tot_e : tot_n;
+        if (fused_fwd_half(P, h)) {
+            // aggregation gathered into LDS tiles of the Conv1d-pair GEMM; the aggregate is still
+            // written once (h.a) for the weight-gradient GEMM of the backward
+            FusedArgs fa{};
+            FusedJob& j = fa.job[0];
+            j.total_rows = tot;
+            j.cap_rows = cap;
+            j.nseg = h.pin >= 0 ? 2 : 1;
+            FusedSeg& g = j.seg[0];
+            g.list = src.v[h.edge ? S_WL : S_W];
+            g.src = feat_src(P, ws, h.gin, src.x0, src.xl0);
+            g.ld = h.cg;
+            g.cs = h.cg;
+            g.ns = P.jt;
+            g.bn = feat_bn(P, ws, prm, h.gin);
+            g.b = at<float>(ws, h.wc);
+            g.b_n = h.kp;
+            g.b_s = h.cg;
+            if (h.pin >= 0) {
+                FusedSeg& pp = j.seg[1];
+                pp.list = src.v[h.edge ? S_PE : S_PN];
+                pp.src = feat_src(P, ws, h.pin, src.x0, src.xl0);
+                pp.ld = h.cp;
+                pp.cs = h.cp;
+                pp.ns = 2;
+                pp.bn = feat_bn(P, ws, prm, h.pin);
+                pp.b = at<float>(ws, h.wc) + (size_t)P.jt * h.cg;
+                pp.b_n = h.kp;
+                pp.b_s = h.cp;
+            }
+            j.n = P.c2;
+            j.out = at<float>(ws, P.feats[h.out].y);
+            j.ldo = P.c2;
+            j.bias = at<float>(ws, h.bc);
+            j.relu_from = h.relu_from;
+            j.bn_part = c->training ? at<float>(ws, h.part) : nullptr;
+            j.a_out = at<float>(ws, h.a);
+            j.lda_out = h.kp;
+            TL(HGNN_K_FUSED_FWD, launch_fused(fa, FEPI_FWD, s));
+        } else {
         AggFwdArgs ag{};
         ag.total_rows = tot;
         ag.cap_rows = cap;
@@ -471,6 +525,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
         gf.ldy = P.c2;
         gf.bn_part = c->training ? at<float>(ws, h.part) : nullptr;
         TL(HGNN_K_GEMM_FWD, launch_gemm_fwd(gf, s));
+        }
         }
 
         BnFwdArgs bf{};
@@ -673,7 +728,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     // stream, overlapping the next half -- 268K vs 286K graphs/s: the concurrent memory-bound
     // kernels only slowed each other.)
     auto fork_dw = [&](const Half& h, int cap, const int* tot, float* dyb, float* dbp, bool ndw_side,
-                       float* dab) -> int {
+                       float* dab, bool da_side = false) -> int {
         const int kc = dw3_kchunk(cap, P.c2, h.k);
         HGNN_HOST_CHECK(hipEventRecord(side->fork[parity], s));
         HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, side->fork[parity], 0));
@@ -681,6 +736,11 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         s = side->s;  // TL records its timer events on the stream the kernel runs on
         int r = 0;
         do {
+            // fused backward: dX needs no dA, only the dense operator gradient does -- its G
+            // columns (dY . Wcat_G) are made here, beside the main stream
+            if (ndw_side && da_side)
+                TL(HGNN_K_DW_DENSE, launch_gemm3_da(dyb, P.c2, tot, cap, P.c2, at<float>(ws, h.wt), P.c2, P.jt * h.cg,
+                                                    dab, h.kp, s));
             if (ndw_side) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, dab, h.kp, false, 1));
             TL(HGNN_K_GEMM_DW, launch_gemm3_dw(dyb, P.c2, at<float>(ws, h.a), h.kp, tot, cap, P.c2, h.k, kc,
                                                at<float>(ws, P.slabs), s));
@@ -724,8 +784,62 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
         const bool ndw = need_dw && !h.edge;
         // with a dA GEMM the BN backward's apply pass is fused into its operand staging
-        const bool fused_da = P.v2 && (ng || np || ndw) && fused_da_enabled();
+        const bool fused_da = !P.fused && P.v2 && (ng || np || ndw) && fused_da_enabled();
         TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s, fused_da ? 0 : 1));
+
+        if (P.fused) {
+            // dW (and the dense operator gradient) on the side stream, dX on the main stream:
+            // dX_gin (+)= (W^T dY) Wcat_G and dX_pin (+)= ({Pm, Pd}^T dY) Wcat_P, gathered from the
+            // 2d-wide dY rows inside the GEMM (fused.hip) -- no [rows][K] dA buffer
+            float* da = at<float>(ws, parity ? P.da2 : P.da);
+            TRY(fork_dw(h, cap, tot, dyb, dbp, ndw, da, true));
+            if (!ng && !np) continue;
+            FusedArgs fa{};
+            int nj = 0;
+            if (ng) {
+                FusedJob& j = fa.job[nj++];
+                j.total_rows = tot;
+                j.cap_rows = cap;
+                j.nseg = 1;
+                FusedSeg& g = j.seg[0];
+                g.list = src.v[h.edge ? S_WLT : S_WT];
+                g.src = dyb;
+                g.ld = P.c2;
+                g.cs = P.c2;
+                g.ns = P.jt;
+                g.b = at<float>(ws, h.wt);
+                g.b_n = P.c2;
+                g.b_s = (long long)h.cg * P.c2;
+                j.n = h.cg;
+                j.out = at<float>(ws, P.feats[h.gin].grad);
+                j.ldo = h.cg;
+                j.accumulate = init[h.gin];
+            }
+            if (np) {
+                const bool other_edge = !h.edge;
+                FusedJob& j = fa.job[nj++];
+                j.total_rows = other_edge ? tot_e : tot_n;
+                j.cap_rows = other_edge ? P.cap_e : P.cap_n;
+                j.nseg = 1;
+                FusedSeg& g = j.seg[0];
+                g.list = src.v[h.edge ? S_PN : S_PE];
+                g.src = dyb;
+                g.ld = P.c2;
+                g.cs = P.c2;
+                g.ns = 2;
+                g.b = at<float>(ws, h.wt) + (size_t)P.jt * h.cg * P.c2;
+                g.b_n = P.c2;
+                g.b_s = (long long)h.cp * P.c2;
+                j.n = h.cp;
+                j.out = at<float>(ws, P.feats[h.pin].grad);
+                j.ldo = h.cp;
+                j.accumulate = init[h.pin];
+            }
+            TL(HGNN_K_FUSED_BWD, launch_fused(fa, FEPI_ACC, s));
+            if (ng) init[h.gin] = 1;
+            if (np) init[h.pin] = 1;
+            continue;
+        }
 
         if (!P.v2) {
             GemmDwArgs gw{};

@@ -15,9 +15,9 @@ PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_FP32_MFMA_TFS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak
 
 (K_STRUCT, K_AGG_FWD, K_GEMM_FWD, K_BN_FWD, K_READOUT, K_BN_BWD, K_GEMM_DW, K_GEMM_DA, K_AGG_BWD, K_DW_DENSE,
- K_DW_REDUCE) = range(11)
+ K_DW_REDUCE, K_FUSED_FWD, K_FUSED_BWD) = range(13)
 NAMES = ["struct", "agg_fwd", "gemm_fwd", "bn_fwd", "readout", "bn_bwd", "gemm_dw", "gemm_da", "agg_bwd", "dw_dense",
-         "dw_reduce"]
+         "dw_reduce", "fused_fwd", "fused_bwd"]
 N_CLASSES = len(NAMES)
 
 
