@@ -192,7 +192,7 @@ def main():
 
     # the dominant class, plus the two aggregation classes: the north_star's HBM-roofline target is
     # on the aggregation (sparse operator x feature gathers) of the forward
-    hbm_classes = [RF.K_AGG_FWD, RF.K_AGG_BWD]
+    hbm_classes = [RF.K_AGG_FWD, RF.K_AGG_BWD] + ([RF.K_FUSED_FWD, RF.K_FUSED_BWD] if RF.fused_net(args.d) else [])
     timed = [dominant] + [k for k in hbm_classes if k != dominant] if dominant is not None else []
     max_launch = sum(per[k][1] for k in timed) // prof_steps if dominant is not None else 0
     timer = KernelTimer(max(1, max_launch * args.steps + 8), timed) if dominant is not None else None
@@ -246,6 +246,7 @@ def main():
         torch.cuda.synchronize()
     roof = None
     roof_hbm = None
+    roof_fused = None
     if timer is not None:
         ms, n = timer.elapsed(dominant)
         timer_ms = {k: timer.elapsed(k) for k in timed}
@@ -256,13 +257,17 @@ def main():
         roof["timed_in"] = f"second timed region: {args.steps} eager steps with HIP events around the class's launches"
         roof["class_ms_per_step_profile"] = {RF.NAMES[k]: round(v[0] / prof_steps, 4) for k, v in per.items()}
         roof_hbm = {}
+        roof_fused = {}
         for k in hbm_classes:
             kms, kn = timer_ms[k]
             e = RF.roofline_entry(k, kms, kn, counts, args.order, 5, args.d, args.layers, args.steps,
                                   pmc_path=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-            roof_hbm[RF.NAMES[k]] = {x: e[x] for x in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                                                       "algorithmic_bytes_per_launch", "launches_per_step",
-                                                       "avg_launch_us")}
+            ent = {x: e[x] for x in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                     "algorithmic_bytes_per_launch", "launches_per_step", "avg_launch_us")}
+            if e["bound"] == "hbm":
+                roof_hbm[RF.NAMES[k]] = ent
+            else:
+                roof_fused[RF.NAMES[k]] = ent
 
     # forward-only line (config "cfg2f"): the north star's HBM target is stated on the batched
     # LG-GNN forward.  Train-mode BN (batch statistics), no autograd graph kept.
@@ -281,11 +286,12 @@ def main():
             fwd()
         torch.cuda.synchronize()
         fms = (time.perf_counter() - t0) * 1e3 / args.steps
-        with KT(4096, [RF.K_AGG_FWD]) as tf:
+        with KT(4096, [RF.K_AGG_FWD, RF.K_FUSED_FWD]) as tf:
             for _ in range(args.steps):
                 fwd()
             torch.cuda.synchronize()
             ams, an = tf.elapsed(RF.K_AGG_FWD)
+            fms_f, fn_f = tf.elapsed(RF.K_FUSED_FWD)
         tf.close()
         counts_f = RF.batch_counts(W.detach(), WL, Pm, Pd, Nb, Eb)
         ffl, fby = RF.forward_work(counts_f, args.order, 5, args.d, args.layers)
@@ -298,6 +304,9 @@ def main():
                     "achieved_gbs": round(fby / fms / 1e6, 2),
                     "frac_hbm": round(fby / fms / 1e6 / RF.PEAK_HBM_GBS, 4),
                     "agg_fwd": {x: agg[x] for x in ("achieved", "unit", "frac", "launches_per_step", "avg_launch_us")}}
+        if fn_f:
+            fe = RF.roofline_entry(RF.K_FUSED_FWD, fms_f, fn_f, counts_f, args.order, 5, args.d, args.layers, args.steps)
+            roof_fwd["fused_fwd"] = {x: fe[x] for x in ("achieved", "unit", "frac", "launches_per_step", "avg_launch_us")}
 
     value = args.bs * world * args.steps / elapsed
     res = {
@@ -323,6 +332,7 @@ def main():
         },
         "roofline": roof,
         "roofline_hbm": roof_hbm,
+        "roofline_fused": roof_fused,
         "roofline_fwd": roof_fwd,
         "cpu_baseline": None,
         "parity": None,

@@ -25,6 +25,7 @@
 // chunk identically for A and B, ds_read_b128 fragments); each chunk is summed into a fresh
 // accumulator and added (fp32 chains of <= 80 terms).
 #include <algorithm>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -37,16 +38,30 @@ namespace {
 constexpr int FBM = 64;   // output rows per block
 constexpr int FCW = 16;   // input channels per chunk
 constexpr int FEU = 6;    // entries per row held in registers (the rest are streamed)
+constexpr unsigned OOB = 0x7ffffff0u;  // buffer-load offset past every range: reads 0
 
 __device__ __forceinline__ float4 f4fma(float v, float4 x, float4 a) {
     return make_float4(fmaf(v, x.x, a.x), fmaf(v, x.y, a.y), fmaf(v, x.z, a.z), fmaf(v, x.w, a.w));
 }
 
-template <int BN, int NSM, int EPI>
-__global__ void __launch_bounds__(256, 2) k_fused(FusedArgs fa) {
-    constexpr int KCM = NSM * FCW, LDK = KCM + 4;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, long long bytes) {
+    // descriptor inputs made provably wave-uniform (no waterfall loops around the loads)
+    const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    const unsigned n = __builtin_amdgcn_readfirstlane((unsigned)(bytes > 0x7fffffffll ? 0x7fffffffll : bytes));
+    float* q = reinterpret_cast<float*>(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, 0, n, 0x00020000);
+}
+
+__device__ __forceinline__ float4 ld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
+template <int BN, int JT, int EPI>
+__global__ void __launch_bounds__(256, JT == 3 ? 2 : 1) k_fused(FusedArgs fa) {
+    constexpr int KCM = JT * FCW, LDK = KCM + 4;
     constexpr int TN = BN / 2, AN = TN / 32;
-    static_assert(AN >= 1, "tile");
+    static_assert(AN >= 1 && JT >= 3, "tile");
     __shared__ __attribute__((aligned(16))) float As[2][FBM * LDK];
     __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
 
@@ -63,143 +78,11 @@ __global__ void __launch_bounds__(256, 2) k_fused(FusedArgs fa) {
     const int N = J.n;
     if (n0 >= N) return;
 
-    // ---- producer state: thread -> (row rr, channel quad q)
+    // producer thread -> (row rr, channel quad q of the 16-channel chunk)
     const int rr = tid >> 2, q = tid & 3;
     const int grow = m0 + rr;
     const bool rvalid = grow < Mv;
-    int cnt[2] = {0, 0}, st[2] = {0, 0};
-    float4 ent[2][FEU];
-    float2 ent2[2][NSM > 3 ? FEU : 1];
-#pragma unroll
-    for (int sg = 0; sg < 2; ++sg) {
-        if (sg < J.nseg && rvalid) {
-            const RowInfo ri = J.seg[sg].list.rows[grow];
-            cnt[sg] = ri.count;
-            st[sg] = ri.start;
-        }
-#pragma unroll
-        for (int u = 0; u < FEU; ++u) {
-            ent[sg][u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if constexpr (NSM > 3) ent2[sg][u] = make_float2(0.f, 0.f);
-            if (u < cnt[sg]) {
-                const float* e = J.seg[sg].list.entries + (long long)(st[sg] + u) * J.seg[sg].list.stride;
-                ent[sg][u] = *reinterpret_cast<const float4*>(e);
-                if constexpr (NSM > 3)
-                    if (J.seg[sg].ns > 3) ent2[sg][u] = *reinterpret_cast<const float2*>(e + 4);
-            }
-        }
-    }
-    const int nch0 = J.seg[0].cs / FCW;
-    const int nch = nch0 + (J.nseg > 1 ? J.seg[1].cs / FCW : 0);
-
-    // ---- chunk staging registers
-    float4 xg[FEU];     // gathered feature pieces of the chunk being prepared
-    float4 mu, sc;      // BN constants of those 4 channels
-    float bnb = 0.f;
-    constexpr int BF4 = BN * KCM / 4 / 256;  // B float4 per thread (at the widest chunk)
-    static_assert(BF4 * 256 * 4 == BN * KCM, "B staging");
-    float4 rb[BF4];
-
-    auto seg_of = [&](int i, int& cc) {
-        if (i < nch0) {
-            cc = i;
-            return 0;
-        }
-        cc = i - nch0;
-        return 1;
-    };
-    // issue the loads of chunk i (features of the cached entries, BN constants, B tile)
-    auto load = [&](int i) {
-        int cc;
-        const int sg = seg_of(i, cc);
-        const FusedSeg& S = J.seg[sg];
-        const int c0 = cc * FCW + q * 4;
-#pragma unroll
-        for (int u = 0; u < FEU; ++u) {
-            const int col = __float_as_int(ent[sg][u].x);
-            xg[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (u < cnt[sg]) xg[u] = *reinterpret_cast<const float4*>(S.src + (long long)col * S.ld + c0);
-        }
-        if (S.bn.mean) {
-            mu = *reinterpret_cast<const float4*>(S.bn.mean + c0);
-            sc = *reinterpret_cast<const float4*>(S.bn.std + c0);
-            bnb = *S.bn.b;
-            const float w = *S.bn.w;
-            sc = make_float4(bn_scale(w, sc.x), bn_scale(w, sc.y), bn_scale(w, sc.z), bn_scale(w, sc.w));
-        }
-        const int ns = S.ns, kc4 = ns * (FCW / 4);
-#pragma unroll
-        for (int f = 0; f < BF4; ++f) {
-            const int e = tid + f * 256;
-            const int n = e / kc4, rem = e % kc4, s = rem / (FCW / 4), cq = rem % (FCW / 4);
-            const int gn = n0 + n;
-            rb[f] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (n < BN && gn < N)
-                rb[f] = *reinterpret_cast<const float4*>(S.b + (long long)gn * S.b_n + (long long)s * S.b_s + cc * FCW +
-                                                         cq * 4);
-        }
-    };
-    // finish chunk i into LDS buffer buf: aggregate (BN on load), entries beyond FEU streamed
-    auto store = [&](int i, int buf) {
-        int cc;
-        const int sg = seg_of(i, cc);
-        const FusedSeg& S = J.seg[sg];
-        const int ns = S.ns, c0 = cc * FCW + q * 4;
-        const bool bn = S.bn.mean != nullptr;
-        float4 acc[NSM];
-#pragma unroll
-        for (int s = 0; s < NSM; ++s) acc[s] = make_float4(0.f, 0.f, 0.f, 0.f);
-        auto bnx = [&](float4 x) {
-            if (!bn) return x;
-            return make_float4(bn_z_s(x.x, mu.x, sc.x, bnb), bn_z_s(x.y, mu.y, sc.y, bnb), bn_z_s(x.z, mu.z, sc.z, bnb),
-                               bn_z_s(x.w, mu.w, sc.w, bnb));
-        };
-        auto add = [&](const float4& e4, const float2& e2, float4 x) {
-            acc[0] = f4fma(e4.y, x, acc[0]);
-            if (NSM > 1 && ns > 1) acc[1] = f4fma(e4.z, x, acc[1]);
-            if (NSM > 2 && ns > 2) acc[2] = f4fma(e4.w, x, acc[2]);
-            if constexpr (NSM > 3) {
-                if (ns > 3) acc[3] = f4fma(e2.x, x, acc[3]);
-                if (NSM > 4 && ns > 4) acc[4] = f4fma(e2.y, x, acc[4]);
-            }
-        };
-#pragma unroll
-        for (int u = 0; u < FEU; ++u) {
-            if (u < cnt[sg]) {
-                float2 e2 = make_float2(0.f, 0.f);
-                if constexpr (NSM > 3) e2 = ent2[sg][u];
-                add(ent[sg][u], e2, bnx(xg[u]));
-            }
-        }
-        // rows with more entries than fit in registers (phantom-slot rows, SBM degrees)
-        for (int u = FEU; u < cnt[sg]; ++u) {
-            const float* e = S.list.entries + (long long)(st[sg] + u) * S.list.stride;
-            const float4 e4 = *reinterpret_cast<const float4*>(e);
-            float2 e2 = make_float2(0.f, 0.f);
-            if constexpr (NSM > 3)
-                if (ns > 3) e2 = *reinterpret_cast<const float2*>(e + 4);
-            const float4 x = *reinterpret_cast<const float4*>(S.src + (long long)__float_as_int(e4.x) * S.ld + c0);
-            add(e4, e2, bnx(x));
-        }
-        float* as = &As[buf][rr * LDK + q * 4];
-#pragma unroll
-        for (int s = 0; s < NSM; ++s)
-            if (s < ns) *reinterpret_cast<float4*>(as + s * FCW) = acc[s];
-        if (J.a_out && blockIdx.y == 0 && rvalid) {
-            // the aggregate in the reference's column order (slice-major), for the dW GEMM
-            float* ao = J.a_out + (long long)grow * J.lda_out + (sg == 0 ? 0 : J.seg[0].ns * J.seg[0].cs) + c0;
-#pragma unroll
-            for (int s = 0; s < NSM; ++s)
-                if (s < ns) *reinterpret_cast<float4*>(ao + (long long)s * S.cs) = acc[s];
-        }
-        const int kc4 = ns * (FCW / 4);
-#pragma unroll
-        for (int f = 0; f < BF4; ++f) {
-            const int e = tid + f * 256;
-            const int n = e / kc4, rem = e % kc4, s = rem / (FCW / 4), cq = rem % (FCW / 4);
-            if (n < BN) *reinterpret_cast<float4*>(&Bs[buf][n * LDK + s * FCW + cq * 4]) = rb[f];
-        }
-    };
+    const int h = lane >> 5, l31 = lane & 31;
 
     f32x16 acc[AN], tacc[AN];
 #pragma unroll
@@ -207,44 +90,160 @@ __global__ void __launch_bounds__(256, 2) k_fused(FusedArgs fa) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
-    const int h = lane >> 5, l31 = lane & 31;
-    load(0);
-    store(0, 0);
-    __syncthreads();
-    for (int t = 0; t < nch; ++t) {
-        const int buf = t & 1;
-        if (t + 1 < nch) load(t + 1);
-        int cc;
-        const int ns = J.seg[seg_of(t, cc)].ns;
-        const int kh = ns * (FCW / 2);  // half of this chunk's k range
-        const float* as = &As[buf][(wm * 32 + l31) * LDK + h * kh];
-        const float* bs = &Bs[buf][(wn * TN + l31) * LDK + h * kh];
+    int buf = 0;
+    // one K segment: NS slices per gathered piece, cs / 16 chunks, pipelined one chunk deep
+    auto run_seg = [&](auto nsc, const FusedSeg& S, int koff) {
+        constexpr int NS = decltype(nsc)::value;
+        constexpr int KC4 = NS * (FCW / 4);                  // float4 per B row of a chunk
+        constexpr int BF4 = (BN * KC4 + 255) / 256;          // B float4 per thread
+        constexpr int KH = NS * (FCW / 2);                   // half of the chunk's k range
+        const auto rs_x = rsrc(S.src, S.src_bytes);
+        const auto rs_b = rsrc(S.b, S.b_bytes);
+        const int ld = S.ld, nch = S.cs / FCW, stride = S.list.stride;
+        const bool bn = S.bn.mean != nullptr;
+        // this thread's row: the first FEU entries in registers (dead slots: zero coefficients,
+        // out-of-range feature offsets -> the loads return 0)
+        int cnt = 0, st = 0;
+        if (rvalid) {
+            const RowInfo ri = S.list.rows[grow];
+            cnt = ri.count;
+            st = ri.start;
+        }
+        float4 ent[FEU];
+        float2 ent2[NS > 3 ? FEU : 1];
 #pragma unroll
-        for (int j = 0; j < AN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) tacc[j][r] = 0.f;
-        for (int g = 0; g < kh / 4; ++g) {
-            const float4 a = *reinterpret_cast<const float4*>(as + 4 * g);
-            float4 b[AN];
-#pragma unroll
-            for (int j = 0; j < AN; ++j) b[j] = *reinterpret_cast<const float4*>(bs + j * 32 * LDK + 4 * g);
-#pragma unroll
-            for (int j = 0; j < AN; ++j) {
-                tacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b[j].x, tacc[j], 0, 0, 0);
-                tacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b[j].y, tacc[j], 0, 0, 0);
-                tacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b[j].z, tacc[j], 0, 0, 0);
-                tacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b[j].w, tacc[j], 0, 0, 0);
+        for (int u = 0; u < FEU; ++u) {
+            ent[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (NS > 3) ent2[u] = make_float2(0.f, 0.f);
+            if (u < cnt) {
+                const float* e = S.list.entries + (long long)(st + u) * stride;
+                ent[u] = *reinterpret_cast<const float4*>(e);
+                if constexpr (NS > 3) ent2[u] = *reinterpret_cast<const float2*>(e + 4);
             }
         }
+        unsigned xoff[FEU];
 #pragma unroll
-        for (int j = 0; j < AN; ++j) acc[j] += tacc[j];
-        if (t + 1 < nch) store(t + 1, buf ^ 1);
+        for (int u = 0; u < FEU; ++u)
+            xoff[u] = u < cnt ? (unsigned)((long long)__float_as_int(ent[u].x) * ld + q * 4) * 4u : OOB;
+        float4 xg[FEU], rb[BF4], mu = make_float4(0.f, 0.f, 0.f, 0.f), sc = mu;
+        float bnb = 0.f, bnw = 0.f;
+        if (bn) {
+            bnb = *S.bn.b;
+            bnw = *S.bn.w;
+        }
+        auto load = [&](int cc) {
+#pragma unroll
+            for (int u = 0; u < FEU; ++u) xg[u] = ld4(rs_x, xoff[u] == OOB ? OOB : xoff[u] + cc * FCW * 4);
+            if (bn) {
+                mu = *reinterpret_cast<const float4*>(S.bn.mean + cc * FCW + q * 4);
+                sc = *reinterpret_cast<const float4*>(S.bn.std + cc * FCW + q * 4);
+            }
+#pragma unroll
+            for (int f = 0; f < BF4; ++f) {
+                const int e = tid + f * 256;
+                const int n = e / KC4, rem = e % KC4, sl = rem / (FCW / 4), cq = rem % (FCW / 4);
+                const int gn = n0 + n;
+                const bool ok = n < BN && gn < N && e < BN * KC4;
+                const long long o = (long long)gn * S.b_n + (long long)sl * S.b_s + cc * FCW + cq * 4;
+                rb[f] = ld4(rs_b, ok ? (unsigned)(o * 4) : OOB);
+            }
+        };
+        auto store = [&](int cc, int bf) {
+            float4 a[NS];
+#pragma unroll
+            for (int sl = 0; sl < NS; ++sl) a[sl] = make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 s4 = sc;
+            if (bn) s4 = make_float4(bn_scale(bnw, sc.x), bn_scale(bnw, sc.y), bn_scale(bnw, sc.z), bn_scale(bnw, sc.w));
+            auto bnx = [&](float4 x) {
+                if (!bn) return x;
+                return make_float4(bn_z_s(x.x, mu.x, s4.x, bnb), bn_z_s(x.y, mu.y, s4.y, bnb),
+                                   bn_z_s(x.z, mu.z, s4.z, bnb), bn_z_s(x.w, mu.w, s4.w, bnb));
+            };
+            auto add = [&](const float4& e4, const float2& e2, float4 x) {
+                a[0] = f4fma(e4.y, x, a[0]);
+                a[1] = f4fma(e4.z, x, a[1]);
+                if constexpr (NS > 2) a[2] = f4fma(e4.w, x, a[2]);
+                if constexpr (NS > 3) a[3] = f4fma(e2.x, x, a[3]);
+                if constexpr (NS > 4) a[4] = f4fma(e2.y, x, a[4]);
+            };
+#pragma unroll
+            for (int u = 0; u < FEU; ++u) {
+                float2 e2 = make_float2(0.f, 0.f);
+                if constexpr (NS > 3) e2 = ent2[u];
+                // a dead slot read 0 and has zero coefficients: BN must not turn it into b
+                const float4 x = xoff[u] == OOB ? xg[u] : bnx(xg[u]);
+                add(ent[u], e2, x);
+            }
+            // rows with more entries than registers (phantom-slot rows, high degrees): streamed
+            for (int u = FEU; u < cnt; ++u) {
+                const float* e = S.list.entries + (long long)(st + u) * stride;
+                const float4 e4 = *reinterpret_cast<const float4*>(e);
+                float2 e2 = make_float2(0.f, 0.f);
+                if constexpr (NS > 3) e2 = *reinterpret_cast<const float2*>(e + 4);
+                const unsigned o = (unsigned)((long long)__float_as_int(e4.x) * ld + cc * FCW + q * 4) * 4u;
+                add(e4, e2, bnx(ld4(rs_x, o)));
+            }
+            float* as = &As[bf][rr * LDK + q * 4];
+#pragma unroll
+            for (int sl = 0; sl < NS; ++sl) *reinterpret_cast<float4*>(as + sl * FCW) = a[sl];
+            if (EPI == FEPI_FWD && J.a_out && blockIdx.y == 0 && rvalid) {
+                // the aggregate in the reference's column order (slice-major), for the dW GEMM
+                float* ao = J.a_out + (long long)grow * J.lda_out + koff + cc * FCW + q * 4;
+#pragma unroll
+                for (int sl = 0; sl < NS; ++sl) *reinterpret_cast<float4*>(ao + (long long)sl * S.cs) = a[sl];
+            }
+#pragma unroll
+            for (int f = 0; f < BF4; ++f) {
+                const int e = tid + f * 256;
+                const int n = e / KC4, rem = e % KC4, sl = rem / (FCW / 4), cq = rem % (FCW / 4);
+                if (n < BN && e < BN * KC4) *reinterpret_cast<float4*>(&Bs[bf][n * LDK + sl * FCW + cq * 4]) = rb[f];
+            }
+        };
+        auto mfma = [&](int bf) {
+            const float* as = &As[bf][(wm * 32 + l31) * LDK + h * KH];
+            const float* bs = &Bs[bf][(wn * TN + l31) * LDK + h * KH];
+#pragma unroll
+            for (int j = 0; j < AN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) tacc[j][r] = 0.f;
+#pragma unroll
+            for (int g = 0; g < KH / 4; ++g) {
+                const float4 av = *reinterpret_cast<const float4*>(as + 4 * g);
+                float4 bv[AN];
+#pragma unroll
+                for (int j = 0; j < AN; ++j) bv[j] = *reinterpret_cast<const float4*>(bs + j * 32 * LDK + 4 * g);
+#pragma unroll
+                for (int j = 0; j < AN; ++j) {
+                    tacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv[j].x, tacc[j], 0, 0, 0);
+                    tacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv[j].y, tacc[j], 0, 0, 0);
+                    tacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv[j].z, tacc[j], 0, 0, 0);
+                    tacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv[j].w, tacc[j], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < AN; ++j) acc[j] += tacc[j];
+        };
+        load(0);
+        store(0, buf);
         __syncthreads();
-    }
+        for (int cc = 0; cc < nch; ++cc) {
+            if (cc + 1 < nch) load(cc + 1);
+            mfma(buf);
+            if (cc + 1 < nch) store(cc + 1, buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        }
+    };
+    using I2 = std::integral_constant<int, 2>;
+    using IJ = std::integral_constant<int, JT>;
+    // segment 0 is the operator list (J + 2 slices) unless this job gathers only {Pm, Pd}
+    if (J.seg[0].ns == 2) run_seg(I2{}, J.seg[0], 0);
+    else run_seg(IJ{}, J.seg[0], 0);
+    if (J.nseg > 1) run_seg(I2{}, J.seg[1], J.seg[0].ns * J.seg[0].cs);
 
     // ---- epilogue.  C/D layout of the 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
     if constexpr (EPI == FEPI_FWD) {
-        if (J.a_out && blockIdx.y == 0 && rvalid && tid < 4 * FBM) {
+        if (J.a_out && blockIdx.y == 0 && rvalid) {
             // zero the aggregate's row padding [K, lda_out): the dW GEMM runs over the padded width
             const int kk = J.seg[0].ns * J.seg[0].cs + (J.nseg > 1 ? J.seg[1].ns * J.seg[1].cs : 0);
             if (q < J.lda_out - kk) J.a_out[(long long)grow * J.lda_out + kk + q] = 0.f;
@@ -347,16 +346,27 @@ bool seg_ok(const FusedSeg& s) {
     if (!al(s.src) || s.ld % 4 != 0 || !al(s.b) || s.b_n % 4 != 0 || s.b_s % 4 != 0) return false;
     if (s.list.stride % 4 != 0 || (s.ns > 3 && s.list.stride < 8)) return false;
     if (s.bn.mean && (!al(s.bn.mean) || !al(s.bn.std))) return false;
+    if (s.src_bytes <= 0 || s.src_bytes > 0x7fffffffll || s.b_bytes <= 0 || s.b_bytes > 0x7fffffffll) return false;
     return true;
 }
 
-template <int BN, int NSM>
+template <int BN, int JT>
 int launch_bn(const FusedArgs& a, int epi, int grid_y, hipStream_t s) {
     const dim3 g(a.job[0].blocks + a.job[1].blocks, grid_y);
-    if (epi == FEPI_FWD) hipLaunchKernelGGL((k_fused<BN, NSM, FEPI_FWD>), g, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_fused<BN, NSM, FEPI_ACC>), g, dim3(256), 0, s, a);
+    if (epi == FEPI_FWD) hipLaunchKernelGGL((k_fused<BN, JT, FEPI_FWD>), g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_fused<BN, JT, FEPI_ACC>), g, dim3(256), 0, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;
+}
+
+template <int BN>
+int launch_jt(const FusedArgs& a, int epi, int jt, int grid_y, hipStream_t s) {
+    switch (jt) {
+        case 3: return launch_bn<BN, 3>(a, epi, grid_y, s);
+        case 4: return launch_bn<BN, 4>(a, epi, grid_y, s);
+        case 5: return launch_bn<BN, 5>(a, epi, grid_y, s);
+        default: return HGNN_ERR_UNSUPPORTED;
+    }
 }
 
 }  // namespace
@@ -372,7 +382,7 @@ bool fused_ok(const FusedJob& j) {
 }
 
 int launch_fused(FusedArgs a, int epi, hipStream_t s) {
-    int nsm = 0, nmax = 0;
+    int jt = 3, nmax = 0;
     for (int i = 0; i < 2; ++i) {
         FusedJob& j = a.job[i];
         if (i == 1 && j.nseg == 0) {
@@ -381,15 +391,19 @@ int launch_fused(FusedArgs a, int epi, hipStream_t s) {
         }
         if (!fused_ok(j)) return HGNN_ERR_UNSUPPORTED;
         if (epi == FEPI_FWD && (i == 1 || !j.bias)) return HGNN_ERR_ARG;
+        // segment 0: the operator list (J + 2 slices) or a {Pm, Pd} list; segment 1: {Pm, Pd}
+        if (j.seg[0].ns != 2) jt = j.seg[0].ns;
+        if (j.nseg > 1 && j.seg[1].ns != 2) return HGNN_ERR_UNSUPPORTED;
         j.blocks = fused_blocks(j.cap_rows);
-        for (int k = 0; k < j.nseg; ++k) nsm = std::max(nsm, j.seg[k].ns);
         nmax = std::max(nmax, j.n);
     }
+    for (int i = 0; i < 2; ++i)
+        if (a.job[i].nseg && a.job[i].seg[0].ns != 2 && a.job[i].seg[0].ns != jt) return HGNN_ERR_UNSUPPORTED;
+    if (jt < 3) return HGNN_ERR_UNSUPPORTED;
     if (a.job[0].blocks + a.job[1].blocks == 0) return 0;
     // 64-column tiles up to N = 64 (d <= 32), else 128-column tiles (grid.y = ceil(N / 128))
-    if (nmax <= 64) return nsm <= 3 ? launch_bn<64, 3>(a, epi, 1, s) : launch_bn<64, 5>(a, epi, 1, s);
-    const int gy = ceil_div(nmax, 128);
-    return nsm <= 3 ? launch_bn<128, 3>(a, epi, gy, s) : launch_bn<128, 5>(a, epi, gy, s);
+    if (nmax <= 64) return launch_jt<64>(a, epi, jt, 1, s);
+    return launch_jt<128>(a, epi, jt, ceil_div(nmax, 128), s);
 }
 
 }  // namespace hgnn

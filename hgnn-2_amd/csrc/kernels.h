@@ -207,11 +207,11 @@ int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o,
 struct FusedSeg {
     StructView list;      // row lists over the job's output rows
     const float* src;     // gathered rows [src_rows][ld]
-    long long ld;
+    long long ld, src_bytes;  // src_bytes: the whole gathered matrix (buffer-load range, <= 2 GB)
     int cs, ns;           // channels (multiple of 16), slices (entry coefficients 1 .. ns)
     BnView bn;            // BN applied on load (mean == nullptr: none)
     const float* b;
-    long long b_n, b_s;
+    long long b_n, b_s, b_bytes;  // b_bytes: range of b (buffer-load range)
 };
 struct FusedJob {
     const int* total_rows;  // device row count of the output

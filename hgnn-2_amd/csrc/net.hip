@@ -54,7 +54,8 @@ struct Program {
     int entry_stride_w = 4;
     size_t dy = 0, dy2 = 0, da = 0, da2 = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0, dbpart2 = 0;
     bool v2 = false;  // GEMM v2 path (2d % 4 == 0); gemm.hip otherwise
-    bool fused = false;  // fused aggregation + GEMM (fused.hip): 2d % 16 == 0, 2d <= 256
+    bool fused = false;      // fused aggregation + GEMM forward (fused.hip): 2d % 16 == 0, 2d <= 256
+    bool fused_bwd = false;  // fused backward dX (HGNN_FUSED_BWD=1; see DESIGN.md §8 for why it is off)
     size_t bytes = 0;
 };
 
@@ -84,10 +85,15 @@ bool valid_config(const hgnn_net_config* c) {
 
 // HGNN_FUSED=0 selects the unfused kernels (aggregation -> [rows][K] buffer -> GEMM; dA GEMM ->
 // transposed aggregation) for A/B runs; the parity tests run both.
-static bool fused_enabled() {
-    const char* e = getenv("HGNN_FUSED");
-    return !(e && e[0] == '0');
+static bool env_flag(const char* name, bool dflt) {
+    const char* e = getenv(name);
+    if (!e || !e[0]) return dflt;
+    return e[0] != '0';
 }
+static bool fused_enabled() { return env_flag("HGNN_FUSED", true); }
+
+// Row capacity of a feature's buffer.
+static int feat_rows(const Program& P, int f) { return P.feats[f].edge ? P.cap_e : P.cap_n; }
 
 // A half whose aggregation is gathered inside the GEMM (both input widths multiples of 16).
 static bool fused_fwd_half(const Program& P, const Half& h) {
@@ -234,6 +240,7 @@ Program build_program(const hgnn_net_config* c) {
     int max_cap = 0;
     P.v2 = (P.c2 % 4) == 0;
     P.fused = P.v2 && P.c2 % 16 == 0 && P.c2 <= 256 && fused_enabled();
+    P.fused_bwd = P.fused && env_flag("HGNN_FUSED_BWD", false);
     for (auto& h : P.halves) {
         const int cap = h.edge ? P.cap_e : P.cap_n;
         h.kp = P.v2 ? (h.k + 3) / 4 * 4 : h.k;
@@ -456,23 +463,27 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
             g.list = src.v[h.edge ? S_WL : S_W];
             g.src = feat_src(P, ws, h.gin, src.x0, src.xl0);
             g.ld = h.cg;
+            g.src_bytes = (long long)feat_rows(P, h.gin) * h.cg * 4;
             g.cs = h.cg;
             g.ns = P.jt;
             g.bn = feat_bn(P, ws, prm, h.gin);
             g.b = at<float>(ws, h.wc);
             g.b_n = h.kp;
             g.b_s = h.cg;
+            g.b_bytes = (long long)P.c2 * h.kp * 4;
             if (h.pin >= 0) {
                 FusedSeg& pp = j.seg[1];
                 pp.list = src.v[h.edge ? S_PE : S_PN];
                 pp.src = feat_src(P, ws, h.pin, src.x0, src.xl0);
                 pp.ld = h.cp;
+                pp.src_bytes = (long long)feat_rows(P, h.pin) * h.cp * 4;
                 pp.cs = h.cp;
                 pp.ns = 2;
                 pp.bn = feat_bn(P, ws, prm, h.pin);
                 pp.b = at<float>(ws, h.wc) + (size_t)P.jt * h.cg;
                 pp.b_n = h.kp;
                 pp.b_s = h.cp;
+                pp.b_bytes = ((long long)P.c2 * h.kp - (long long)P.jt * h.cg) * 4;
             }
             j.n = P.c2;
             j.out = at<float>(ws, P.feats[h.out].y);
@@ -623,7 +634,7 @@ static bool fused_da_enabled() {
 
 int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
                  const float* const* prm, void* ws, const float* dout, float* const* grads, float* dX, float* dW,
-                 hipStream_t s, Timer* tm) {
+                 hipStream_t s, Timer* tm, void* const* ev = nullptr, int n_ev = 0) {
     const Program P = build_program(c);
     if (!fits_32bit(P)) return HGNN_ERR_UNSUPPORTED;
     const Src src = make_src(P, ws, csr);
@@ -752,7 +763,18 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         pending[parity] = true;
         return r;
     };
-    for (int hi = (int)P.halves.size() - 1; hi >= 0; --hi, parity ^= 1) {
+    // per-layer completion events (hgnn_net_backward_ex): recorded once the first half (in program
+    // order) of a layer -- the last one the reverse walk reaches -- has been enqueued
+    const bool lgk = c->kind == 1;
+    auto mark = [&](int hd) -> int {
+        if (!ev || n_ev <= 0 || (lgk && hd % 2 != 0)) return 0;
+        const int l = lgk ? hd / 2 : hd;
+        if (2 * l + 1 >= n_ev) return 0;
+        HGNN_HOST_CHECK(hipEventRecord(static_cast<hipEvent_t>(ev[2 * l]), s));
+        HGNN_HOST_CHECK(hipEventRecord(static_cast<hipEvent_t>(ev[2 * l + 1]), side ? side->s : s));
+        return 0;
+    };
+    auto half_bwd = [&](int hi) -> int {
         const Half& h = P.halves[hi];
         const int cap = h.edge ? P.cap_e : P.cap_n;
         const int* tot = h.edge ? tot_e : tot_n;
@@ -784,16 +806,16 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
         const bool ndw = need_dw && !h.edge;
         // with a dA GEMM the BN backward's apply pass is fused into its operand staging
-        const bool fused_da = !P.fused && P.v2 && (ng || np || ndw) && fused_da_enabled();
+        const bool fused_da = !P.fused_bwd && P.v2 && (ng || np || ndw) && fused_da_enabled();
         TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s, fused_da ? 0 : 1));
 
-        if (P.fused) {
+        if (P.fused_bwd) {
             // dW (and the dense operator gradient) on the side stream, dX on the main stream:
             // dX_gin (+)= (W^T dY) Wcat_G and dX_pin (+)= ({Pm, Pd}^T dY) Wcat_P, gathered from the
             // 2d-wide dY rows inside the GEMM (fused.hip) -- no [rows][K] dA buffer
             float* da = at<float>(ws, parity ? P.da2 : P.da);
             TRY(fork_dw(h, cap, tot, dyb, dbp, ndw, da, true));
-            if (!ng && !np) continue;
+            if (!ng && !np) return 0;
             FusedArgs fa{};
             int nj = 0;
             if (ng) {
@@ -805,11 +827,13 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
                 g.list = src.v[h.edge ? S_WLT : S_WT];
                 g.src = dyb;
                 g.ld = P.c2;
+                g.src_bytes = (long long)cap * P.c2 * 4;
                 g.cs = P.c2;
                 g.ns = P.jt;
                 g.b = at<float>(ws, h.wt);
                 g.b_n = P.c2;
                 g.b_s = (long long)h.cg * P.c2;
+                g.b_bytes = (long long)h.k * P.c2 * 4;
                 j.n = h.cg;
                 j.out = at<float>(ws, P.feats[h.gin].grad);
                 j.ldo = h.cg;
@@ -825,11 +849,13 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
                 g.list = src.v[h.edge ? S_PN : S_PE];
                 g.src = dyb;
                 g.ld = P.c2;
+                g.src_bytes = (long long)cap * P.c2 * 4;
                 g.cs = P.c2;
                 g.ns = 2;
                 g.b = at<float>(ws, h.wt) + (size_t)P.jt * h.cg * P.c2;
                 g.b_n = P.c2;
                 g.b_s = (long long)h.cp * P.c2;
+                g.b_bytes = ((long long)h.k - (long long)P.jt * h.cg) * P.c2 * 4;
                 j.n = h.cp;
                 j.out = at<float>(ws, P.feats[h.pin].grad);
                 j.ldo = h.cp;
@@ -838,7 +864,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             TL(HGNN_K_FUSED_BWD, launch_fused(fa, FEPI_ACC, s));
             if (ng) init[h.gin] = 1;
             if (np) init[h.pin] = 1;
-            continue;
+            return 0;
         }
 
         if (!P.v2) {
@@ -862,7 +888,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
 
         if (!ng && !np && !ndw) {
             if (P.v2) TRY(fork_dw(h, cap, tot, dyb, dbp, false, nullptr));
-            continue;
+            return 0;
         }
         float* da = at<float>(ws, (P.v2 && parity) ? P.da2 : P.da);
         if (P.v2) {
@@ -925,6 +951,11 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         else if (np) TL(HGNN_K_AGG_BWD, launch_agg_bwd(pab, s));
         if (ng) init[h.gin] = 1;
         if (np) init[h.pin] = 1;
+        return 0;
+    };
+    for (int hi = (int)P.halves.size() - 1; hi >= 0; --hi, parity ^= 1) {
+        TRY(half_bwd(hi));
+        TRY(mark(hi));
     }
     for (int p = 0; p < 2; ++p)
         if (pending[p]) HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[p], 0));
@@ -1093,6 +1124,17 @@ int hgnn_net_forward_csr(const hgnn_net_config* cfg, const hgnn_csr_batch* batch
     if (!valid_config(cfg) || !csr_matches(cfg, batch) || !params || !workspace || !d_out) return HGNN_ERR_ARG;
     return net_forward(cfg, nullptr, batch, params, bn_running, workspace, d_out, static_cast<hipStream_t>(stream),
                        nullptr);
+}
+
+int hgnn_net_backward_ex(const hgnn_net_config* cfg, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
+                         const float* const* params, void* workspace, const float* d_dout, float* const* grads,
+                         float* d_dX, float* d_dW, void* stream, void* timer, void* const* events, int n_events) {
+    if (!valid_config(cfg) || !params || !workspace || !d_dout || !grads) return HGNN_ERR_ARG;
+    if (csr && (!csr_matches(cfg, csr) || cfg->need_dw)) return HGNN_ERR_ARG;
+    if (!csr && cfg->need_dw && (!in || !in->d_X)) return HGNN_ERR_ARG;
+    if (n_events < 0 || (n_events > 0 && !events)) return HGNN_ERR_ARG;
+    return net_backward(cfg, in, csr, params, workspace, d_dout, grads, d_dX, d_dW, static_cast<hipStream_t>(stream),
+                        static_cast<Timer*>(timer), events, n_events);
 }
 
 int hgnn_net_backward_csr(const hgnn_net_config* cfg, const hgnn_csr_batch* batch, const float* const* params,

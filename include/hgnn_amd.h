@@ -129,6 +129,22 @@ int hgnn_net_backward(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
                       const float* d_dout, float* const* grads,
                       float* d_dX, float* d_dW, void* stream);
 
+struct hgnn_csr_batch;  /* defined below (native sparse batcher) */
+
+/* Extended backward: the batch comes from `in` (dense) or `csr` (exactly one non-NULL), an
+ * optional launch timer, and optional per-layer completion events for overlapping a gradient
+ * all-reduce with the rest of the backward: events[2 l] is recorded on `stream`
+ * and events[2 l + 1] on the executor's side stream once every gradient of layer l
+ * (l = 0 .. n_layers - 2; layerlast.fc counts as layer n_layers - 2) has been enqueued on
+ * that stream -- a communication stream that waits on both may reduce layer l's gradients
+ * while layers < l are still being differentiated.  events: hipEvent_t handles;
+ * n_events = 2 (n_layers - 1), or 0 for none. */
+int hgnn_net_backward_ex(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
+                         const struct hgnn_csr_batch* csr, const float* const* params,
+                         void* workspace, const float* d_dout, float* const* grads,
+                         float* d_dX, float* d_dW, void* stream, void* timer,
+                         void* const* events, int n_events);
+
 /* Kernel classes for the optional launch timer (bench.py measures the
  * dominant kernel with HIP events on the launching stream, inside its timed
  * region).  A timer records a start/stop event pair around every launch of a
