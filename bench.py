@@ -192,7 +192,8 @@ def main():
 
     # the dominant class, plus the two aggregation classes: the north_star's HBM-roofline target is
     # on the aggregation (sparse operator x feature gathers) of the forward
-    hbm_classes = [RF.K_AGG_FWD, RF.K_AGG_BWD] + ([RF.K_FUSED_FWD, RF.K_FUSED_BWD] if RF.fused_net(args.d) else [])
+    hbm_classes = [RF.K_AGG_FWD, RF.K_AGG_BWD] + ([RF.K_FUSED_FWD] if RF.fused_net(args.d) else []) + \
+        ([RF.K_FUSED_BWD] if RF.fused_bwd(args.d) else [])
     timed = [dominant] + [k for k in hbm_classes if k != dominant] if dominant is not None else []
     max_launch = sum(per[k][1] for k in timed) // prof_steps if dominant is not None else 0
     timer = KernelTimer(max(1, max_launch * args.steps + 8), timed) if dominant is not None else None

@@ -83,14 +83,18 @@ bool valid_config(const hgnn_net_config* c) {
     return true;
 }
 
-// HGNN_FUSED=0 selects the unfused kernels (aggregation -> [rows][K] buffer -> GEMM; dA GEMM ->
-// transposed aggregation) for A/B runs; the parity tests run both.
+// HGNN_FUSED=1 selects the fused aggregation + GEMM forward (fused.hip) instead of aggregation ->
+// [rows][K] buffer -> GEMM; HGNN_FUSED_BWD=1 in addition the fused backward dX.  The parity tests
+// run every combination.
 static bool env_flag(const char* name, bool dflt) {
     const char* e = getenv(name);
     if (!e || !e[0]) return dflt;
     return e[0] != '0';
 }
-static bool fused_enabled() { return env_flag("HGNN_FUSED", true); }
+// Off by default: measured on the box (bench.py, same tree) 1.71-1.73 ms per step with the fused
+// forward against 1.59 unfused -- the fused kernel keeps the MFMA pipes ~26 % busy (rocprof
+// SQ_VALU_MFMA_BUSY_CYCLES), its producer and MFMA phases do not overlap enough yet.
+static bool fused_enabled() { return env_flag("HGNN_FUSED", false); }
 
 // Row capacity of a feature's buffer.
 static int feat_rows(const Program& P, int f) { return P.feats[f].edge ? P.cap_e : P.cap_n; }

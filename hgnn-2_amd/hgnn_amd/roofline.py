@@ -49,7 +49,7 @@ def lg_halves(order, f_in, d, n_layers, jt):
 def fused_net(d):
     """Mirror of net.hip build_program's P.fused (fused aggregation + GEMM kernels in use)."""
     import os
-    return (2 * d) % 16 == 0 and 2 * d <= 256 and os.environ.get("HGNN_FUSED", "1") != "0"
+    return (2 * d) % 16 == 0 and 2 * d <= 256 and os.environ.get("HGNN_FUSED", "0") not in ("", "0")
 
 
 def fused_bwd(d):
@@ -190,7 +190,7 @@ def pmc_traffic(kcls, path):
 def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, steps, jt=3, pmc_path=None):
     """bench.py 'roofline' object for a kernel class measured over `steps` steps."""
     fl, by = class_work(kcls, counts, order, f_in, d, n_layers, jt)
-    sec = ms_total / 1e3
+    sec = max(ms_total / 1e3, 1e-12)
     if kcls in (K_GEMM_FWD, K_GEMM_DA, K_GEMM_DW, K_FUSED_FWD, K_FUSED_BWD):
         achieved = fl * steps / sec / 1e12
         peak, unit, bound = PEAK_FP32_MFMA_TFS, "TFLOP/s", "mfma"
