@@ -52,11 +52,17 @@ def parse():
     return ap.parse_args()
 
 
-def make_batch(bs, seed):
+def make_batch(bs, seed, world=1, rank=0):
+    """This rank's share of a global batch of bs * world QM9-shape graphs: Σ(N+M)-balanced shards
+    (hgnn_amd.dp.shard_graphs, SURVEY.md §8 e); the reference's dense padded 11-tuple."""
     import hgnn_amd.datagen as dg
     from functions.batching import prepare_batch
     from functions.operators import graph_operators
-    graphs = dg.qm9_shape_dataset(bs, seed=seed)
+    from hgnn_amd.dp import graph_cost, shard_graphs
+    graphs = dg.qm9_shape_dataset(bs * world, seed=seed)
+    if world > 1:
+        mine = shard_graphs([graph_cost(X, A) for X, A, _ in graphs], world)[rank]
+        graphs = [graphs[i] for i in mine]
     data = [[X, A, t, *graph_operators([X, A], 1, True)] for X, A, t in graphs]
     return list(prepare_batch(data, 0, 1))
 
@@ -145,13 +151,15 @@ def main():
     torch.manual_seed(0)
     model = GNN_lg(0, args.d, args.layers, 5, 1, 1, args.order).to(dev)
     params = list(model.parameters())
-    batch_cpu = make_batch(args.bs, 1000 + rank)
+    batch_cpu = make_batch(args.bs, 1000, world, rank)
     X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = [t.to(dev) for t in batch_cpu]
     X.requires_grad_(True)
     W.requires_grad_(True)
     crit = torch.nn.MSELoss()
-    from hgnn_amd.dp import GradAllReduce
-    allreduce = GradAllReduce(params)
+    from hgnn_amd.dp import GradAllReduce, LayerBucketAllReduce
+    # N > 1: per-layer gradient buckets reduced on a communication stream while the executor's
+    # backward is still running (its per-layer events), BN running statistics averaged
+    allreduce = LayerBucketAllReduce(model) if world > 1 and not args.graph else GradAllReduce(params)
     last_out = [None]
 
     def compute():

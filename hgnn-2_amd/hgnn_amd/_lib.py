@@ -110,6 +110,8 @@ SIGNATURES = {
     "hgnn_csr_batch_plan": ([_I, _VP, _VP, _I, _I, _I, ctypes.POINTER(CsrLayout)], _I),
     "hgnn_csr_batch_build": ([_I, _VP, _VP, _VP, _I, _I, _I, ctypes.POINTER(CsrLayout), _VP], _I),
     "hgnn_csr_batch_view": ([ctypes.POINTER(CsrLayout), _VP, ctypes.POINTER(CsrBatch)], _I),
+    "hgnn_net_backward_ex": ([ctypes.POINTER(NetConfig), ctypes.POINTER(NetInputs), ctypes.POINTER(CsrBatch), _VP, _VP,
+                              _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I], _I),
     "hgnn_net_forward_csr": ([ctypes.POINTER(NetConfig), ctypes.POINTER(CsrBatch), _VP, _VP, _VP, _VP, _VP], _I),
     "hgnn_net_backward_csr": ([ctypes.POINTER(NetConfig), ctypes.POINTER(CsrBatch), _VP, _VP, _VP, _VP, _VP,
                                _VP], _I),

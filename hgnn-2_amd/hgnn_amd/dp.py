@@ -1,20 +1,68 @@
-"""Batch-axis data parallelism for the drop-in models (SURVEY.md §8 e).
+"""Batch-axis data parallelism for the drop-in models (SURVEY.md §8 e, DESIGN.md §6).
 
 Graphs are independent except for the batch statistics of BN and the padded
 sizes Nmax/Emax, so the natural shard is the batch axis: every rank runs the
-full network on its own graphs and the only exchange is one all-reduce of the
-gradients (torch.distributed "nccl" = RCCL over xGMI on MI355X; "gloo" in the
+full network on its own graphs and the only exchange is the gradient
+all-reduce (torch.distributed "nccl" = RCCL over xGMI on MI355X; "gloo" in the
 CPU tests).  With gradient-only all-reduce each rank normalises BN over its
-own shard: the result equals "world reference batches, gradients averaged",
-which is what tests/test_dp_cpu.py checks.
+own shard: the result equals "world reference batches, gradients averaged"
+(the reference itself has one batch, models/layers/batch_normalization.py:80-93),
+which tests/test_dp_cpu.py and tests/test_gpu_dp.py check.
 
-The gradient set is small (2.1 MB at d = 64, 8.4 MB at d = 128), so it goes as
-one flat bucket: one latency-bound collective per step instead of one per
-parameter.
+* shard_graphs: the global batch split into `world` shards balanced by the
+  per-graph work N + M (nodes + edge slots, the rows every kernel walks),
+  longest-processing-time first, so ragged graphs do not leave a rank idle.
+* LayerBucketAllReduce: one gradient bucket per layer (layerlast.fc rides with
+  the last layer).  The network executor records two HIP events per layer in
+  its backward (hgnn_net_backward_ex: main stream and the weight-GEMM side
+  stream); a communication stream waits on them and all-reduces that layer's
+  bucket while the earlier layers are still being differentiated.  The
+  gradients are written by the executor straight into one flat buffer, so the
+  collective needs no packing copies.
+* average_running_stats: the BN running statistics (plain attributes, not
+  state, batch_normalization.py:30-38) averaged across ranks after a step, so
+  every rank -- and a checkpoint written by rank 0 -- holds the same eval-mode
+  statistics.
+* GradAllReduce: the single flat all-reduce for any module (used by TrainStep
+  when no executor events are available).
 """
+
+import weakref
 
 import torch
 import torch.distributed as dist
+
+# model -> its LayerBucketAllReduce (kept outside the module so torch.save(model) stays the
+# reference's plain whole-module pickle, functions/logs.py:99-111)
+_ATTACHED = weakref.WeakKeyDictionary()
+
+
+def attached(model):
+    return _ATTACHED.get(model)
+
+
+def graph_cost(X, A):
+    """Work of one graph for balancing: nodes + edge slots (M = nnz(A), functions/operators.py:36)."""
+    return int(X.shape[0]) + int((A != 0).sum())
+
+
+def shard_graphs(costs, world):
+    """Split graph indices into `world` shards of near-equal total cost (LPT: longest first onto
+    the least-loaded shard; ties to the lower rank).  Each shard keeps the original order."""
+    costs = list(costs)
+    loads = [0] * world
+    owner = [0] * len(costs)
+    for i in sorted(range(len(costs)), key=lambda i: (-costs[i], i)):
+        r = min(range(world), key=lambda k: (loads[k], k))
+        owner[i] = r
+        loads[r] += costs[i]
+    return [[i for i in range(len(costs)) if owner[i] == r] for r in range(world)]
+
+
+def _world(group):
+    if not dist.is_available() or not dist.is_initialized():
+        return 1
+    return dist.get_world_size(group)
 
 
 class GradAllReduce:
@@ -23,12 +71,9 @@ class GradAllReduce:
     def __init__(self, params, group=None):
         self.params = [p for p in params]
         self.group = group
-        self._flat = None
 
     def __call__(self):
-        if not dist.is_available() or not dist.is_initialized():
-            return
-        world = dist.get_world_size(self.group)
+        world = _world(self.group)
         if world == 1:
             return
         grads = []
@@ -36,8 +81,7 @@ class GradAllReduce:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
             grads.append(p.grad)
-        # one concatenation, one collective, one multi-tensor copy back: a handful of launches
-        # instead of two copies per parameter (49 tensors for GNN_lg)
+        # one concatenation, one collective, one multi-tensor copy back
         flat = torch.cat([g.reshape(-1) for g in grads])
         dist.all_reduce(flat, group=self.group)  # SUM on every backend (gloo has no AVG)
         flat.div_(world)
@@ -48,3 +92,101 @@ class GradAllReduce:
             views.append(flat[off:off + k].view_as(g))
             off += k
         torch._foreach_copy_(grads, views)
+
+
+def running_stats(model):
+    """The BN running statistics tensors of a GNN_lg / GNN_simple drop-in (bn1, bn2 per layer)."""
+    out = []
+    for layer in model._layers():
+        for nm in ("bn1", "bn2"):
+            bn = getattr(layer, nm, None)
+            if bn is not None:
+                out += [bn.running_mean, bn.running_std]
+    return out
+
+
+def average_running_stats(model, group=None):
+    world = _world(group)
+    if world == 1:
+        return
+    ts = running_stats(model)
+    flat = torch.cat([t.reshape(-1) for t in ts])
+    dist.all_reduce(flat, group=group)
+    flat.div_(world)
+    off = 0
+    views = []
+    for t in ts:
+        views.append(flat[off:off + t.numel()].view_as(t))
+        off += t.numel()
+    torch._foreach_copy_(ts, views)
+
+
+class LayerBucketAllReduce:
+    """Per-layer gradient buckets of a drop-in GNN, reduced during the executor's backward.
+
+    Attaches itself to `model` (dp.attached(model)): the executor then writes every parameter gradient
+    into self.flat and records the per-layer events.  Call the object after loss.backward():
+    it enqueues, last layer first, a wait on the layer's events and the all-reduce of its
+    bucket on a communication stream, then joins that stream and divides by the world size.
+    sync_running=True also averages the BN running statistics.
+    """
+
+    def __init__(self, model, group=None, sync_running=True):
+        self.model = model
+        self.group = group
+        self.sync_running = sync_running
+        spec = model._spec(next(model.parameters()).device)
+        self.params = list(spec.params)
+        dev = self.params[0].device
+        self.device = dev
+        per = 12 if spec.kind == 1 else 6
+        n_layers = spec.n_layers - 1
+        sizes = [p.numel() for p in self.params]
+        self.flat = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
+        self.views = []
+        off = 0
+        for p, k in zip(self.params, sizes):
+            self.views.append(self.flat[off:off + k].view_as(p))
+            off += k
+        # bucket l = layer l's parameters; the fc pair joins the last layer's bucket
+        self.buckets = []
+        off = 0
+        for l in range(n_layers):
+            n = sum(sizes[l * per:(l + 1) * per]) + (sizes[-2] + sizes[-1] if l == n_layers - 1 else 0)
+            self.buckets.append((off, n))
+            off += n
+        assert off == self.flat.numel()
+        self.events = []
+        if dev.type == "cuda":
+            cur = torch.cuda.current_stream(dev)
+            for _ in range(2 * n_layers):
+                ev = torch.cuda.Event()
+                ev.record(cur)  # materialise the HIP event; the executor re-records it
+                self.events.append(ev)
+            self.comm = torch.cuda.Stream(dev)
+        self.event_handles = [int(e.cuda_event) for e in self.events]
+        _ATTACHED[model] = self
+
+    def __call__(self):
+        world = _world(self.group)
+        # the executor wrote into self.views; autograd may have copied instead of stealing them
+        for p, v in zip(self.params, self.views):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v
+        if world == 1:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for l in reversed(range(len(self.buckets))):
+            self.comm.wait_event(self.events[2 * l])
+            self.comm.wait_event(self.events[2 * l + 1])
+            off, n = self.buckets[l]
+            with torch.cuda.stream(self.comm):
+                dist.all_reduce(self.flat[off:off + n], group=self.group)
+        cur.wait_stream(self.comm)
+        self.flat.div_(world)
+        if self.sync_running:
+            average_running_stats(self.model, self.group)
+
+    def detach(self):
+        if _ATTACHED.get(self.model) is self:
+            del _ATTACHED[self.model]

@@ -136,7 +136,8 @@ def _i64(t):
 class NetSpec:
     """Static description of a network call (model hyper-parameters + mode)."""
 
-    def __init__(self, kind, order, d, n_layers, dim_out, params, running, training):
+    def __init__(self, kind, order, d, n_layers, dim_out, params, running, training, dp=None):
+        self.dp = dp  # hgnn_amd.dp.LayerBucketAllReduce: flat gradient buffer + per-layer events
         self.kind = kind
         self.order = order
         self.d = d
@@ -218,6 +219,7 @@ class _NetFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.ws = ws
         ctx.inp = inp
+        ctx.spec = spec
         ctx.keep = (X, W, XL, WL, Pm, Pd, Nb, Eb, mask, mask_lg)
         ctx.params = params
         return out
@@ -227,20 +229,30 @@ class _NetFn(torch.autograd.Function):
         cfg = ctx.cfg
         X = ctx.keep[0]
         dout = dout.contiguous().to(torch.float32)
-        grads = [torch.empty_like(p) for p in ctx.params]
+        grads, evs, nev = _grad_targets(ctx.spec, ctx.params)
         dX = torch.empty_like(X) if ctx.needs_input_grad[2] else None
         dW = torch.empty_like(ctx.keep[1]) if ctx.needs_input_grad[3] else None
         cfg.need_dx = 1 if dX is not None else 0
         cfg.need_dw = 1 if dW is not None else 0
-        args = (ctypes.byref(cfg), ctypes.byref(ctx.inp), L.ptr_array(ctx.params), ctypes.c_void_p(ctx.ws.data_ptr()),
-                ctypes.c_void_p(dout.data_ptr()), L.ptr_array(grads), L.ptr(dX), L.ptr(dW), L.stream_handle(X.device))
         with torch.cuda.device(X.device):
-            if _timer is not None:
-                st = L.lib().hgnn_net_backward_timed(*args, ctypes.c_void_p(_timer.handle))
-            else:
-                st = L.lib().hgnn_net_backward(*args)
+            st = L.lib().hgnn_net_backward_ex(
+                ctypes.byref(cfg), ctypes.byref(ctx.inp), None, L.ptr_array(ctx.params),
+                ctypes.c_void_p(ctx.ws.data_ptr()), ctypes.c_void_p(dout.data_ptr()), L.ptr_array(grads), L.ptr(dX),
+                L.ptr(dW), L.stream_handle(X.device), ctypes.c_void_p(_timer.handle) if _timer is not None else None,
+                evs, nev)
         L.check(st, "network backward")
         return (None, None, dX, dW, *grads)
+
+
+def _grad_targets(spec, params):
+    """Gradient buffers for the backward: views into the data-parallel flat buffer (with its
+    per-layer events) when a LayerBucketAllReduce is attached, else fresh tensors."""
+    dp = spec.dp
+    if dp is not None and len(dp.views) == len(params) and all(
+            v.shape == p.shape and v.device == p.device for v, p in zip(dp.views, params)):
+        evs = (ctypes.c_void_p * max(1, len(dp.event_handles)))(*dp.event_handles)
+        return list(dp.views), evs, len(dp.event_handles)
+    return [torch.empty_like(p) for p in params], None, 0
 
 
 def run_net(spec, X, W, N_batch, mask, XL=None, WL=None, Pm=None, Pd=None, E_batch=None, mask_lg=None):
@@ -340,7 +352,7 @@ class _NetCsrFn(torch.autograd.Function):
                                          L.ptr_array(spec.running), ctypes.c_void_p(ws.data_ptr()),
                                          ctypes.c_void_p(out.data_ptr()), L.stream_handle(dev)),
                 "network forward (csr)")
-        ctx.cfg, ctx.ws, ctx.batch, ctx.params = cfg, ws, batch, params
+        ctx.cfg, ctx.ws, ctx.batch, ctx.params, ctx.spec = cfg, ws, batch, params, spec
         return out
 
     @staticmethod
@@ -348,15 +360,16 @@ class _NetCsrFn(torch.autograd.Function):
         cfg = ctx.cfg
         batch = ctx.batch
         dout = dout.contiguous().to(torch.float32)
-        grads = [torch.empty_like(p) for p in ctx.params]
+        grads, evs, nev = _grad_targets(ctx.spec, ctx.params)
         dX = torch.empty(batch.nodes, batch.f_in, dtype=torch.float32, device=batch.device) \
             if ctx.needs_input_grad[2] else None
         cfg.need_dx = 1 if dX is not None else 0
         cfg.need_dw = 0
         with torch.cuda.device(batch.device):
-            st = L.lib().hgnn_net_backward_csr(ctypes.byref(cfg), ctypes.byref(batch.view), L.ptr_array(ctx.params),
+            st = L.lib().hgnn_net_backward_ex(ctypes.byref(cfg), None, ctypes.byref(batch.view), L.ptr_array(ctx.params),
                                               ctypes.c_void_p(ctx.ws.data_ptr()), ctypes.c_void_p(dout.data_ptr()),
-                                              L.ptr_array(grads), L.ptr(dX), L.stream_handle(batch.device))
+                                              L.ptr_array(grads), L.ptr(dX), None, L.stream_handle(batch.device),
+                                              None, evs, nev)
         L.check(st, "network backward (csr)")
         return (None, None, dX, *grads)
 

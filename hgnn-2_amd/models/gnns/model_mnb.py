@@ -16,6 +16,7 @@ training mode exactly as the reference rebinds them.
 import torch
 import torch.nn as nn
 
+from hgnn_amd.dp import attached
 from hgnn_amd.net import NetSpec, run_net, run_net_csr
 from models.layers import layers_mnb
 
@@ -59,7 +60,7 @@ class GNN_simple(nn.Module):
             running += list(layer.bn1.running_on(device))
         params += [self.layerlast.fc.weight, self.layerlast.fc.bias]
         return NetSpec(kind=0, order=0, d=self.n_features, n_layers=self.n_layers, dim_out=self.n_outputs,
-                       params=params, running=running, training=self.training)
+                       params=params, running=running, training=self.training, dp=attached(self))
 
     def forward(self, state, N_batch, mask):
         X, W = state
@@ -107,7 +108,7 @@ class GNN_lg(nn.Module):
         params += [self.layerlast.fc.weight, self.layerlast.fc.bias]
         order = self.order if self.order in (1, 2) else 3
         return NetSpec(kind=1, order=order, d=self.n_features, n_layers=self.n_layers, dim_out=self.n_outputs,
-                       params=params, running=running, training=self.training)
+                       params=params, running=running, training=self.training, dp=attached(self))
 
     def forward(self, state, N_batch, mask, E_batch, mask_lg):
         X, XL, W, WL, Pm, Pd = state

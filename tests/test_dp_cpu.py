@@ -83,3 +83,22 @@ def test_gloo_world2_grad_allreduce_matches_shard_average():
         v = torch.from_numpy(v)
         ref = (g0[k].grad + g1[k].grad) / 2
         assert torch.allclose(v, ref, rtol=1e-6, atol=1e-7), k
+
+
+def test_shard_graphs_balanced_partition():
+    """Σ(N+M)-balanced LPT sharding: a partition, loads within one graph's cost of each other."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "hgnn-2_amd"))
+    import hgnn_amd.datagen as dg
+    from hgnn_amd.dp import graph_cost, shard_graphs
+    graphs = dg.qm9_shape_dataset(4096, seed=3)
+    costs = [graph_cost(X, A) for X, A, _ in graphs]
+    for world in (1, 2, 4, 8):
+        sh = shard_graphs(costs, world)
+        assert sorted(i for s in sh for i in s) == list(range(len(costs)))
+        assert all(s == sorted(s) for s in sh)
+        loads = [sum(costs[i] for i in s) for s in sh]
+        assert max(loads) - min(loads) <= max(costs)
+        counts = [len(s) for s in sh]
+        assert max(counts) - min(counts) <= max(1, len(costs) // (world * 20)), counts
+    assert shard_graphs([3, 1, 2], 2) == [[0], [1, 2]]

@@ -1,0 +1,145 @@
+"""World-size-2 data parallelism with the real HIP executor (SURVEY.md §8 e).
+
+Two ranks (gloo on GPU tensors, both on cuda:0) take Σ(N+M)-balanced shards of one global batch
+(hgnn_amd.dp.shard_graphs), run GNN_lg forward + backward through the executor with the per-layer
+bucketed all-reduce (hgnn_amd.dp.LayerBucketAllReduce: the executor writes the gradients into the
+flat buffer and records per-layer events that the communication stream waits on) and average
+their BN running statistics.  Checked against the fp64 oracle run on each shard (oracle/ref_mnb.py):
+"2 reference batches, gradients averaged" -- the semantics of gradient-only DP (the reference itself
+has one batch: models/layers/batch_normalization.py:80-93).
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+D, L, ORDER, NG, WSEED = 16, 4, 2, 40, 71
+
+
+def _paths():
+    import sys
+    for p in (REPO, os.path.join(REPO, "hgnn-2_amd"), os.path.join(REPO, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shards(world):
+    _paths()
+    import hgnn_amd.datagen as dg
+    from hgnn_amd.dp import graph_cost, shard_graphs
+    graphs = dg.qm9_shape_dataset(NG, seed=909)
+    return graphs, shard_graphs([graph_cost(X, A) for X, A, _ in graphs], world)
+
+
+def _batch(graphs):
+    from functions.batching import prepare_batch
+    from functions.operators import graph_operators
+    data = [[X, A, t, *graph_operators([X, A], 1, True)] for X, A, t in graphs]
+    return list(prepare_batch(data, 0, 1))
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HGNN_STRICT", "1")
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _paths()
+        import fixture_util as fu
+        from hgnn_amd.dp import LayerBucketAllReduce, running_stats
+        from models.gnns.model_mnb import GNN_lg
+        torch.cuda.set_device(0)
+        graphs, shards = _shards(world)
+        b = [t.cuda() for t in _batch([graphs[i] for i in shards[rank]])]
+        X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = b
+        model = GNN_lg(0, D, L, 5, 1, 1, ORDER).cuda()
+        fu.det_init(model, WSEED)
+        dp = LayerBucketAllReduce(model)
+        for step in range(2):  # twice: the flat buffer and the events are reused across steps
+            for p in model.parameters():
+                p.grad = None
+            out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+            torch.nn.MSELoss()(out, T).backward()
+            dp()
+        torch.cuda.synchronize()
+        res = {"grad." + k: p.grad.detach().cpu().numpy().copy() for k, p in model.named_parameters()}
+        res["flat_is_grad"] = all(p.grad.data_ptr() == v.data_ptr() for p, v in zip(dp.params, dp.views))
+        res["running"] = [t.detach().cpu().numpy().copy() for t in running_stats(model)]
+        q.put((rank, res))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _oracle_shard(graphs, idx):
+    _paths()
+    import fixture_util as fu
+    from models.gnns.model_mnb import GNN_lg
+    from oracle import ref_mnb as R
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _batch([graphs[i] for i in idx])
+    m = GNN_lg(0, D, L, 5, 1, 1, ORDER)
+    fu.det_init(m, WSEED)
+    dt = torch.float64
+    p = {k: v.detach().to(dt).requires_grad_(True) for k, v in m.state_dict().items()}
+    st = R.bn_states(L, 2 * D, dtype=dt)
+    runs = []
+    for _ in range(2):  # the ranks ran two steps: running stats advanced twice
+        for v in p.values():
+            v.grad = None
+        out = R.gnn_lg(p, [X.to(dt), XL.to(dt), W.to(dt), WL.to(dt), Pm.to(dt), Pd.to(dt)], Nb, mask.to(dt), Eb,
+                       mask_lg.to(dt), L, ORDER, st, True, fast=True)
+        torch.nn.MSELoss()(out, T.to(dt)).backward()
+        runs.append({k: v.grad.clone() for k, v in p.items()})
+    return runs[-1], st
+
+
+def test_world2_bucketed_allreduce_matches_shard_average():
+    import multiprocessing as mp
+    ctx = mp.get_context("forkserver")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=240) for _ in range(2))
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    graphs, shards = _shards(2)
+    # balanced shards: every graph in exactly one, loads within one graph's cost
+    assert sorted(shards[0] + shards[1]) == list(range(NG))
+    (g0, s0), (g1, s1) = _oracle_shard(graphs, shards[0]), _oracle_shard(graphs, shards[1])
+    ref = {k: (g0[k] + g1[k]) / 2 for k in g0}
+    gmax = max(v.abs().max().item() for v in ref.values())
+    for r in (0, 1):
+        res = got[r]
+        assert res["flat_is_grad"]
+        for k, v in ref.items():
+            g = torch.from_numpy(res["grad." + k]).double()
+            assert torch.all((g - v).abs() <= 1e-4 * gmax + 1e-5 * v.abs()), (r, k)
+        # BN running statistics averaged across the ranks
+        i = 0
+        for l in range(L - 1):
+            for nm in ("bn1", "bn2"):
+                for key in ("running_mean", "running_std"):
+                    want = ((s0[f"layer{l}.{nm}"][key] + s1[f"layer{l}.{nm}"][key]) / 2).numpy()
+                    np.testing.assert_allclose(res["running"][i], want, rtol=1e-4, atol=1e-5)
+                    i += 1
+    # both ranks hold identical averaged gradients
+    for k in ref:
+        assert np.array_equal(got[0]["grad." + k], got[1]["grad." + k]), k
