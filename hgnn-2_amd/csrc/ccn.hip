@@ -26,7 +26,8 @@
 namespace hgnn {
 namespace {
 
-constexpr int CCN_MAXD = 64;  // degree bound (one wave per receptive field row)
+constexpr int CCN_MAXD = 64;     // CCN-2D degree bound (one wave per receptive field row, 64-bit ballots)
+constexpr int CCN1_MAXD = 1024;  // CCN-1D degree bound (rows walked in 64-lane chunks; per-wave LDS row sums)
 
 struct CcnPlanView {
     const int* node_off;   // (bs + 1)
@@ -42,7 +43,8 @@ struct CcnPlanView {
 
 // ------------------------------------------------------------------ plan
 __global__ void __launch_bounds__(256) k_ccn_nbrs(const float* __restrict__ adj, int nmax, const int* node_off,
-                                                  int* deg, int* nbr, int* selfpos, int* graph, uint32_t* err) {
+                                                  int* deg, int* nbr, int* selfpos, int* graph, uint32_t* err,
+                                                  int maxd) {
     const int b = blockIdx.x;
     const int n0 = node_off[b];
     const int nb = node_off[b + 1] - n0;
@@ -69,7 +71,7 @@ __global__ void __launch_bounds__(256) k_ccn_nbrs(const float* __restrict__ adj,
         if (lane == 0) {
             deg[gi] = cnt;
             graph[gi] = b;
-            if (cnt > CCN_MAXD) atomicOr(err, (uint32_t)ERR_CCN_DEGREE);
+            if (cnt > maxd) atomicOr(err, (uint32_t)ERR_CCN_DEGREE);
         }
         if (hs == 0ull) {
             if (lane == 0) {
@@ -128,66 +130,77 @@ __global__ void __launch_bounds__(256) k_ccn_pos(CcnPlanView v, const int* total
     const int lane = threadIdx.x & 63;
     if (i >= *total_nodes) return;
     const int n = v.deg[i];
-    if (n > CCN_MAXD) return;
+    if (n > CCN1_MAXD) return;
     const int* ni = v.nbr + (long long)i * v.nmax;
-    const int me = lane < n ? ni[lane] : -1;
-    for (int a = 0; a < n; ++a) {
-        const int j = ni[a];
-        const int dj = v.deg[j];
-        const int* nj = v.nbr + (long long)j * v.nmax;
-        int p = -1;
-        if (lane < n) {
-            int lo = 0, hi = dj - 1;
-            while (lo <= hi) {
-                const int mid = (lo + hi) >> 1;
-                const int val = nj[mid];
-                if (val == me) {
-                    p = mid;
-                    break;
+    for (int x0 = 0; x0 < n; x0 += 64) {
+        const int x = x0 + lane;
+        const int me = x < n ? ni[x] : -1;
+        for (int a = 0; a < n; ++a) {
+            const int j = ni[a];
+            const int dj = v.deg[j];
+            const int* nj = v.nbr + (long long)j * v.nmax;
+            int p = -1;
+            if (x < n) {
+                int lo = 0, hi = dj - 1;
+                while (lo <= hi) {
+                    const int mid = (lo + hi) >> 1;
+                    const int val = nj[mid];
+                    if (val == me) {
+                        p = mid;
+                        break;
+                    }
+                    if (val < me) lo = mid + 1;
+                    else hi = mid - 1;
                 }
-                if (val < me) lo = mid + 1;
-                else hi = mid - 1;
+                pos[v.off2[i] + (long long)a * n + x] = p;
             }
-            pos[v.off2[i] + a * n + lane] = p;
         }
     }
 }
 
 // ------------------------------------------------------------------ CCN-1D
-// One wave per node; lane x = receptive-field position.  Level-0 input is X tiled
-// (utils_ccn.py:212-216): F_0[j][p] = X[j].
+// One wave per node; lane x = receptive-field position, in 64-lane chunks for degrees above 64
+// (SBM-1000 nodes reach d ~ 200).  Level-0 input is X tiled (utils_ccn.py:212-216): F_0[j][p] = X[j].
+// Row sums (over a) accumulate per position in the wave's LDS row, column sums (over x) are wave
+// sums of the chunks; for d <= 64 the summation order is the single-chunk one.
 __global__ void __launch_bounds__(256) k_ccn1_fwd(CcnPlanView v, const int* total_nodes, const float* __restrict__ fin,
                                                   int level0, const float* __restrict__ X, int cin,
                                                   const float* __restrict__ W, const float* __restrict__ bias, int h,
                                                   float* __restrict__ coll, float* __restrict__ fout) {
-    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    __shared__ float srow[4][CCN1_MAXD];
+    const int wv = threadIdx.x >> 6;
+    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
     const int lane = threadIdx.x & 63;
     if (i >= *total_nodes) return;
     const int n = v.deg[i];
-    if (n > CCN_MAXD) return;
+    if (n > CCN1_MAXD) return;
     const int* ni = v.nbr + (long long)i * v.nmax;
     const int* pi = v.pos + v.off2[i];
-    const long long row = (long long)v.off1[i] + lane;
+    const long long r0 = v.off1[i];
     const int k2 = 2 * cin;
+    float* rs = srow[wv];  // wave-private; each position owned by one lane
     for (int c = 0; c < cin; ++c) {
-        float rsum = 0.f, mycol = 0.f;
+        for (int x = lane; x < n; x += 64) rs[x] = 0.f;
         for (int a = 0; a < n; ++a) {
             const int j = ni[a];
-            float t = 0.f;
-            if (lane < n) {
-                const int p = pi[a * n + lane];
-                if (p >= 0) t = level0 ? X[(long long)j * cin + c] : fin[((long long)v.off1[j] + p) * cin + c];
+            const long long rj = v.off1[j];
+            float cs = 0.f;
+            for (int x0 = 0; x0 < n; x0 += 64) {
+                const int x = x0 + lane;
+                float t = 0.f;
+                if (x < n) {
+                    const int p = pi[(long long)a * n + x];
+                    if (p >= 0) t = level0 ? X[(long long)j * cin + c] : fin[(rj + p) * cin + c];
+                    rs[x] += t;
+                }
+                cs += wave_sum(t);
             }
-            rsum += t;
-            const float cs = wave_sum(t);
-            if (lane == a) mycol = cs;
+            if (lane == 0) coll[(r0 + a) * k2 + cin + c] = cs;
         }
-        if (lane < n) {
-            coll[row * k2 + c] = rsum;
-            coll[row * k2 + cin + c] = mycol;
-        }
+        for (int x = lane; x < n; x += 64) coll[(r0 + x) * k2 + c] = rs[x];
     }
-    if (lane < n) {
+    for (int x = lane; x < n; x += 64) {
+        const long long row = r0 + x;
         for (int o = 0; o < h; ++o) {
             float s = bias[o];
             for (int k = 0; k < k2; ++k) s = fmaf(W[o * k2 + k], coll[row * k2 + k], s);
@@ -205,29 +218,29 @@ __global__ void __launch_bounds__(256) k_ccn1_bwd_node(CcnPlanView v, const int*
     const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     if (i >= *total_nodes) return;
-    const int n = v.deg[i];
+    int n = v.deg[i];
+    if (n > CCN1_MAXD) n = 0;  // flagged by the plan; partials written as zeros
     const int k2 = 2 * cin;
-    const long long row = (long long)v.off1[i] + lane;
-    const bool act = lane < n && n <= CCN_MAXD;
+    const long long r0 = v.off1[i];
     float* pp = ppart + (long long)i * (h * k2 + h);
+    auto dpre = [&](long long row, int o) { return F[row * h + o] > 0.f ? dF[row * h + o] : 0.f; };
     for (int o = 0; o < h; ++o) {
-        float dp = 0.f;
-        if (act) dp = F[row * h + o] > 0.f ? dF[row * h + o] : 0.f;
         for (int k = 0; k < k2; ++k) {
-            const float c = act ? coll[row * k2 + k] : 0.f;
-            const float s = wave_sum(dp * c);
+            float acc = 0.f;
+            for (int x = lane; x < n; x += 64) acc += dpre(r0 + x, o) * coll[(r0 + x) * k2 + k];
+            const float s = wave_sum(acc);
             if (lane == 0) pp[o * k2 + k] = s;
         }
-        const float sb = wave_sum(dp);
+        float accb = 0.f;
+        for (int x = lane; x < n; x += 64) accb += dpre(r0 + x, o);
+        const float sb = wave_sum(accb);
         if (lane == 0) pp[h * k2 + o] = sb;
     }
-    if (act) {
+    for (int x = lane; x < n; x += 64) {
+        const long long row = r0 + x;
         for (int k = 0; k < k2; ++k) {
             float s = 0.f;
-            for (int o = 0; o < h; ++o) {
-                const float dp = F[row * h + o] > 0.f ? dF[row * h + o] : 0.f;
-                s = fmaf(W[o * k2 + k], dp, s);
-            }
+            for (int o = 0; o < h; ++o) s = fmaf(W[o * k2 + k], dpre(row, o), s);
             dcoll[row * k2 + k] = s;
         }
     }
@@ -243,30 +256,31 @@ __global__ void __launch_bounds__(256) k_ccn1_bwd_gather(CcnPlanView v, const in
     const int lane = threadIdx.x & 63;
     if (j >= *total_nodes) return;
     const int n = v.deg[j];
-    if (n > CCN_MAXD) return;
+    if (n > CCN1_MAXD) return;
     const int* nj = v.nbr + (long long)j * v.nmax;
     const int* pj = v.pos + v.off2[j];
     const int sj = v.selfpos[j];
     const int g = v.graph[j];
     const int k2 = 2 * cin;
     for (int c = 0; c < cin; ++c) {
-        float acc = 0.f;
-        if (lane < n) {
+        const float rd = dsum ? dsum[(long long)g * dsum_ld + dsum_off + c] : 0.f;
+        float tot = 0.f;
+        for (int u = lane; u < n; u += 64) {
+            float acc = 0.f;
             for (int a = 0; a < n; ++a) {
                 const int i = nj[a];
-                const int q = pj[a * n + lane];
+                const int q = pj[(long long)a * n + u];
                 if (q < 0) continue;
-                const int aj = pj[a * n + sj];
+                const int aj = pj[(long long)a * n + sj];
                 const long long ri = v.off1[i];
                 acc += dcoll[(ri + q) * k2 + c] + dcoll[(ri + aj) * k2 + cin + c];
             }
+            if (level0) tot += acc;
+            else dout[((long long)v.off1[j] + u) * cin + c] = acc + rd;
         }
-        const float rd = dsum ? dsum[(long long)g * dsum_ld + dsum_off + c] : 0.f;
         if (level0) {
-            const float s = wave_sum(acc);
+            const float s = wave_sum(tot);
             if (lane == 0) dout[(long long)j * cin + c] = s + (float)n * rd;
-        } else if (lane < n) {
-            dout[((long long)v.off1[j] + lane) * cin + c] = acc + rd;
         }
     }
 }
@@ -293,21 +307,24 @@ struct C2Save {
 //   pass B, wave per b, lane z:  Sa[b][z] = sum_{a: b in C_a} T, q3[b] = sum_z Sa (wave sum)
 // The validity of the loop index (z in pass A, a in pass B) is wave-uniform, so each wave walks
 // the set bits of a ballot.  Level 0 (F_0[j] = X[j] tiled, utils_ccn.py:167-172) needs no gather.
-constexpr int C2_CMAX = 8;  // channels of a CCN-2D level (f_in or hidden) handled per pass
-constexpr int C2_HMAX = 8;  // hidden size bound of the fused output stage
+constexpr int C2_CMAX = 8;  // channels of a CCN-2D level (f_in or hidden) handled per pass (narrow kernels)
+constexpr int C2_HMAX = 8;  // hidden size bound of the fused output stage (narrow kernels)
+constexpr int C2_CMAX_WIDE = 16;  // the wide instantiations: f_in, hidden <= 16
+constexpr int C2_HMAX_WIDE = 16;
 
+template <int CM, int HM>
 __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* total_nodes, const float* __restrict__ fin,
                                                   int level0, const float* __restrict__ X, int cin,
                                                   const float* __restrict__ W, const float* __restrict__ bias, int h,
                                                   C2Save sv, float* __restrict__ fout) {
     __shared__ int sp[CCN_MAXD * CCN_MAXD];
     __shared__ unsigned long long vmask[CCN_MAXD];  // bit x of vmask[a]: x in C_a
-    __shared__ float sred[2][4][C2_CMAX];           // per-wave partial q1-total and d3
+    __shared__ float sred[2][4][CM];           // per-wave partial q1-total and d3
     __shared__ int s_j[CCN_MAXD], s_dj[CCN_MAXD], s_oj[CCN_MAXD];  // neighbour a: node, degree, 2D row offset
     const int i = blockIdx.x;
     if (i >= *total_nodes) return;
     const int n = v.deg[i];
-    if (n > CCN_MAXD || cin > C2_CMAX || h > C2_HMAX) return;
+    if (n > CCN_MAXD || cin > CM || h > HM) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int* ni = v.nbr + (long long)i * v.nmax;
     const long long o2 = v.off2[i], o1 = v.off1[i];
@@ -326,22 +343,22 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
     __syncthreads();
 
     // ---- pass A: wave per neighbour a, lane b
-    float tq[C2_CMAX], td3[C2_CMAX];
+    float tq[CM], td3[CM];
 #pragma unroll
-    for (int c = 0; c < C2_CMAX; ++c) tq[c] = td3[c] = 0.f;
+    for (int c = 0; c < CM; ++c) tq[c] = td3[c] = 0.f;
     for (int a = wv; a < n; a += 4) {
         const int j = ni[a];
         const unsigned long long ma = vmask[a];
         const int pb = lane < n ? sp[a * n + lane] : -1;
         const bool vb = pb >= 0;
-        float sc[C2_CMAX], d1[C2_CMAX], d2[C2_CMAX];
+        float sc[CM], d1[CM], d2[CM];
 #pragma unroll
-        for (int c = 0; c < C2_CMAX; ++c) sc[c] = d1[c] = d2[c] = 0.f;
+        for (int c = 0; c < CM; ++c) sc[c] = d1[c] = d2[c] = 0.f;
         if (level0) {
             const float mf = (float)__popcll(ma);
             const bool va = (ma >> a) & 1ull;
 #pragma unroll
-            for (int c = 0; c < C2_CMAX; ++c) {
+            for (int c = 0; c < CM; ++c) {
                 if (c >= cin) break;
                 const float xj = X[(long long)j * cin + c];
                 sc[c] = vb ? mf * xj : 0.f;
@@ -362,12 +379,12 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
                     zz[u] = zs ? __ffsll((long long)zs) - 1 : -1;
                     zs &= zs ? zs - 1ull : 0ull;
                 }
-                float t[4][C2_CMAX];
+                float t[4][CM];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int pz = zz[u] >= 0 ? sp[a * n + zz[u]] : 0;  // valid row: loads need no mask
 #pragma unroll
-                    for (int c = 0; c < C2_CMAX; ++c) t[u][c] = c < cin ? row[(long long)pz * cin + c] : 0.f;
+                    for (int c = 0; c < CM; ++c) t[u][c] = c < cin ? row[(long long)pz * cin + c] : 0.f;
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
@@ -375,7 +392,7 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
                     if (z < 0) break;
                     if (vb) {
 #pragma unroll
-                        for (int c = 0; c < C2_CMAX; ++c) {
+                        for (int c = 0; c < CM; ++c) {
                             if (c >= cin) break;
                             sc[c] += t[u][c];
                             if (z == lane) d1[c] = t[u][c];
@@ -388,7 +405,7 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
         if (lane < n) {
             const long long r = (o2 + (long long)a * n + lane) * cin;
 #pragma unroll
-            for (int c = 0; c < C2_CMAX; ++c) {
+            for (int c = 0; c < CM; ++c) {
                 if (c >= cin) break;
                 sv.Sc[r + c] = sc[c];
                 sv.D1[r + c] = d1[c];
@@ -396,7 +413,7 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
             }
         }
 #pragma unroll
-        for (int c = 0; c < C2_CMAX; ++c) {
+        for (int c = 0; c < CM; ++c) {
             if (c >= cin) break;
             const float q = wave_sum(sc[c]);           // q1[a] = sum_b Sc[a][b]
             if (lane == 0) sv.q1[(o1 + a) * cin + c] = q;
@@ -405,7 +422,7 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
         }
     }
 #pragma unroll
-    for (int c = 0; c < C2_CMAX; ++c) {
+    for (int c = 0; c < CM; ++c) {
         if (c >= cin) break;
         const float t3 = wave_sum(td3[c]);
         if (lane == 0) {
@@ -416,9 +433,9 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
 
     // ---- pass B: wave per receptive-field row b, lane z
     for (int b = wv; b < n; b += 4) {
-        float sa[C2_CMAX];
+        float sa[CM];
 #pragma unroll
-        for (int c = 0; c < C2_CMAX; ++c) sa[c] = 0.f;
+        for (int c = 0; c < CM; ++c) sa[c] = 0.f;
         // the neighbours a with b in C_a, ascending, in batches of 4 (loads first, then the sums)
         unsigned long long as = __ballot(lane < n && ((vmask[lane < n ? lane : 0] >> b) & 1ull));
         while (as) {
@@ -428,7 +445,7 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
                 aa[u] = as ? __ffsll((long long)as) - 1 : -1;
                 as &= as ? as - 1ull : 0ull;
             }
-            float t[4][C2_CMAX];
+            float t[4][CM];
             bool vz[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -443,14 +460,14 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
                     q = fin + ((long long)s_oj[a] + (long long)pb * s_dj[a] + pz) * cin;
                 }
 #pragma unroll
-                for (int c = 0; c < C2_CMAX; ++c) t[u][c] = c < cin ? q[c] : 0.f;
+                for (int c = 0; c < CM; ++c) t[u][c] = c < cin ? q[c] : 0.f;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 if (aa[u] < 0) break;
                 if (vz[u]) {
 #pragma unroll
-                    for (int c = 0; c < C2_CMAX; ++c) {
+                    for (int c = 0; c < CM; ++c) {
                         if (c >= cin) break;
                         sa[c] += t[u][c];
                     }
@@ -458,7 +475,7 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
             }
         }
 #pragma unroll
-        for (int c = 0; c < C2_CMAX; ++c) {
+        for (int c = 0; c < CM; ++c) {
             if (c >= cin) break;
             if (lane < n) sv.Sa[(o2 + (long long)b * n + lane) * cin + c] = sa[c];
             const float q3 = wave_sum(sa[c]);
@@ -481,14 +498,14 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
     // the statistics of an entry are read once per channel and feed every output o (weights in LDS)
     const float nf = (float)n;
     const int K = 18 * cin;
-    __shared__ float sw[C2_HMAX * 18 * C2_CMAX];
+    __shared__ float sw[HM * 18 * CM];
     for (int t = threadIdx.x; t < h * K; t += 256) sw[t] = W[t];
     __syncthreads();
     for (int e = threadIdx.x; e < n * n; e += 256) {
         const int x = e / n, y = e % n;
-        float s[C2_HMAX];
+        float s[HM];
 #pragma unroll
-        for (int o = 0; o < C2_HMAX; ++o) s[o] = o < h ? bias[o] : 0.f;
+        for (int o = 0; o < HM; ++o) s[o] = o < h ? bias[o] : 0.f;
         for (int c = 0; c < cin; ++c) {
             const float sc = sv.Sc[(o2 + x * n + y) * cin + c];
             const float sa = sv.Sa[(o2 + x * n + y) * cin + c];
@@ -505,7 +522,7 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
             blk[16] = sv.D2[(o2 + y * n + x) * cin + c];
             blk[17] = x == y ? sv.d3[(long long)i * cin + c] : 0.f;
 #pragma unroll
-            for (int o = 0; o < C2_HMAX; ++o) {
+            for (int o = 0; o < HM; ++o) {
                 if (o >= h) break;
                 const float* w = sw + o * K;
 #pragma unroll
@@ -513,7 +530,7 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
             }
         }
 #pragma unroll
-        for (int o = 0; o < C2_HMAX; ++o) {
+        for (int o = 0; o < HM; ++o) {
             if (o >= h) break;
             fout[(o2 + e) * h + o] = s[o] < 0.f ? 0.f : s[o];
         }
@@ -532,42 +549,43 @@ struct C2Grad {
 // One sweep over the n^2 entries per output o for the parameter partials (the 9 distinct
 // contraction blocks x cin accumulate in registers, then one wave-sum + LDS combine each), and one
 // sweep for the input-side gradients (every channel of an entry from one read of dpre).
+template <int CM, int HM>
 __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int* total_nodes,
                                                        const float* __restrict__ dF, const float* __restrict__ F,
                                                        C2Save sv, int cin, const float* __restrict__ W, int h,
                                                        C2Grad gd, float* __restrict__ ppart,
                                                        float* __restrict__ g0) {
-    __shared__ float sdq1[CCN_MAXD * C2_CMAX], sdq3[CCN_MAXD * C2_CMAX], sdtot[C2_CMAX], sdd3[C2_CMAX];
-    __shared__ float red[4][10 * C2_CMAX];
-    __shared__ float sw[C2_HMAX * 18 * C2_CMAX];
+    __shared__ float sdq1[CCN_MAXD * CM], sdq3[CCN_MAXD * CM], sdtot[CM], sdd3[CM];
+    __shared__ float red[4][10 * CM];
+    __shared__ float sw[HM * 18 * CM];
     const int i = blockIdx.x;
     if (i >= *total_nodes) return;
     const int n = v.deg[i];
-    if (n > CCN_MAXD || cin > C2_CMAX || h > C2_HMAX) return;
+    if (n > CCN_MAXD || cin > CM || h > HM) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long o2 = v.off2[i], o1 = v.off1[i];
     const float nf = (float)n;
     const int K = 18 * cin;
     float* pp = ppart + (long long)i * (h * K + h);
     for (int t = threadIdx.x; t < h * K; t += 256) sw[t] = W[t];
-    for (int t = threadIdx.x; t < n * C2_CMAX; t += 256) sdq1[t] = sdq3[t] = 0.f;
+    for (int t = threadIdx.x; t < n * CM; t += 256) sdq1[t] = sdq3[t] = 0.f;
     if (threadIdx.x < cin) sdtot[threadIdx.x] = sdd3[threadIdx.x] = 0.f;
     // parameter partials: dW[o][q*C + c] = sum_xy dpre[x][y][o] * block_q[x][y][c]
     // distinct blocks: 0 (n Sc; also 6..14), 1 q1, 2 n Sa, 3 q3, 4 tot (diag), 5 Sc, 15 D1, 16 D2^T, 17 d3 (diag)
     for (int o = 0; o < h; ++o) {
-        float acc[9][C2_CMAX];
+        float acc[9][CM];
         float sb = 0.f;
 #pragma unroll
         for (int q = 0; q < 9; ++q)
 #pragma unroll
-            for (int c = 0; c < C2_CMAX; ++c) acc[q][c] = 0.f;
+            for (int c = 0; c < CM; ++c) acc[q][c] = 0.f;
         for (int e = threadIdx.x; e < n * n; e += 256) {
             const int x = e / n, y = e % n;
             const long long r = o2 + e;
             const float dp = F[r * h + o] > 0.f ? dF[r * h + o] : 0.f;
             sb += dp;
 #pragma unroll
-            for (int c = 0; c < C2_CMAX; ++c) {
+            for (int c = 0; c < CM; ++c) {
                 if (c >= cin) break;
                 const float sc = sv.Sc[r * cin + c];
                 acc[0][c] = fmaf(dp, nf * sc, acc[0][c]);
@@ -586,37 +604,37 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
 #pragma unroll
         for (int q = 0; q < 9; ++q)
 #pragma unroll
-            for (int c = 0; c < C2_CMAX; ++c) {
+            for (int c = 0; c < CM; ++c) {
                 if (c >= cin) break;
                 const float t = wave_sum(acc[q][c]);
-                if (lane == 0) red[wv][q * C2_CMAX + c] = t;
+                if (lane == 0) red[wv][q * CM + c] = t;
             }
         sb = wave_sum(sb);
-        if (lane == 0) red[wv][9 * C2_CMAX] = sb;
+        if (lane == 0) red[wv][9 * CM] = sb;
         __syncthreads();
         for (int t = threadIdx.x; t < 18 * cin; t += 256) {
             const int q = t / cin, c = t % cin;
             const int d = q < 6 ? q : (q < 15 ? 0 : q - 9);  // distinct-block index of q
-            pp[o * K + q * cin + c] = red[0][d * C2_CMAX + c] + red[1][d * C2_CMAX + c] + red[2][d * C2_CMAX + c] +
-                                      red[3][d * C2_CMAX + c];
+            pp[o * K + q * cin + c] = red[0][d * CM + c] + red[1][d * CM + c] + red[2][d * CM + c] +
+                                      red[3][d * CM + c];
         }
-        if (threadIdx.x == 0) pp[h * K + o] = red[0][9 * C2_CMAX] + red[1][9 * C2_CMAX] + red[2][9 * C2_CMAX] +
-                                              red[3][9 * C2_CMAX];
+        if (threadIdx.x == 0) pp[h * K + o] = red[0][9 * CM] + red[1][9 * CM] + red[2][9 * CM] +
+                                              red[3][9 * CM];
         __syncthreads();
     }
     // input-side gradients of the contraction blocks: g_q = W_q^T dpre
     for (int e = threadIdx.x; e < n * n; e += 256) {
         const int x = e / n, y = e % n;
         const long long r = o2 + e;
-        float dp[C2_HMAX];
+        float dp[HM];
 #pragma unroll
-        for (int o = 0; o < C2_HMAX; ++o) dp[o] = (o < h && F[r * h + o] > 0.f) ? dF[r * h + o] : 0.f;
+        for (int o = 0; o < HM; ++o) dp[o] = (o < h && F[r * h + o] > 0.f) ? dF[r * h + o] : 0.f;
         for (int c = 0; c < cin; ++c) {
             float g[18];
 #pragma unroll
             for (int q = 0; q < 18; ++q) g[q] = 0.f;
 #pragma unroll
-            for (int o = 0; o < C2_HMAX; ++o) {
+            for (int o = 0; o < HM; ++o) {
                 if (o >= h) break;
                 const float* w = sw + o * K;
 #pragma unroll
@@ -629,8 +647,8 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
             gd.dSa[r * cin + c] = nf * g[2];
             gd.dD1[r * cin + c] = g[15];
             gd.dD2[(o2 + y * n + x) * cin + c] = g[16];
-            atomicAdd(&sdq1[x * C2_CMAX + c], g[1]);
-            atomicAdd(&sdq3[x * C2_CMAX + c], g[3]);
+            atomicAdd(&sdq1[x * CM + c], g[1]);
+            atomicAdd(&sdq3[x * CM + c], g[3]);
             if (x == y) {
                 atomicAdd(&sdtot[c], g[4]);
                 atomicAdd(&sdd3[c], g[17]);
@@ -642,8 +660,8 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
         const int a = e / n;
         const long long r = o2 + e;
         for (int c = 0; c < cin; ++c) {
-            gd.dSc[r * cin + c] += sdq1[a * C2_CMAX + c];                 // q1[a] = sum_b Sc[a][b]
-            gd.dSa[r * cin + c] += sdq3[a * C2_CMAX + c] + sdtot[c];      // q3[b] = sum_z Sa[b][z]; tot: every entry
+            gd.dSc[r * cin + c] += sdq1[a * CM + c];                 // q1[a] = sum_b Sc[a][b]
+            gd.dSa[r * cin + c] += sdq3[a * CM + c] + sdtot[c];      // q3[b] = sum_z Sa[b][z]; tot: every entry
         }
     }
     if (threadIdx.x < cin) gd.dd3[(long long)i * cin + threadIdx.x] = sdd3[threadIdx.x];
@@ -724,7 +742,7 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_gather(CcnPlanView v, const in
     // C: channel bound of this instantiation (cin <= C); NB: neighbours gathered per batch
     __shared__ int sp[CCN_MAXD * CCN_MAXD];
     __shared__ unsigned long long vmask[CCN_MAXD];
-    __shared__ float red[4][C2_CMAX];
+    __shared__ float red[4][C];
     __shared__ int s_i[CCN_MAXD], s_di[CCN_MAXD], s_oi[CCN_MAXD], s_aj[CCN_MAXD];  // neighbour a of j
     const int j = blockIdx.x;
     if (j >= *total_nodes) return;
@@ -1071,7 +1089,7 @@ size_t al(size_t x) { return (x + 255) / 256 * 256; }
 bool ccn_ok(const hgnn_ccn_config* c) {
     return c && (c->order == 1 || c->order == 2) && c->bs > 0 && c->nmax > 0 && c->f_in > 0 && c->hidden > 0 &&
            c->layers >= 1 && c->layers <= 15 && c->n_out > 0 &&
-           (c->order == 1 || (c->f_in <= C2_CMAX && c->hidden <= C2_CMAX && c->hidden <= C2_HMAX));
+           (c->order == 1 || (c->f_in <= C2_CMAX_WIDE && c->hidden <= C2_CMAX_WIDE && c->hidden <= C2_HMAX_WIDE));
 }
 
 CcnLayout ccn_layout(const hgnn_ccn_config* c, long long sum_d, long long sum_d2) {
@@ -1226,7 +1244,7 @@ int hgnn_ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t*
     CcnPlanView v = plan_view(cfg, L, plan_ws);
     hipLaunchKernelGGL(k_ccn_nbrs, dim3(cfg->bs), dim3(256), 0, s, d_adj, cfg->nmax, v.node_off,
                        P<int>(plan_ws, L.deg), P<int>(plan_ws, L.nbr), P<int>(plan_ws, L.selfpos),
-                       P<int>(plan_ws, L.graph), m.err);
+                       P<int>(plan_ws, L.graph), m.err, cfg->order == 1 ? CCN1_MAXD : CCN_MAXD);
     HGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_ccn_scan, dim3(1), dim3(256), 0, s, P<int>(plan_ws, L.deg), m.totals,
                        P<int>(plan_ws, L.off1), P<int>(plan_ws, L.off2), m.totals + 2);
@@ -1282,8 +1300,13 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
             hipLaunchKernelGGL(k_ccn1_fwd, dim3(nodes > 0 ? (nodes + 3) / 4 : 1), dim3(256), 0, s, v, tot, fin,
                                l == 0 ? 1 : 0, d_X, cin, w, b, h, P<float>(W, L.coll[l]), P<float>(W, L.F[l]));
         } else {
-            hipLaunchKernelGGL(k_ccn2_fwd, dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s, v, tot, fin, l == 0 ? 1 : 0,
-                               d_X, cin, w, b, h, save_of(L, W, l), P<float>(W, L.F[l]));
+            if (cin <= C2_CMAX && h <= C2_HMAX)
+                hipLaunchKernelGGL((k_ccn2_fwd<C2_CMAX, C2_HMAX>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s, v, tot,
+                                   fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, save_of(L, W, l), P<float>(W, L.F[l]));
+            else
+                hipLaunchKernelGGL((k_ccn2_fwd<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0,
+                                   s, v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, save_of(L, W, l),
+                                   P<float>(W, L.F[l]));
         }
         HGNN_LAUNCH_CHECK();
     }
@@ -1344,8 +1367,14 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
         } else {
             C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
                       P<float>(W, L.g_d3)};
-            hipLaunchKernelGGL(k_ccn2_bwd_node, dim3(nb1), dim3(256), 0, s, v, tot, dF, P<float>(W, L.F[l]),
-                               save_of(L, W, l), cin, w, h, gd, ppart, l == 0 ? P<float>(W, L.g0) : nullptr);
+            if (cin <= C2_CMAX && h <= C2_HMAX)
+                hipLaunchKernelGGL((k_ccn2_bwd_node<C2_CMAX, C2_HMAX>), dim3(nb1), dim3(256), 0, s, v, tot, dF,
+                                   P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart,
+                                   l == 0 ? P<float>(W, L.g0) : nullptr);
+            else
+                hipLaunchKernelGGL((k_ccn2_bwd_node<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nb1), dim3(256), 0, s, v, tot,
+                                   dF, P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart,
+                                   l == 0 ? P<float>(W, L.g0) : nullptr);
         }
         HGNN_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_ccn_param_reduce, dim3(h * K + h), dim3(256), 0, s, ppart, tot, h * K, h, grads[2 * l],
@@ -1367,9 +1396,12 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                 if (cin <= 2)
                     hipLaunchKernelGGL((k_ccn2_bwd_gather<2, 4>), dim3(nb1), dim3(256), 0, s, v, tot, gd, cin, dsum,
                                        nf, doff, lvl0, dst);
-                else
+                else if (cin <= C2_CMAX)
                     hipLaunchKernelGGL((k_ccn2_bwd_gather<C2_CMAX, 1>), dim3(nb1), dim3(256), 0, s, v, tot, gd, cin,
                                        dsum, nf, doff, lvl0, dst);
+                else
+                    hipLaunchKernelGGL((k_ccn2_bwd_gather<C2_CMAX_WIDE, 1>), dim3(nb1), dim3(256), 0, s, v, tot, gd,
+                                       cin, dsum, nf, doff, lvl0, dst);
         }
         HGNN_LAUNCH_CHECK();
         float* t = dF;

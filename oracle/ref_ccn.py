@@ -14,6 +14,8 @@ Reference line map (all under /root/reference):
   python_contract/tensorprod functions/utils_ccn.py:37-45, 57-63
   collapse6to3               functions/contraction.py:21-121
   CCN_1D / CCN_2D forward    models/compnets/model_ccn.py:41-64, 93-105
+Closed / vectorised forms for the sizes the literal loops cannot reach: ccn2_forward_closed
+(CCN-2D, SBM-200) and ccn1_forward_vec (CCN-1D, SBM-400..1000), each pinned to ccn_forward.
 """
 
 import torch
@@ -147,4 +149,32 @@ def ccn2_forward_closed(p, X, adj, layers):
         F = new
         levels.append(F)
     summed = [sum(v.sum(0).sum(0) for v in f) for f in levels]
+    return _linear(p, "fc", torch.cat(summed, 0))
+
+
+def ccn1_forward_vec(p, X, adj, layers):
+    """CCN_1D forward for one graph, vectorised per node: the same function as
+    ccn_forward(..., order=1) (utils_ccn.py:185-222, 242-252, 303-324) with the chi position maps
+    from one dense index table instead of per-pair Python dicts, so it runs on SBM graphs of
+    N = 400-1000 (degrees ~70-200).  Pinned against ccn_forward by tests/test_oracle.py."""
+    n_nodes = X.shape[0]
+    nbrs = [torch.nonzero(adj[i] > 0).view(-1) for i in range(n_nodes)]
+    deg = [len(v) for v in nbrs]
+    idx = torch.full((n_nodes, n_nodes), -1, dtype=torch.long)  # idx[j, v] = position of v in nbr_j
+    for j in range(n_nodes):
+        idx[j, nbrs[j]] = torch.arange(deg[j])
+    F = [X[i].view(1, -1).expand(deg[i], -1) for i in range(n_nodes)]
+    levels = [F]
+    for l in range(layers):
+        new = []
+        Fp = torch.nn.utils.rnn.pad_sequence(F, batch_first=True)  # (nodes, dmax, C), autograd through it
+        for i in range(n_nodes):
+            J = nbrs[i]
+            P = idx[J][:, J]                                   # P[a][x] = position of nbr_i[x] in nbr_{j_a}
+            T = Fp[J.view(-1, 1), P.clamp(min=0)] * (P >= 0).to(X.dtype).unsqueeze(2)   # (d, d, C): T[a][x]
+            coll = torch.cat([T.sum(0), T.sum(1)], 1)
+            new.append(Fn.relu(_linear(p, "w{}".format(l + 1), coll)))
+        F = new
+        levels.append(F)
+    summed = [sum(v.sum(0) for v in f) for f in levels]
     return _linear(p, "fc", torch.cat(summed, 0))

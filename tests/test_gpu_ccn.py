@@ -188,3 +188,60 @@ def test_ccn2_sbm200_config5_matches_closed_form_oracle():
         _grad_close(Xr.grad[b, :x.shape[0]], xr.grad, f"sbm200 dX graph {b}")
     for n, p in net.named_parameters():
         _grad_close(p.grad, p64[n].grad, f"sbm200 grad {n}")
+
+
+def test_ccn1_sbm_large_degree_vs_oracle():
+    """CCN-1D beyond one wave of receptive field: SBM N = 400 (degrees ~70-90) and N = 1000 (~175-210,
+    the north star's largest SBM) in one padded batch vs the fp64 vectorised oracle
+    (oracle/ref_ccn.py ccn1_forward_vec, pinned to the literal restatement): outputs, dX, grads."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_1D
+    from oracle import ref_ccn as RC
+    graphs = dg.sbm_dataset(2, n=400, seed=41) + dg.sbm_dataset(1, n=1000, seed=42)
+    graphs = [(X, A + torch.eye(A.shape[0]), t) for X, A, t in graphs]
+    assert max(int((a > 0).sum(1).max()) for _, a, _ in graphs) > 128
+    net = CCN_1D(5, 1, 2, 2)
+    fu.det_init(net, 43)
+    p64 = {n: v.detach().double().clone().requires_grad_(True) for n, v in net.named_parameters()}
+    net = net.cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    Xr = X.clone().requires_grad_(True)
+    out = net.forward_batch(Xr, A, nb)
+    w = torch.tensor([[1.0], [-0.5], [0.25]])
+    (out * w.cuda()).sum().backward()
+    for b, (x, a, _) in enumerate(graphs):
+        xr = x.double().requires_grad_(True)
+        ref = RC.ccn1_forward_vec(p64, xr, a.double(), 2)
+        _close(out[b], ref, f"sbm graph {b}")
+        (ref * w[b].double()).sum().backward()
+        _grad_close(Xr.grad[b, :x.shape[0]], xr.grad, f"sbm dX graph {b}")
+    for n, p in net.named_parameters():
+        _grad_close(p.grad, p64[n].grad, f"sbm grad {n}")
+
+
+@pytest.mark.parametrize("hidden", [16, 12])
+def test_ccn2_wide_channels_vs_closed_form_oracle(hidden):
+    """CCN-2D with hidden > 8 (the wide kernel instantiations, channels <= 16) vs the fp64 closed-form
+    oracle on QM9-shape graphs and one SBM-30 graph: outputs, dX and parameter gradients."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_2D
+    from oracle import ref_ccn as RC
+    graphs = dg.qm9_shape_dataset(6, seed=91) + dg.sbm_dataset(1, n=30, seed=92)
+    graphs = [(X, A + torch.eye(A.shape[0]), t) for X, A, t in graphs]
+    net = CCN_2D(5, 1, hidden, 2)
+    fu.det_init(net, 93)
+    p64 = {n: v.detach().double().clone().requires_grad_(True) for n, v in net.named_parameters()}
+    net = net.cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    Xr = X.clone().requires_grad_(True)
+    out = net.forward_batch(Xr, A, nb)
+    w = torch.randn(out.shape, generator=torch.Generator().manual_seed(94))
+    (out * w.cuda()).sum().backward()
+    for b, (x, a, _) in enumerate(graphs):
+        xr = x.double().requires_grad_(True)
+        ref = RC.ccn2_forward_closed(p64, xr, a.double(), 2)
+        _close(out[b], ref, f"hidden {hidden} graph {b}")
+        (ref * w[b].double()).sum().backward()
+        _grad_close(Xr.grad[b, :x.shape[0]], xr.grad, f"hidden {hidden} dX graph {b}")
+    for n, p in net.named_parameters():
+        _grad_close(p.grad, p64[n].grad, f"hidden {hidden} grad {n}")

@@ -222,3 +222,26 @@ def test_oracle_ccn2_closed_form_matches_literal(golden):
         assert torch.allclose(xa.grad, xb.grad, rtol=1e-10, atol=1e-10)
         for n in p:
             assert torch.allclose(pa[n].grad, pb[n].grad, rtol=1e-10, atol=1e-10), n
+
+
+def test_oracle_ccn1_vectorised_matches_literal(golden):
+    """The vectorised CCN-1D oracle (used at SBM-400..1000 size, degrees above 64) equals the literal
+    restatement -- outputs and every gradient -- on the reference fixture graphs and SBM graphs."""
+    from oracle import ref_ccn as RC
+    import hgnn_amd.datagen as dg
+    z = golden("ccn")
+    graphs = ccn_graphs(z)[:6] + [(X, A + torch.eye(A.shape[0]), t) for X, A, t in dg.sbm_dataset(2, n=16, seed=19)]
+    for k, (X, A, _) in enumerate(graphs):
+        _, p = ccn_params("1d", k, torch.float64)
+        pa = {n: v.clone().requires_grad_(True) for n, v in p.items()}
+        pb = {n: v.clone().requires_grad_(True) for n, v in p.items()}
+        xa = X.double().requires_grad_(True)
+        xb = X.double().requires_grad_(True)
+        a = RC.ccn_forward(pa, xa, A.double(), 1, 2)
+        b = RC.ccn1_forward_vec(pb, xb, A.double(), 2)
+        assert torch.allclose(a, b, rtol=1e-12, atol=1e-10), (k, a, b)
+        a.sum().backward()
+        b.sum().backward()
+        assert torch.allclose(xa.grad, xb.grad, rtol=1e-10, atol=1e-10)
+        for n in p:
+            assert torch.allclose(pa[n].grad, pb[n].grad, rtol=1e-10, atol=1e-10), n
