@@ -68,14 +68,32 @@ def _plan(cfg, adj, n_batch, stream):
     return plan, max_d2, sums
 
 
+class CcnPlan:
+    """The batch's index construction (receptive fields, chi position maps, ragged totals), built
+    once: a training loop that replays a captured HIP graph for the step (no host sync inside it)
+    plans each batch beforehand and passes the plan to forward_batch."""
+
+    def __init__(self, spec, adj, n_batch):
+        _require_cuda([adj, n_batch], "CCN plan")
+        bs, nmax = adj.shape[0], adj.shape[1]
+        self.cfg = spec.config(bs, nmax)
+        self.key = (spec.order, bs, nmax)
+        self.plan, self.max_d2, self.sums = _plan(self.cfg, _f32(adj), _i64(n_batch), L.stream_handle(adj.device))
+
+
 class _CcnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, spec, X, adj, n_batch, *params):
+    def forward(ctx, spec, pl, X, adj, n_batch, *params):
         lib = L.lib()
         bs, nmax, _ = X.shape
         cfg = spec.config(bs, nmax)
         s = L.stream_handle(X.device)
-        plan, max_d2, sums = _plan(cfg, adj, n_batch, s)
+        if pl is not None:
+            if pl.key != (spec.order, bs, nmax):
+                raise RuntimeError("hgnn_amd: CCN plan was built for another batch shape / order")
+            plan, max_d2, sums = pl.plan, pl.max_d2, pl.sums
+        else:
+            plan, max_d2, sums = _plan(cfg, adj, n_batch, s)
         ws = torch.empty(max(lib.hgnn_ccn_workspace_bytes(ctypes.byref(cfg), sums), 1), dtype=torch.uint8,
                          device=X.device)
         out = torch.empty(bs, spec.n_out, dtype=torch.float32, device=X.device)
@@ -97,11 +115,12 @@ class _CcnFn(torch.autograd.Function):
         L.check(lib.hgnn_ccn_backward(ctypes.byref(ctx.cfg), ctx.sums, L.ptr_array(ctx.params), L.ptr(ctx.plan),
                                       ctx.max_d2, L.ptr(ctx.ws), L.ptr(dout), L.ptr_array(grads), L.ptr(dX),
                                       L.stream_handle(dev)), "hgnn_ccn_backward")
-        return (None, dX, None, None, *grads)
+        return (None, None, dX, None, None, *grads)
 
 
-def run_ccn(spec, params, X, adj, n_batch):
-    """Batched CCN forward: X (bs,nmax,f), adj (bs,nmax,nmax), n_batch (bs,) -> (bs, n_out)."""
+def run_ccn(spec, params, X, adj, n_batch, plan=None):
+    """Batched CCN forward: X (bs,nmax,f), adj (bs,nmax,nmax), n_batch (bs,) -> (bs, n_out).
+    plan: a CcnPlan of this adj / n_batch (else the plan is built here, with one host sync)."""
     _require_cuda([X, adj, n_batch, *params], "CCN")
     if X.dim() != 3 or adj.dim() != 3:
         raise RuntimeError(f"hgnn_amd: CCN expects X (bs,nmax,f) and adj (bs,nmax,nmax), got {tuple(X.shape)}, "
@@ -113,7 +132,7 @@ def run_ccn(spec, params, X, adj, n_batch):
     for p, shp in zip(params, spec.param_shapes()):
         if tuple(p.shape) != shp:
             raise RuntimeError(f"hgnn_amd: CCN parameter shape {tuple(p.shape)} != {shp}")
-    return _CcnFn.apply(spec, _f32(X), _f32(adj), _i64(n_batch), *[_f32(p) for p in params])
+    return _CcnFn.apply(spec, plan, _f32(X), _f32(adj), _i64(n_batch), *[_f32(p) for p in params])
 
 
 def plan_maps(order, X, adj, n_batch):

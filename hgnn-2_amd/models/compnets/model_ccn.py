@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 
 from functions.utils_ccn import CompnetUtils
-from hgnn_amd.ccn import CcnSpec, run_ccn
+from hgnn_amd.ccn import CcnPlan, CcnSpec, run_ccn
 
 
 class _CCN(nn.Module):
@@ -34,8 +34,13 @@ class _CCN(nn.Module):
     def _spec(self):
         return CcnSpec(self.order, self.input_feats, self.w1.out_features, self.layers, self.n_outputs)
 
-    def forward_batch(self, X, adj, n_batch):
-        return run_ccn(self._spec(), self._params(), X, adj, n_batch)
+    def plan(self, adj, n_batch):
+        """Index construction of a padded batch, reusable across forward_batch calls on it
+        (hgnn_amd.ccn.CcnPlan; lets the step be captured in a HIP graph)."""
+        return CcnPlan(self._spec(), adj, n_batch)
+
+    def forward_batch(self, X, adj, n_batch, plan=None):
+        return run_ccn(self._spec(), self._params(), X, adj, n_batch, plan)
 
     def forward(self, X, adj):
         if X.dim() != 2 or adj.dim() != 2:

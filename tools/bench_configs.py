@@ -59,6 +59,23 @@ def ccn_batch(graphs):
     return X.cuda(), A.cuda(), T.cuda(), nb.cuda()
 
 
+def graphed(step, warmup=3):
+    """Capture one call of step() (forward + loss + backward: every executor launch, the side
+    stream's fork/join included) in a HIP graph; returns its replay."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(warmup):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    torch.cuda.synchronize()
+    return g.replay
+
+
 def timeit(step, steps, warmup):
     for _ in range(warmup):
         step()
@@ -146,7 +163,7 @@ def run_train(steps, warmup, bs=512, csr=False):
                 dtype="fp32", loss=float(step.stats[0].item()))
 
 
-def run_simple(steps, warmup):
+def run_simple(steps, warmup, graph=False):
     from models.gnns.model_mnb import GNN_simple
     torch.manual_seed(0)
     model = GNN_simple(0, 2, 20, 5, 1, 1).cuda()
@@ -156,30 +173,38 @@ def run_simple(steps, warmup):
     crit = torch.nn.MSELoss()
 
     def step():
-        model.zero_grad(set_to_none=True)
+        for p in model.parameters():
+            p.grad = None
         X.grad = W.grad = None
         crit(model([X, W], Nb, mask), T).backward()
 
-    sec = timeit(step, steps, warmup)
-    return dict(config="cfg1", workload="GNN_simple(0,2,20,5,1,1) fwd+bwd, 32 SBM N=50 graphs",
+    sec = timeit(graphed(step) if graph else step, steps, warmup)
+    return dict(config="cfg1g" if graph else "cfg1",
+                workload="GNN_simple(0,2,20,5,1,1) fwd+bwd, 32 SBM N=50 graphs"
+                + (", step replayed from a HIP graph" if graph else ", eager"),
                 graphs_per_step=32, ms_per_step=round(sec * 1e3, 4), value=round(32 / sec, 2), unit="graphs/s",
                 dtype="fp32")
 
 
-def run_ccn(name, order, graphs, desc, steps, warmup):
+def run_ccn(name, order, graphs, desc, steps, warmup, graph=False):
     from models.compnets.model_ccn import CCN_1D, CCN_2D
     torch.manual_seed(0)
     net = (CCN_1D if order == 1 else CCN_2D)(5, 1, 2, 2).cuda()
     X, A, T, nb = ccn_batch(graphs)
     X.requires_grad_(True)
+    plan = net.plan(A, nb) if graph else None  # graph mode: the batch is planned once, outside
 
     def step():
-        net.zero_grad(set_to_none=True)
+        for p in net.parameters():
+            p.grad = None
         X.grad = None
-        out = net.forward_batch(X, A, nb)
+        out = net.forward_batch(X, A, nb, plan)
         ((out - T) ** 2).sum().backward()  # sum of the per-graph MSE losses (scripts/train_ccn.py:52-60)
 
-    sec = timeit(step, steps, warmup)
+    sec = timeit(graphed(step) if graph else step, steps, warmup)
+    if graph:
+        name += "g"
+        desc += ", plan built once, step replayed from a HIP graph"
     deg = (A > 0).sum(-1).double()
     return dict(config=name, workload=desc, graphs_per_step=len(graphs), ms_per_step=round(sec * 1e3, 4),
                 value=round(len(graphs) / sec, 2), unit="graphs/s", dtype="fp32",
@@ -197,6 +222,7 @@ def main():
     import hgnn_amd.datagen as dg
     jobs = {
         "cfg1": lambda: run_simple(a.steps, a.warmup),
+        "cfg1g": lambda: run_simple(a.steps, a.warmup, graph=True),
         "cfg2f": lambda: run_lg("cfg2f", "GNN_lg d=64 order 2 L=5, forward only, 512 QM9-shape", 64, 2, 512,
                                 a.steps, a.warmup, backward=False),
         "cfg2o1": lambda: run_lg("cfg2o1", "GNN_lg d=64 order 1 L=5 fwd+bwd, 512 QM9-shape", 64, 1, 512, a.steps,
@@ -208,6 +234,8 @@ def main():
         "cfg2train_csr": lambda: run_train(a.steps, a.warmup, csr=True),
         "cfg3": lambda: run_ccn("cfg3", 1, dg.qm9_shape_dataset(256, seed=0),
                                 "CCN_1D(5,1,2,2) fwd+bwd, 256 QM9-shape graphs", a.steps, a.warmup),
+        "cfg3g": lambda: run_ccn("cfg3", 1, dg.qm9_shape_dataset(256, seed=0),
+                                 "CCN_1D(5,1,2,2) fwd+bwd, 256 QM9-shape graphs", a.steps, a.warmup, graph=True),
         "cfg4": lambda: run_lg("cfg4", "GNN_lg d=128 order 2 L=5 fwd+bwd, 512 QM9-shape (1 GPU of 4096)", 128, 2,
                                512, a.steps, a.warmup),
         "cfg5": lambda: run_ccn("cfg5", 2, dg.sbm_dataset(64, n=200, seed=0),
