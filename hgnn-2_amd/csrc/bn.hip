@@ -182,7 +182,9 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
     if (r0 >= total) return;
     const int r1 = min(total, r0 + 64);
     const float wv = *a.w;
-    const int L = a.c >> 2, RG = 256 / L;
+    // row groups: at most the tile's 64 rows (narrow C: more groups would only lengthen the serial
+    // per-channel combine below -- 256 of them made this kernel 16 us at C = 4, cfg1)
+    const int L = a.c >> 2, RG = min(256 / L, 64);
     const int lane = threadIdx.x % L, rg = threadIdx.x / L;
     __shared__ float4 red[4][256];
     float4 s[4];
@@ -260,7 +262,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
     const int r0 = blockIdx.x * 64;
     if (r0 >= total) return;
     const int r1 = min(total, r0 + 64);
-    const int L = a.c >> 2, RG = 256 / L;
+    const int L = a.c >> 2, RG = min(256 / L, 64);  // see k_bn_bwd_part4
     const int lane = threadIdx.x % L, rg = threadIdx.x / L;
     __shared__ float4 red[256];
     float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -44,7 +44,8 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
                      ((reinterpret_cast<uintptr_t>(a.dA) | reinterpret_cast<uintptr_t>(a.xp)) & 15) == 0;
 
     float* dWb = a.dW + (long long)b * nmax * nmax * J;
-    for (int base = 0; base < nitems; base += 4 * MAXI) {  // block-uniform passes over the items
+    // block-uniform passes over the items; gridDim.y blocks of a graph share them
+    for (int base = blockIdx.y * 4 * MAXI; base < nitems; base += gridDim.y * 4 * MAXI) {
     f32x16 acc[MAXI];
 #pragma unroll
     for (int q = 0; q < MAXI; ++q)
@@ -219,10 +220,10 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
 }
 
 template <int FC>
-static void launch_fc(const DwDenseArgs& a, int maxi, size_t lds, hipStream_t s) {
-    if (maxi <= 1) hipLaunchKernelGGL((k_dw_dense<FC, 1>), dim3(a.bs), dim3(256), lds, s, a);
-    else if (maxi <= 3) hipLaunchKernelGGL((k_dw_dense<FC, 3>), dim3(a.bs), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL((k_dw_dense<FC, 5>), dim3(a.bs), dim3(256), lds, s, a);
+static void launch_fc(const DwDenseArgs& a, int maxi, int gy, size_t lds, hipStream_t s) {
+    if (maxi <= 1) hipLaunchKernelGGL((k_dw_dense<FC, 1>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    else if (maxi <= 3) hipLaunchKernelGGL((k_dw_dense<FC, 3>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((k_dw_dense<FC, 5>), dim3(a.bs, gy), dim3(256), lds, s, a);
 }
 
 int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
@@ -231,10 +232,17 @@ int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
     const size_t lds = sizeof(float) * (size_t)npad * ((a.jt * fc + 1) + (fc + 1));
     if (lds > 64 * 1024) return 2;
     const int tiles = npad / 32;
-    const int maxi = ceil_div(tiles * tiles * a.jt, 4);
-    if (fc == 64) launch_fc<64>(a, maxi, lds, s);
-    else if (fc == 32) launch_fc<32>(a, maxi, lds, s);
-    else launch_fc<16>(a, maxi, lds, s);
+    const int nitems = tiles * tiles * a.jt;
+    int maxi = ceil_div(nitems, 4), gy = 1;
+    if (a.bs < 256 && nitems > 4) {
+        // few graphs (cfg1: 32): one item per wave and the items' passes spread over blocks, so the
+        // grid is not a handful of long blocks (17 -> a few us per launch)
+        maxi = 1;
+        gy = ceil_div(nitems, 4);
+    }
+    if (fc == 64) launch_fc<64>(a, maxi, gy, lds, s);
+    else if (fc == 32) launch_fc<32>(a, maxi, gy, lds, s);
+    else launch_fc<16>(a, maxi, gy, lds, s);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

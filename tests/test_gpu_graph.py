@@ -15,13 +15,22 @@ import fixture_util as fu
 pytestmark = pytest.mark.gpu
 
 
-def _capture(step):
+def _capture(step, keep=None):
+    """keep: the dict the step stores its output in; emptied before the capture so that no eagerly
+    allocated autograd graph (executor workspace included) is freed while capturing -- that was
+    seen to crash the graph instantiation (capture_end) on the box."""
+    if keep is not None:
+        keep.clear()
+    torch.cuda.synchronize()
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
         for _ in range(2):
             step()
     torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    if keep is not None:
+        keep.clear()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
@@ -63,7 +72,7 @@ def test_graph_replay_equals_eager_step(kind):
     ref_out = out_buf["out"].detach().clone()
     ref = {k: p.grad.clone() for k, p in model.named_parameters()}
     ref_dx = X.grad.clone()
-    g = _capture(step)
+    g = _capture(step, out_buf)
     for _ in range(3):
         g.replay()
     torch.cuda.synchronize()
@@ -106,9 +115,10 @@ def test_ccn1_graph_replay_with_plan_equals_eager():
     ref = {k: p.grad.clone() for k, p in net.named_parameters()}
     ref_dx = X.grad.clone()
     # the eager step without a plan computes the same
-    out2 = net.forward_batch(X, A, nb)
-    assert torch.equal(out2.detach(), ref_out)
-    g = _capture(step)
+    with torch.no_grad():
+        assert torch.equal(net.forward_batch(X, A, nb), ref_out)
+    torch.cuda.synchronize()
+    g = _capture(step, buf)
     for _ in range(3):
         g.replay()
     torch.cuda.synchronize()
