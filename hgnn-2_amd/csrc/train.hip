@@ -55,6 +55,46 @@ __global__ void __launch_bounds__(256) k_mse_loss(const float* __restrict__ out,
     }
 }
 
+// Classification branch of the reference step (scripts/train_mnb.py:50-51: mean == 0 ->
+// T = T.squeeze().long(); the drivers pass nn.CrossEntropyLoss, scripts/main_generate.py:147):
+// loss = mean_i (logsumexp(out_i) - out_i[t_i]), dout = (softmax(out_i) - onehot(t_i)) / n,
+// the running loss as in k_mse_loss; the MAE meters are not updated (train_mnb.py:81-82).
+// One block; a thread per row, classes in a serial loop (C is the model's dim_output).
+__global__ void __launch_bounds__(256) k_xent_loss(const float* __restrict__ out, const float* __restrict__ t, int n,
+                                                   int c, float* __restrict__ stats, float* __restrict__ dout,
+                                                   uint32_t* __restrict__ err) {
+    __shared__ double red[4];
+    double se = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const float* x = out + (long long)i * c;
+        const int ti = (int)t[i];  // LongTensor cast truncates toward zero
+        if (ti < 0 || ti >= c || (float)ti != t[i]) {
+            atomicOr(err, 1u);
+            continue;
+        }
+        float m = x[0];
+        for (int k = 1; k < c; ++k) m = fmaxf(m, x[k]);
+        float s = 0.f;
+        for (int k = 0; k < c; ++k) s += expf(x[k] - m);
+        const float lse = m + logf(s);
+        se += (double)(lse - x[ti]);
+        if (dout) {
+            const float inv = 1.0f / (float)n;
+            for (int k = 0; k < c; ++k) dout[(long long)i * c + k] = (expf(x[k] - lse) - (k == ti ? 1.f : 0.f)) * inv;
+        }
+    }
+    se = wave_sum_d(se);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = se;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double S = 0.0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) S += red[i];
+        const float loss = n > 0 ? (float)(S / n) : 0.f;
+        stats[0] = loss;
+        stats[2] = stats[2] == 0.f ? loss : 0.9f * loss + 0.1f * stats[2];
+    }
+}
+
 constexpr int ADAMAX_MAX = 64;
 
 struct AdamaxTable {
@@ -97,6 +137,15 @@ int hgnn_mse_loss(const float* d_out, const float* d_t, int n, float t_mean, flo
     if (!d_out || !d_t || !d_stats || n < 0) return HGNN_ERR_ARG;
     hipLaunchKernelGGL(k_mse_loss, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), d_out, d_t, n, t_mean,
                        t_std, d_stats, d_dout);
+    HGNN_LAUNCH_CHECK();
+    return HGNN_OK;
+}
+
+int hgnn_xent_loss(const float* d_out, const float* d_t, int n, int c, float* d_stats, float* d_dout,
+                   uint32_t* d_err, void* stream) {
+    if (!d_out || !d_t || !d_stats || !d_err || n < 0 || c < 1) return HGNN_ERR_ARG;
+    hipLaunchKernelGGL(k_xent_loss, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), d_out, d_t, n, c,
+                       d_stats, d_dout, d_err);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
 }

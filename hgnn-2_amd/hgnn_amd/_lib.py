@@ -116,6 +116,7 @@ SIGNATURES = {
     "hgnn_net_backward_csr": ([ctypes.POINTER(NetConfig), ctypes.POINTER(CsrBatch), _VP, _VP, _VP, _VP, _VP,
                                _VP], _I),
     "hgnn_mse_loss": ([_VP, _VP, _I, ctypes.c_float, ctypes.c_float, _VP, _VP, _VP], _I),
+    "hgnn_xent_loss": ([_VP, _VP, _I, _I, _VP, _VP, _VP, _VP], _I),
     "hgnn_adamax_step": ([_I, _VP, _VP, _VP, _VP, _VP, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                           ctypes.c_double, ctypes.c_double, ctypes.c_longlong, _VP], _I),
     "hgnn_conv1x1_workspace_bytes": ([_I, _I, _I, _I], ctypes.c_size_t),

@@ -14,8 +14,9 @@ device and no host synchronisation:
   all-reduce   optional gradient bucket all-reduce (hgnn_amd.dp.GradAllReduce)
   optimizer    hgnn_adamax_step: Adamax over every parameter in one launch
 
-Regression targets only (the reference's `mean == 0` branch casts T to
-LongTensor for a classification criterion, scripts/train_mnb.py:50-53).
+Classification (the reference's `mean == 0` branch, scripts/train_mnb.py:50-51: T cast to
+class indices, the drivers' nn.CrossEntropyLoss, scripts/main_generate.py:147) uses
+hgnn_xent_loss instead; the MAE meters stay untouched as in the reference.
 """
 
 import ctypes
@@ -34,8 +35,10 @@ class TrainStep:
     """
 
     def __init__(self, model, lr=3e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, t_mean=0.0, t_std=1.0,
-                 grad_allreduce=None):
+                 grad_allreduce=None, classification=None):
         self.model = model
+        # the reference's rule: mean == 0 marks generated (classification) data
+        self.classification = (float(t_mean) == 0.0) if classification is None else bool(classification)
         self.params = [p for p in model.parameters()]
         self.lr = float(lr)
         self.betas = (float(betas[0]), float(betas[1]))
@@ -51,6 +54,7 @@ class TrainStep:
             if p.dtype != torch.float32 or not p.is_contiguous():
                 raise RuntimeError("hgnn_amd: TrainStep needs contiguous float32 parameters")
         self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
+        self._err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._numel = (ctypes.c_int64 * len(self.params))(*[p.numel() for p in self.params])
         self.reset_optimizer()
 
@@ -85,12 +89,18 @@ class TrainStep:
             p.grad = None
         out, T = self._forward(batch)
         T = T.to(torch.float32).contiguous()
-        if T.numel() != out.numel():
-            raise RuntimeError(f"hgnn_amd: targets {tuple(T.shape)} do not match the output {tuple(out.shape)}")
         stream = L.stream_handle(out.device)
         dout = torch.empty_like(out)
-        L.check(lib.hgnn_mse_loss(L.ptr(out.detach()), L.ptr(T), out.numel(), self.t_mean, self.t_std,
-                                  L.ptr(self.stats), L.ptr(dout), stream), "mse loss")
+        if self.classification:
+            if T.numel() != out.shape[0]:
+                raise RuntimeError(f"hgnn_amd: class targets {tuple(T.shape)} do not match {out.shape[0]} rows")
+            L.check(lib.hgnn_xent_loss(L.ptr(out.detach()), L.ptr(T), out.shape[0], out.shape[1], L.ptr(self.stats),
+                                       L.ptr(dout), L.ptr(self._err), stream), "cross-entropy loss")
+        else:
+            if T.numel() != out.numel():
+                raise RuntimeError(f"hgnn_amd: targets {tuple(T.shape)} do not match the output {tuple(out.shape)}")
+            L.check(lib.hgnn_mse_loss(L.ptr(out.detach()), L.ptr(T), out.numel(), self.t_mean, self.t_std,
+                                      L.ptr(self.stats), L.ptr(dout), stream), "mse loss")
         torch.autograd.backward(out, dout)
         if self.allreduce is not None:
             self.allreduce()
@@ -103,3 +113,8 @@ class TrainStep:
                                      self.betas[0], self.betas[1], self.eps, self.weight_decay, self.step_count,
                                      stream), "adamax step")
         return self.stats
+
+    def check_targets(self):
+        """Raise if a classification step saw a target outside [0, dim_output) (host sync)."""
+        if int(self._err.item()):
+            raise RuntimeError("hgnn_amd: class target outside [0, dim_output) or not an integer")

@@ -16,8 +16,17 @@ training mode exactly as the reference rebinds them.
 import torch
 import torch.nn as nn
 
+import os
+
 from hgnn_amd.dp import attached
+from hgnn_amd.library import run_net_ops
 from hgnn_amd.net import NetSpec, run_net, run_net_csr
+
+
+def use_torch_ops():
+    """The registered torch.library operators (hgnn_amd.library) while torch.compile traces the
+    module, or always with HGNN_TORCH_OPS=1; the autograd.Function path otherwise."""
+    return os.environ.get("HGNN_TORCH_OPS") == "1" or torch.compiler.is_compiling()
 from models.layers import layers_mnb
 
 
@@ -64,6 +73,8 @@ class GNN_simple(nn.Module):
 
     def forward(self, state, N_batch, mask):
         X, W = state
+        if use_torch_ops():
+            return run_net_ops(self._spec(X.device), X, W, N_batch, mask)
         return run_net(self._spec(X.device), X, W, N_batch, mask)
 
     def forward_csr(self, batch):
@@ -112,6 +123,8 @@ class GNN_lg(nn.Module):
 
     def forward(self, state, N_batch, mask, E_batch, mask_lg):
         X, XL, W, WL, Pm, Pd = state
+        if use_torch_ops():
+            return run_net_ops(self._spec(X.device), X, W, N_batch, mask, XL, WL, Pm, Pd, E_batch, mask_lg)
         return run_net(self._spec(X.device), X, W, N_batch, mask, XL, WL, Pm, Pd, E_batch, mask_lg)
 
     def forward_csr(self, batch):

@@ -249,6 +249,14 @@ int hgnn_net_backward_csr(const hgnn_net_config* cfg, const hgnn_csr_batch* batc
  * ---------------------------------------------------------------------- */
 int hgnn_mse_loss(const float* d_out, const float* d_t, int n, float t_mean, float t_std, float* d_stats,
                   float* d_dout, void* stream);
+
+/* Classification branch (scripts/train_mnb.py:50-51, nn.CrossEntropyLoss of
+ * scripts/main_generate.py:147): d_out (n, c) logits, d_t (n,) class indices stored
+ * as float (prepare_batch's T); stats[0] = mean cross entropy, stats[2] its
+ * RunningAverage (stats[1], stats[3] untouched: no MAE for classes); d_dout =
+ * (softmax - onehot) / n.  A target outside [0, c) or not integral sets *d_err. */
+int hgnn_xent_loss(const float* d_out, const float* d_t, int n, int c, float* d_stats,
+                   float* d_dout, uint32_t* d_err, void* stream);
 int hgnn_adamax_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
                      float* const* exp_inf, const int64_t* numel, double lr, double beta1, double beta2,
                      double eps, double weight_decay, long long step, void* stream);

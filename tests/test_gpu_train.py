@@ -109,3 +109,54 @@ def test_adamax_kernel_matches_torch_exactly_on_fixed_grads():
                                          L.stream_handle(ps[0].device)), "adamax")
         for p, q in zip(ps, qs):
             assert torch.allclose(p, q.detach(), rtol=0, atol=1e-7 * max(1.0, q.abs().max().item()))
+
+
+def test_train_step_classification_matches_cross_entropy_adamax():
+    """mean == 0 (generated data): T -> class indices, nn.CrossEntropyLoss (scripts/train_mnb.py:50-51,
+    scripts/main_generate.py:147); the device step against torch's loss + Adamax from equal states."""
+    import hgnn_amd.datagen as dg
+    from hgnn_amd.train import TrainStep
+    from models.gnns.model_mnb import GNN_lg
+    torch.manual_seed(21)
+    model = GNN_lg(0, 16, 4, 5, 3, 1, 2).cuda()  # dim_output = 3 classes
+    ref = copy.deepcopy(model)
+    lr = 1e-3
+    opt = torch.optim.Adamax(ref.parameters(), lr=lr)
+    crit = torch.nn.CrossEntropyLoss()
+    step = TrainStep(model, lr=lr, t_mean=0.0)
+    assert step.classification
+    run_loss = None
+    for i in range(3):
+        graphs = dg.qm9_shape_dataset(48, seed=700 + i)
+        b = _batch(graphs)
+        b[2] = torch.randint(0, 3, (48, 1), generator=torch.Generator().manual_seed(i)).float().cuda()
+        X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = b
+        opt.zero_grad()
+        out = ref([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+        loss = crit(out, T.squeeze().long())
+        loss.backward()
+        opt.step()
+        lv = loss.item()
+        run_loss = lv if run_loss is None else 0.9 * lv + 0.1 * run_loss
+        s = step(b).cpu()
+        step.check_targets()
+        assert abs(s[0].item() - lv) <= 1e-5 * max(1.0, abs(lv)), (s[0].item(), lv)
+        assert abs(s[2].item() - run_loss) <= 1e-5 * max(1.0, abs(run_loss))
+        assert s[1].item() == 0.0 and s[3].item() == 0.0  # no MAE for classes
+        gmax = max(q.grad.abs().max().item() for q in ref.parameters())
+        for (n, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+            quiet = q.grad.abs() > 1e-4 * gmax
+            err = (p.detach() - q.detach()).abs()
+            assert err[quiet].numel() == 0 or err[quiet].max().item() <= 1e-5 * max(1.0, q.abs().max().item()), n
+            assert err.max().item() <= 2 * lr, n
+        with torch.no_grad():
+            for k, (p, q) in enumerate(zip(model.parameters(), ref.parameters())):
+                p.copy_(q)
+                st = opt.state[q]
+                step.exp_avg[k].copy_(st["exp_avg"])
+                step.exp_inf[k].copy_(st["exp_inf"])
+    bad = _batch(dg.qm9_shape_dataset(4, seed=9))
+    bad[2] = torch.tensor([[0.0], [5.0], [1.0], [2.0]]).cuda()
+    step(bad)
+    with pytest.raises(RuntimeError, match="class target"):
+        step.check_targets()
