@@ -15,9 +15,14 @@ The reference builds this with O(N^2 + M^2) Python loops (24 ms per QM9-shape
 graph, 1.66 s per SBM-50 graph).  Here the construction is the
 native builder of csrc/builder.cpp (hgnn_graph_operators in include/hgnn_amd.h):
 sparse edge-slot / line-graph construction in C++, dense tensors written once.
-Degrees, row sums and matrix powers are accumulated exactly (every partial sum
-of bond-order weights is representable in fp32), so values equal the
-reference's torch fp32 reductions bit for bit.
+Degrees, row sums and matrix powers are accumulated in double and rounded once.
+Precondition of the bit-exact claim: dyadic weights (bond orders 1, 1.5, 2, 3 --
+every partial sum is representable in fp32, so the reference's torch fp32
+reductions are exact too).  With real-valued weights (distances, model_mnb.py:82;
+weighted SBMs) D and A^2 entries may differ from the reference by its own fp32
+rounding, <= N * 2^-24 * sum|terms| (tests/test_builder.py::
+test_graph_operators_real_valued_weights_within_reference_rounding); I, A, the
+line graph's weights and Pm / Pd stay bit-exact.
 """
 
 import ctypes
