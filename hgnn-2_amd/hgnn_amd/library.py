@@ -143,6 +143,7 @@ def _setup_context(ctx, inputs, output):
     keep = [t for t in (X, W, N_batch, mask, XL, WL, Pm, Pd, E_batch, mask_lg) if t is not None]
     ctx.save_for_backward(ws, *keep, *params)
     ctx.n_params = len(params)
+    ctx.n_running = len(running)
     ctx.meta = (kind, order, d, n_layers, dim_out, training)
 
 
@@ -158,7 +159,7 @@ def _backward(ctx, dout, dws, drunning):
     dX, dW, grads = torch.ops.hgnn_amd.net_backward(dout, ws, X, W, N_batch, mask, XL, WL, Pm, Pd, E_batch, mask_lg,
                                                      params, *ctx.meta, need_dx, need_dw)
     return (dX if need_dx else None, dW if need_dw else None, None, None, None, None, None, None, None, None,
-            list(grads), None, None, None, None, None, None, None)
+            list(grads), [None] * ctx.n_running, None, None, None, None, None, None)
 
 
 net_forward.register_autograd(_backward, setup_context=_setup_context)

@@ -39,7 +39,7 @@ def _step(model, b, kind, fn=None):
     X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = [t.clone() for t in b]
     X.requires_grad_(True)
     W.requires_grad_(True)
-    fn = fn or model
+    fn = model if fn is None else fn
     out = fn([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg) if kind == "lg" else fn([X, W], Nb, mask)
     loss = torch.nn.MSELoss()(out, T)
     loss.backward()
