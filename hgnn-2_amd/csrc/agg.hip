@@ -229,8 +229,10 @@ __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
         store_row<CP, V>(o + base + a.cp, a.cp, lane, ad);
     }
     // zero the row padding [K, ldo): the GEMMs run over the padded width
-    const int kk = JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
-    if (lane < a.ldo - kk) o[kk + lane] = 0.f;
+    if (a.pad_from >= 0) {
+        const int kk = a.pad_from > 0 ? a.pad_from : JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
+        if (lane < a.ldo - kk) o[kk + lane] = 0.f;
+    }
 }
 
 static int cpl_of(int c) {
@@ -245,8 +247,8 @@ static int cpl_of(int c) {
 template <int JT, int CG, int CP>
 static void agg_fwd_v(const AggFwdArgs& a, dim3 g, hipStream_t s) {
     const int kk = JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
-    const bool v = vec_ok(CG, a.cg, a.xg, {}) && (CP == 0 || vec_ok(CP, a.cp, a.xp, {})) &&
-                   vec_ok(CG, a.cg, a.out, {a.ldo, (long long)kk}) &&
+    const bool v = (CG == 0 || vec_ok(CG, a.cg, a.xg, {})) && (CP == 0 || vec_ok(CP, a.cp, a.xp, {})) &&
+                   (CG == 0 || vec_ok(CG, a.cg, a.out, {a.ldo, (long long)kk})) &&
                    (CP == 0 || vec_ok(CP, a.cp, a.out, {a.ldo, (long long)JT * a.cg, (long long)a.cp}));
     if (v) hipLaunchKernelGGL((k_agg_fwd<JT, CG, CP, true>), g, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_agg_fwd<JT, CG, CP, false>), g, dim3(256), 0, s, a);
@@ -269,6 +271,9 @@ static int agg_fwd_cp(const AggFwdArgs& a, dim3 g, hipStream_t s) {
 template <int JT>
 static int agg_fwd_cg(const AggFwdArgs& a, dim3 g, hipStream_t s) {
     switch (cpl_of(a.xg ? a.cg : 0)) {
+        case 0:  // P part only (its columns still start at jtot * cg)
+            if (!a.xp) return 2;
+            return agg_fwd_cp<JT, 0>(a, g, s);
         case 1: return agg_fwd_cp<JT, 1>(a, g, s);
         case 2: return agg_fwd_cp<JT, 2>(a, g, s);
         case 4: return agg_fwd_cp<JT, 4>(a, g, s);

@@ -47,6 +47,7 @@ struct ExtractArgs {
     int entry_stride_w;   // floats per W/WL entry
     int validate;
     int dual;             // 0: GNN_simple (only S_W / S_WT)
+    int kind0;            // first block slot of the launch (blockIdx.y + kind0, struct.hip)
 };
 int launch_extract(const ExtractArgs& a, hipStream_t s);
 
@@ -93,6 +94,9 @@ struct AggFwdArgs {
     BnView pbn;
     float* out;
     int ldo;
+    // the row's zero padding [pad_from, ldo): 0 = after the parts this launch writes, -1 = none
+    // (a G-only launch beside a P-only one, which writes the padding)
+    int pad_from;
 };
 int launch_agg_fwd(const AggFwdArgs& a, hipStream_t s);
 

@@ -393,6 +393,68 @@ struct Timer {
         }                                                                               \
     } while (0)
 
+// Side stream.  Forward (line graph): the G part of a half's aggregation beside the main
+// stream's P part and GEMMs (net_forward).  Backward: the weight-gradient GEMM of a half (and its slab
+// reduction) only feeds the parameter grads, so it runs beside the dA -> dense dW
+// -> aggregation-backward chain of the same half.  Fork after the half's BN
+// backward, join before the next half's BN backward overwrites dY / the bias
+// partials, and once more at the end.  One non-blocking stream and a few events
+// per host thread and device, created on first use.
+struct SideStream {
+    int dev = -1;
+    hipStream_t s = nullptr;
+    hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
+    std::vector<hipEvent_t> pool;  // the forward's per-half events, grown on demand
+    int event(size_t i, hipEvent_t* out) {
+        while (pool.size() <= i) {
+            hipEvent_t e = nullptr;
+            HGNN_HOST_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            pool.push_back(e);
+        }
+        *out = pool[i];
+        return 0;
+    }
+};
+
+static int side_stream(hipStream_t main_s, SideStream** out) {
+    thread_local SideStream ss;
+    // the device the caller's stream belongs to, not the thread's current device: the side
+    // stream's kernels read and write the main stream's buffers
+    hipDevice_t dev = 0;
+    HGNN_HOST_CHECK(hipStreamGetDevice(main_s, &dev));
+    if (ss.dev != dev) {
+        int cur = 0;
+        HGNN_HOST_CHECK(hipGetDevice(&cur));
+        HGNN_HOST_CHECK(hipSetDevice(dev));
+        if (ss.s) {
+            (void)hipStreamDestroy(ss.s);
+            for (int i = 0; i < 2; ++i) {
+                (void)hipEventDestroy(ss.fork[i]);
+                (void)hipEventDestroy(ss.join[i]);
+            }
+            for (hipEvent_t e : ss.pool) (void)hipEventDestroy(e);
+        }
+        ss = SideStream{};
+        HGNN_HOST_CHECK(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) {
+            HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming));
+            HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming));
+        }
+        ss.dev = dev;
+        HGNN_HOST_CHECK(hipSetDevice(cur));
+    }
+    *out = &ss;
+    return 0;
+}
+
+// HGNN_SPLIT_AGG=1: the G part of a half's forward aggregation on the side stream, beside the
+// main stream's P part and GEMMs.  Measured on the box: 290-313 K vs 322 K graphs/s (forward
+// 0.654 vs 0.586 ms): the gathers beside the power-limited MFMA GEMMs slowed both.  Off by default.
+static bool split_agg_enabled() {
+    static const bool on = env_flag("HGNN_SPLIT_AGG", false);
+    return on;
+}
+
 int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
                 const float* const* prm, float* const* run, void* ws, float* out, hipStream_t s, Timer* tm) {
     const Program P = build_program(c);
@@ -452,10 +514,89 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
             }
         }
     }
-    for (const Half& h : P.halves) {
+    // Line graph: a half's aggregation is two independent parts -- G (its own kind's features of
+    // the previous layer, final one half earlier) and P (the other kind's features, produced by
+    // the half just before).  The G part runs on the side stream as soon as its input is final,
+    // beside the main stream's P part and Conv1d GEMM of the previous half: memory-bound gathers
+    // beside an MFMA-bound GEMM.  Events: pool[hi] = half hi's BN statistics final (main),
+    // pool[H + hi] = half hi's G part written (side), pool[2H] = inputs packed (main).
+    const int H = (int)P.halves.size();
+    const bool split = lg && P.v2 && !P.fused && split_agg_enabled();
+    SideStream* side = nullptr;
+    if (split) {
+        TRY(side_stream(s, &side));
+        hipEvent_t e;
+        TRY(side->event(2 * H, &e));
+        HGNN_HOST_CHECK(hipEventRecord(e, s));
+    }
+    auto agg_g_side = [&](int hi) -> int {
+        const Half& h = P.halves[hi];
+        const Half* pr = producer(P, h.gin);
+        int wait_i = 2 * H;
+        if (pr) wait_i = (int)(pr - P.halves.data());
+        hipEvent_t ready, done;
+        TRY(side->event(wait_i, &ready));
+        TRY(side->event(H + hi, &done));
+        HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, ready, 0));
+        AggFwdArgs ag{};
+        ag.total_rows = h.edge ? tot_e : tot_n;
+        ag.cap_rows = h.edge ? P.cap_e : P.cap_n;
+        ag.g = src.v[h.edge ? S_WL : S_W];
+        ag.xg = feat_src(P, ws, h.gin, src.x0, src.xl0);
+        ag.gbn = feat_bn(P, ws, prm, h.gin);
+        ag.cg = h.cg;
+        ag.jtot = P.jt;
+        ag.out = at<float>(ws, h.a);
+        ag.ldo = h.kp;
+        ag.pad_from = -1;
+        hipStream_t main_s = s;
+        s = side->s;
+        int r = 0;
+        do {
+            TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
+            r = hipEventRecord(done, s) == hipSuccess ? 0 : HGNN_ERR_HIP;
+        } while (0);
+        s = main_s;
+        return r;
+    };
+    // the G part of a half is enqueued once the half producing its input has been enqueued
+    // (halves whose input is a network input: right away)
+    int g_next = 0;
+    auto enqueue_ready_g = [&](int done_hi) -> int {
+        while (split && g_next < H) {
+            const Half* pr = producer(P, P.halves[g_next].gin);
+            if (pr && (int)(pr - P.halves.data()) > done_hi) break;
+            TRY(agg_g_side(g_next));
+            ++g_next;
+        }
+        return 0;
+    };
+    TRY(enqueue_ready_g(-1));
+    for (int hi = 0; hi < H; ++hi) {
+        const Half& h = P.halves[hi];
         const int cap = h.edge ? P.cap_e : P.cap_n;
         const int* tot = h.edge ? tot_e : tot_n;
-        if (fused_fwd_half(P, h)) {
+        if (split) {
+            AggFwdArgs ag{};
+            ag.total_rows = tot;
+            ag.cap_rows = cap;
+            ag.cg = h.cg;  // the P columns start at jtot * cg
+            ag.jtot = P.jt;
+            ag.p = src.v[h.edge ? S_PE : S_PN];
+            ag.xp = feat_src(P, ws, h.pin, src.x0, src.xl0);
+            ag.pbn = feat_bn(P, ws, prm, h.pin);
+            ag.cp = h.cp;
+            ag.out = at<float>(ws, h.a);
+            ag.ldo = h.kp;
+            TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
+            hipEvent_t gdone;
+            TRY(side->event(H + hi, &gdone));
+            HGNN_HOST_CHECK(hipStreamWaitEvent(s, gdone, 0));
+            TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<float>(ws, h.wc), h.kp,
+                                                 P.c2, at<float>(ws, h.bc), h.relu_from,
+                                                 at<float>(ws, P.feats[h.out].y), P.c2,
+                                                 c->training ? at<float>(ws, h.part) : nullptr, s));
+        } else if (fused_fwd_half(P, h)) {
             // aggregation gathered into LDS tiles of the Conv1d-pair GEMM; the aggregate is still
             // written once (h.a) for the weight-gradient GEMM of the backward
             FusedArgs fa{};
@@ -558,6 +699,12 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
         bf.momentum = 0.1f;
         if (!c->training && !run) return HGNN_ERR_ARG;
         TL(HGNN_K_BN_FWD, launch_bn_finalize(bf, s));
+        if (split) {
+            hipEvent_t fin;
+            TRY(side->event(hi, &fin));
+            HGNN_HOST_CHECK(hipEventRecord(fin, s));
+            TRY(enqueue_ready_g(hi));
+        }
     }
 
     AggFwdArgs ag{};
@@ -579,48 +726,6 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
     TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
     TL(HGNN_K_READOUT, launch_readout_fwd(at<float>(ws, P.a_last), P.k_last, m.node_off, c->bs, c->nmax, prm[P.p_fcw],
                            prm[P.p_fcb], c->dim_out, at<float>(ws, P.colsum), out, s));
-    return 0;
-}
-
-// Side stream of the backward: the weight-gradient GEMM of a half (and its slab
-// reduction) only feeds the parameter grads, so it runs beside the dA -> dense dW
-// -> aggregation-backward chain of the same half.  Fork after the half's BN
-// backward, join before the next half's BN backward overwrites dY / the bias
-// partials, and once more at the end.  One non-blocking stream and a few events
-// per host thread and device, created on first use.
-struct SideStream {
-    int dev = -1;
-    hipStream_t s = nullptr;
-    hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
-};
-
-static int side_stream(hipStream_t main_s, SideStream** out) {
-    thread_local SideStream ss;
-    // the device the caller's stream belongs to, not the thread's current device: the side
-    // stream's kernels read and write the main stream's buffers
-    hipDevice_t dev = 0;
-    HGNN_HOST_CHECK(hipStreamGetDevice(main_s, &dev));
-    if (ss.dev != dev) {
-        int cur = 0;
-        HGNN_HOST_CHECK(hipGetDevice(&cur));
-        HGNN_HOST_CHECK(hipSetDevice(dev));
-        if (ss.s) {
-            (void)hipStreamDestroy(ss.s);
-            for (int i = 0; i < 2; ++i) {
-                (void)hipEventDestroy(ss.fork[i]);
-                (void)hipEventDestroy(ss.join[i]);
-            }
-        }
-        ss = SideStream{};
-        HGNN_HOST_CHECK(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
-        for (int i = 0; i < 2; ++i) {
-            HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming));
-            HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming));
-        }
-        ss.dev = dev;
-        HGNN_HOST_CHECK(hipSetDevice(cur));
-    }
-    *out = &ss;
     return 0;
 }
 
@@ -748,7 +853,10 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         HGNN_HOST_CHECK(hipEventRecord(side->fork[parity], s));
         HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, side->fork[parity], 0));
         hipStream_t main_s = s;
-        s = side->s;  // TL records its timer events on the stream the kernel runs on
+        // HGNN_SERIAL_BWD=1 (diagnostics): everything on the main stream, so a kernel trace shows
+        // each kernel's standalone duration
+        static const bool serial = env_flag("HGNN_SERIAL_BWD", false);
+        if (!serial) s = side->s;  // TL records its timer events on the stream the kernel runs on
         int r = 0;
         do {
             // fused backward: dX needs no dA, only the dense operator gradient does -- its G

@@ -12,6 +12,8 @@
 // compacts the nonzeros of each 64-column chunk.  The union of the J+2 slices
 // (or of Pm and Pd) is stored once per (row, col), so one gathered feature row
 // feeds every slice.
+#include <stdlib.h>
+
 #include "kernels.h"
 
 namespace hgnn {
@@ -81,65 +83,175 @@ int launch_plan(const int64_t* nb, const int64_t* eb, int bs, int nmax, int emax
 }
 
 // One workgroup per (graph, structure kind).  NC = number of coefficients per
-// entry (J+2 for W/WL, 2 for Pm/Pd).
+// entry (J+2 for W/WL, 2 for Pm/Pd).  A wave takes RU rows at a time and issues all their
+// loads before the first ballot: the per-row load -> ballot -> store chain was latency-bound.
 template <int NC>
 __device__ void extract_rows(int rows, int cols, int row_packed0, int col_packed0,
                              long long slot0, int cap, const float* __restrict__ s0,
                              const float* __restrict__ s1, long long rs, long long cs,
                              long long js, RowInfo* __restrict__ out_rows,
-                             float* __restrict__ entries, int stride) {
+                             float* __restrict__ entries, int stride, int part = 0, int nparts = 1) {
+    constexpr int RU = 8, CH = 2;  // rows per batch, 64-column chunks loaded per batch
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    for (int r = wv; r < rows; r += 4) {
-        const long long slot = slot0 + (long long)r * cap;
-        int cnt = 0;
-        for (int c0 = 0; c0 < cols; c0 += 64) {
-            const int c = c0 + lane;
-            float v[NC];
-            bool nz = false;
+    const int nw = blockDim.x >> 6;
+    const int wv = part * nw + (threadIdx.x >> 6);  // the block's waves over nparts blocks
+    // Loads are unconditional (clamped to a live element) and masked after they land: a load
+    // under a per-lane condition made hipcc wait vmcnt(0) right after it, serialising the batch.
+    auto ld = [&](int r, int c, float (&v)[NC]) {
+        const long long o = (long long)min(r, rows - 1) * rs + (long long)min(c, cols - 1) * cs;
+        if constexpr (NC == 2) {  // Pm / Pd
+            v[0] = s0[o];
+            v[1] = s1[o];
+        } else {
+#pragma unroll
+            for (int j = 0; j < NC; ++j) v[j] = s0[o + j * js];
+        }
+    };
+    auto live = [&](int r, int c, float (&v)[NC]) {
+        if (!(r < rows && c < cols))
 #pragma unroll
             for (int j = 0; j < NC; ++j) v[j] = 0.f;
-            if (c < cols) {
-                if (s1 == nullptr) {
-                    const float* p = s0 + r * rs + c * cs;
+    };
+    for (int rb = wv * RU; rb < rows; rb += nw * nparts * RU) {
+        int cnt[RU];
 #pragma unroll
-                    for (int j = 0; j < NC; ++j) v[j] = p[j * js];
-                } else {
-                    v[0] = s0[r * rs + c * cs];
-                    v[1] = s1[r * rs + c * cs];
+        for (int u = 0; u < RU; ++u) cnt[u] = 0;
+        for (int cb = 0; cb < cols; cb += 64 * CH) {
+            float v[RU][CH][NC];
+#pragma unroll
+            for (int u = 0; u < RU; ++u)
+#pragma unroll
+                for (int h = 0; h < CH; ++h) ld(rb + u, cb + h * 64 + lane, v[u][h]);
+#pragma unroll
+            for (int u = 0; u < RU; ++u)
+#pragma unroll
+                for (int h = 0; h < CH; ++h) live(rb + u, cb + h * 64 + lane, v[u][h]);
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                const int r = rb + u;
+                if (r >= rows) break;
+                const long long slot = slot0 + (long long)r * cap;
+#pragma unroll
+                for (int h = 0; h < CH; ++h) {
+                    const int c = cb + h * 64 + lane;
+                    bool nz = false;
+#pragma unroll
+                    for (int j = 0; j < NC; ++j) nz |= (v[u][h][j] != 0.f);
+                    const unsigned long long mask = __ballot(nz);
+                    const int pos = __popcll(mask & ((1ull << lane) - 1ull));
+                    if (nz) {
+                        float* e = entries + (slot + cnt[u] + pos) * stride;
+                        e[0] = __int_as_float(col_packed0 + c);
+#pragma unroll
+                        for (int j = 0; j < NC; ++j) e[1 + j] = v[u][h][j];
+                    }
+                    cnt[u] += __popcll(mask);
                 }
-#pragma unroll
-                for (int j = 0; j < NC; ++j) nz |= (v[j] != 0.f);
             }
-            const unsigned long long mask = __ballot(nz);
-            const int pos = __popcll(mask & ((1ull << lane) - 1ull));
-            if (nz) {
-                float* e = entries + (slot + cnt + pos) * stride;
-                e[0] = __int_as_float(col_packed0 + c);
-#pragma unroll
-                for (int j = 0; j < NC; ++j) e[1 + j] = v[j];
-            }
-            cnt += __popcll(mask);
         }
         if (lane == 0) {
-            RowInfo ri;
-            ri.start = (int)slot;
-            ri.count = cnt;
-            out_rows[row_packed0 + r] = ri;
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                const int r = rb + u;
+                if (r < rows) {
+                    RowInfo ri;
+                    ri.start = (int)(slot0 + (long long)r * cap);
+                    ri.count = cnt[u];
+                    out_rows[row_packed0 + r] = ri;
+                }
+            }
         }
+    }
+}
+
+// Transposed kinds (S_WT, S_WLT, S_PE): output row r' is column r' of the dense block, so the
+// lanes take 64 consecutive output rows and walk the block's rows in order, CU rows' loads in
+// flight at a time -- every load is one coalesced row segment, and each lane appends its own
+// row's entries (ascending column, the order extract_rows produces).  (Reading a column per
+// wave, as extract_rows does, touched a separate cache line per lane.  Measured alternative, not
+// kept: the dense rows split over 16 waves of a 1024-thread block with an LDS count scan --
+// 104 vs 40 us for the whole extraction, the redundant waves and barriers cost more than the
+// serial walk.)
+template <int NC>
+__device__ void extract_cols(int rows, int cols, int row_packed0, int col_packed0, long long slot0,
+                             int cap, const float* __restrict__ s0, const float* __restrict__ s1,
+                             long long rs, long long js, RowInfo* __restrict__ out_rows,
+                             float* __restrict__ entries, int stride) {
+    const int lane = threadIdx.x & 63;
+    const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
+    constexpr long long cstep = NC == 2 ? 1 : NC;  // dense column stride of this kind
+    constexpr int CU = 16;                         // dense rows loaded per batch
+    for (int r0 = wv * 64; r0 < rows; r0 += nw * 64) {
+        const int r = r0 + lane;
+        const int rl = min(r, rows - 1);  // lanes past the last row load a live one, store nothing
+        const long long slot = slot0 + (long long)r * cap;
+        int cnt = 0;
+        for (int cb = 0; cb < cols; cb += CU) {
+            float v[CU][NC];
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                const long long o = (long long)min(cb + u, cols - 1) * rs + rl * cstep;  // clamped
+                if constexpr (NC == 2) {
+                    v[u][0] = s0[o];
+                    v[u][1] = s1[o];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < NC; ++j) v[u][j] = s0[o + j * js];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                const int c = cb + u;
+                bool nz = false;
+#pragma unroll
+                for (int j = 0; j < NC; ++j) nz |= (v[u][j] != 0.f);
+                if (nz && c < cols && r < rows) {
+                    float* e = entries + (slot + cnt) * stride;
+                    e[0] = __int_as_float(col_packed0 + c);
+#pragma unroll
+                    for (int j = 0; j < NC; ++j) e[1 + j] = v[u][j];
+                    ++cnt;
+                }
+            }
+        }
+        if (r < rows) out_rows[row_packed0 + r] = RowInfo{(int)slot, cnt};
     }
 }
 
 // Flags any nonzero of a dense (R, C, NC) block outside [0, rr) x [0, rc).
 __device__ void validate_block(const float* __restrict__ blk, int R, int C, int NC, int rr,
                                int rc, uint32_t* err) {
-    const long long total = (long long)R * C * NC;
+    const int row = C * NC;
     bool bad = false;
-    for (long long i = threadIdx.x; i < total; i += blockDim.x) {
-        const int r = (int)(i / ((long long)C * NC));
-        const int c = (int)((i / NC) % C);
-        if ((r >= rr || c >= rc) && blk[i] != 0.f) bad = true;
+    // whole rows past rr: one flat sweep; rows below rr: only their columns past rc
+    // (8 loads in flight per thread: one load per iteration made these sweeps the slowest part
+    // of the extraction, 20-30 dependent round trips per block)
+    constexpr int U = 8;
+    const long long tail0 = (long long)rr * row, total = (long long)R * row;
+    const int nt = blockDim.x;
+    for (long long i0 = tail0 + threadIdx.x; i0 < total; i0 += (long long)U * nt) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long i = i0 + (long long)u * nt;
+            v[u] = blk[i < total ? i : total - 1];  // clamped, unconditional (see extract_rows)
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) bad |= v[u] != 0.f;
     }
+    const int pad = row - rc * NC;  // padded columns per live row
+    if (pad > 0)
+        for (int i0 = threadIdx.x; i0 < rr * pad; i0 += U * nt) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = min(i0 + u * nt, rr * pad - 1);
+                const int r = i / pad, q = i - r * pad;
+                v[u] = blk[(long long)r * row + rc * NC + q];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) bad |= v[u] != 0.f;
+        }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, (uint32_t)ERR_PAD_NONZERO);
 }
 
@@ -154,16 +266,30 @@ __device__ void validate_mask(const float* __restrict__ mask, int n, int real, u
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, (uint32_t)ERR_MASK);
 }
 
+// Block slots per graph.  Line graph: the dense WL block is the big one (Emax^2 (J+2) floats),
+// so its row extraction takes two blocks and all validation sweeps a block of their own; the
+// slow slots come first in dispatch order.  GNN_simple: W (+ its validation) and WT.
+enum ExtractSlot : int {
+    X_WL0 = 0, X_WL1, X_VALID, X_WLT, X_PN, X_W, X_PE, X_WT, X_SLOTS,
+};
+
+constexpr int X_THREADS = 256;
+
 template <int JT>
-__global__ void __launch_bounds__(256) k_extract(ExtractArgs a) {
+__global__ void __launch_bounds__(X_THREADS) k_extract(ExtractArgs a) {
     const int b = blockIdx.x;
-    const int kind = blockIdx.y;
+    const int slot = a.dual ? (int)blockIdx.y + a.kind0 : ((int)blockIdx.y + a.kind0 == 0 ? X_W : X_WT);
     const int n0 = a.meta.node_off[b];
     const int nb = a.meta.node_off[b + 1] - n0;
     const int nmax = a.nmax;
     const long long wblk = (long long)nmax * nmax * JT;
-    switch (kind) {
-        case S_W: {
+    const int emax = a.emax;
+    const int e0 = a.dual ? a.meta.edge_off[b] : 0;
+    const int eb = a.dual ? a.meta.edge_off[b + 1] - e0 : 0;
+    const long long lblk = (long long)emax * emax * JT;
+    const long long pblk = (long long)nmax * emax;
+    switch (slot) {
+        case X_W: {
             const float* src = a.W + b * wblk;
             extract_rows<JT>(nb, nb, n0, n0, (long long)b * nmax * nmax, nmax, src, nullptr,
                              (long long)nmax * JT, JT, 1, a.rows[S_W], a.entries[S_W],
@@ -174,61 +300,77 @@ __global__ void __launch_bounds__(256) k_extract(ExtractArgs a) {
             }
             break;
         }
-        case S_WT: {
+        case X_WT: {
             const float* src = a.W + b * wblk;
-            extract_rows<JT>(nb, nb, n0, n0, (long long)b * nmax * nmax, nmax, src, nullptr, JT,
-                             (long long)nmax * JT, 1, a.rows[S_WT], a.entries[S_WT],
+            extract_cols<JT>(nb, nb, n0, n0, (long long)b * nmax * nmax, nmax, src, nullptr,
+                             (long long)nmax * JT, 1, a.rows[S_WT], a.entries[S_WT], a.entry_stride_w);
+            break;
+        }
+        case X_WL0:
+        case X_WL1: {
+            const float* src = a.WL + b * lblk;
+            extract_rows<JT>(eb, eb, e0, e0, (long long)b * emax * emax, emax, src, nullptr,
+                             (long long)emax * JT, JT, 1, a.rows[S_WL], a.entries[S_WL],
+                             a.entry_stride_w, slot - X_WL0, 2);
+            break;
+        }
+        case X_VALID: {
+            if (!a.validate) break;
+            validate_block(a.WL + b * lblk, emax, emax, JT, eb, eb, a.meta.err);
+            validate_mask(a.mask_lg + (long long)b * emax * emax, emax, eb, a.meta.err);
+            validate_block(a.Pm + b * pblk, nmax, emax, 1, nb, eb, a.meta.err);
+            validate_block(a.Pd + b * pblk, nmax, emax, 1, nb, eb, a.meta.err);
+            break;
+        }
+        case X_WLT: {
+            const float* src = a.WL + b * lblk;
+            extract_cols<JT>(eb, eb, e0, e0, (long long)b * emax * emax, emax, src, nullptr,
+                             (long long)emax * JT, 1, a.rows[S_WLT], a.entries[S_WLT],
                              a.entry_stride_w);
             break;
         }
-        default: {
-            const int emax = a.emax;
-            const int e0 = a.meta.edge_off[b];
-            const int eb = a.meta.edge_off[b + 1] - e0;
-            const long long lblk = (long long)emax * emax * JT;
-            const long long pblk = (long long)nmax * emax;
-            if (kind == S_WL) {
-                const float* src = a.WL + b * lblk;
-                extract_rows<JT>(eb, eb, e0, e0, (long long)b * emax * emax, emax, src, nullptr,
-                                 (long long)emax * JT, JT, 1, a.rows[S_WL], a.entries[S_WL],
-                                 a.entry_stride_w);
-                if (a.validate) {
-                    validate_block(src, emax, emax, JT, eb, eb, a.meta.err);
-                    validate_mask(a.mask_lg + (long long)b * emax * emax, emax, eb, a.meta.err);
-                }
-            } else if (kind == S_WLT) {
-                const float* src = a.WL + b * lblk;
-                extract_rows<JT>(eb, eb, e0, e0, (long long)b * emax * emax, emax, src, nullptr,
-                                 JT, (long long)emax * JT, 1, a.rows[S_WLT], a.entries[S_WLT],
-                                 a.entry_stride_w);
-            } else if (kind == S_PN) {
-                const float* pm = a.Pm + b * pblk;
-                const float* pd = a.Pd + b * pblk;
-                extract_rows<2>(nb, eb, n0, e0, (long long)b * nmax * emax, emax, pm, pd, emax,
-                                1, 0, a.rows[S_PN], a.entries[S_PN], 4);
-                if (a.validate) {
-                    validate_block(pm, nmax, emax, 1, nb, eb, a.meta.err);
-                    validate_block(pd, nmax, emax, 1, nb, eb, a.meta.err);
-                }
-            } else {  // S_PE
-                const float* pm = a.Pm + b * pblk;
-                const float* pd = a.Pd + b * pblk;
-                extract_rows<2>(eb, nb, e0, n0, (long long)b * emax * nmax, nmax, pm, pd, 1,
-                                emax, 0, a.rows[S_PE], a.entries[S_PE], 4);
-            }
+        case X_PN: {
+            const float* pm = a.Pm + b * pblk;
+            const float* pd = a.Pd + b * pblk;
+            extract_rows<2>(nb, eb, n0, e0, (long long)b * nmax * emax, emax, pm, pd, emax,
+                            1, 0, a.rows[S_PN], a.entries[S_PN], 4);
+            break;
+        }
+        default: {  // X_PE
+            const float* pm = a.Pm + b * pblk;
+            const float* pd = a.Pd + b * pblk;
+            extract_cols<2>(eb, nb, e0, n0, (long long)b * emax * nmax, nmax, pm, pd, emax, 0,
+                            a.rows[S_PE], a.entries[S_PE], 4);
         }
     }
 }
 
-int launch_extract(const ExtractArgs& a, hipStream_t s) {
-    const dim3 grid(a.bs, a.dual ? S_COUNT : 2);
+static int extract_one(const ExtractArgs& a, dim3 grid, hipStream_t s) {
     switch (a.jtot) {
-        case 3: hipLaunchKernelGGL(k_extract<3>, grid, dim3(256), 0, s, a); break;
-        case 4: hipLaunchKernelGGL(k_extract<4>, grid, dim3(256), 0, s, a); break;
-        case 5: hipLaunchKernelGGL(k_extract<5>, grid, dim3(256), 0, s, a); break;
+        case 3: hipLaunchKernelGGL(k_extract<3>, grid, dim3(X_THREADS), 0, s, a); break;
+        case 4: hipLaunchKernelGGL(k_extract<4>, grid, dim3(X_THREADS), 0, s, a); break;
+        case 5: hipLaunchKernelGGL(k_extract<5>, grid, dim3(X_THREADS), 0, s, a); break;
         default: return 2;
     }
     HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+int launch_extract(const ExtractArgs& a, hipStream_t s) {
+    const int kinds = a.dual ? X_SLOTS : 2;
+    // HGNN_EXTRACT_SPLIT=1 (diagnostics): one launch per block slot, so a kernel trace times
+    // each slot
+    static const bool split = [] {
+        const char* e = getenv("HGNN_EXTRACT_SPLIT");
+        return e && e[0] == '1';
+    }();
+    if (!split) return extract_one(a, dim3(a.bs, kinds), s);
+    for (int k = 0; k < kinds; ++k) {
+        ExtractArgs b = a;
+        b.kind0 = k;
+        const int r = extract_one(b, dim3(a.bs, 1), s);
+        if (r) return r;
+    }
     return 0;
 }
 
