@@ -101,6 +101,8 @@ int launch_bn_apply(const float* y, const int* total_rows, int cap_rows, int c, 
 
 // ---------------------------------------------------------------- BN backward
 int bn_bwd_tiles(int cap_rows) { return ceil_div(cap_rows, 64); }
+constexpr int BN_GROUP = 16;  // tiles per first-level group of the last-arriver reduction
+int bn_bwd_groups(int cap_rows) { return ceil_div(bn_bwd_tiles(cap_rows), BN_GROUP); }
 
 // Per 64-row tile and channel: {sum g, sum g h, sum dz h, sum dz}, g = w dz, h = (y - mean) / std.
 __global__ void __launch_bounds__(256) k_bn_bwd_part(BnBwdArgs a) {
@@ -175,10 +177,78 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part(BnBwdArgs a) {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float& f4c(float4& v, int i) { return reinterpret_cast<float*>(&v)[i]; }
 
+// Last-arriver combine of the per-tile partials (replaces k_bn_bwd_fin): the last block of each
+// group of BN_GROUP tiles sums the group's partials in tile order (fp64), the last group sums
+// the groups in order -- deterministic, and one kernel boundary fewer per BN backward.
+// Hand-off (the counter form of the guide's publish/consume recipe; the XCDs' L2s are not
+// coherent): partials stored write-through (sc1), every storing wave drains its stores, the
+// block's barrier, one relaxed agent-scope ticket; the block drawing the last ticket takes one
+// agent-scope acquire before reading.  Counters are zeroed by the forward's memset and reset by
+// their last user.
+__device__ __forceinline__ void store_sc1(float* base, long long idx, float4 v) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r,
+                                           (int)(idx * 4), 0, 16);  // aux 16 = sc1 (write-through)
+}
+
+typedef __attribute__((address_space(1))) int gi32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+__device__ bool bn_bwd_ticket(int* cnt, int want) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (sc1 stores)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int t = __hip_atomic_fetch_add((gi32*)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == want - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    return last;
+}
+
+__device__ void bn_bwd_combine(const BnBwdArgs& a, int tile, int tiles) {
+    const int grp = tile / BN_GROUP, ngrp = ceil_div(tiles, BN_GROUP);
+    const int gsize = min(BN_GROUP, tiles - grp * BN_GROUP);
+    if (!bn_bwd_ticket(&a.cnt[1 + grp], gsize)) return;
+    const int n4 = a.c * 4;
+    // all of a column's loads in flight before the first add (clamped, selected after)
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+        float v[BN_GROUP];
+#pragma unroll
+        for (int k = 0; k < BN_GROUP; ++k)
+            v[k] = a.part[(long long)(grp * BN_GROUP + min(k, gsize - 1)) * n4 + i];
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < BN_GROUP; ++k) t += k < gsize ? (double)v[k] : 0.0;
+        __hip_atomic_store((gu64*)a.gpart + (long long)grp * n4 + i, __builtin_bit_cast(unsigned long long, t),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store((gi32*)&a.cnt[1 + grp], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!bn_bwd_ticket(&a.cnt[0], ngrp)) return;
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+        double t = 0.0;
+        for (int g0 = 0; g0 < ngrp; g0 += BN_GROUP) {
+            double v[BN_GROUP];
+#pragma unroll
+            for (int k = 0; k < BN_GROUP; ++k) v[k] = a.gpart[(long long)min(g0 + k, ngrp - 1) * n4 + i];
+#pragma unroll
+            for (int k = 0; k < BN_GROUP; ++k) t += g0 + k < ngrp ? v[k] : 0.0;
+        }
+        a.sums[i] = (float)t;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store((gi32*)&a.cnt[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
     const int tile = blockIdx.x;
     const int total = *a.total_rows;
     const int r0 = tile * 64;
+    if (a.cnt && total <= 0 && tile == 0)  // no rows: the statistics are zero (k_bn_bwd_fin's result)
+        for (int i = threadIdx.x; i < a.c * 4; i += blockDim.x) a.sums[i] = 0.f;
     if (r0 >= total) return;
     const int r1 = min(total, r0 + 64);
     const float wv = *a.w;
@@ -231,14 +301,18 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
     __syncthreads();
     for (int ch = threadIdx.x; ch < a.c; ch += 256) {
         const int l = ch >> 2, comp = ch & 3;
-        float* p = a.part + ((long long)tile * a.c + ch) * 4;
+        float4 t4;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             float t = 0.f;
             for (int q = 0; q < RG; ++q) t += f4c(red[j][q * L + l], comp);
-            p[j] = t;
+            f4c(t4, j) = t;
         }
+        const long long idx = ((long long)tile * a.c + ch) * 4;
+        if (a.cnt) store_sc1(a.part, idx, t4);  // handed to the combining block (bn_bwd_combine)
+        else *reinterpret_cast<float4*>(a.part + idx) = t4;
     }
+    if (a.cnt) bn_bwd_combine(a, tile, ceil_div(total, 64));
 }
 
 __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
@@ -420,13 +494,24 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     const int tiles = bn_bwd_tiles(a.cap_rows);
     const bool v4 = bn_vec4(a);
+    // the last-arriver combine only for small batches (<= 64 tiles): at the config-2 sizes (364 edge
+    // tiles) the combining tail cost more than the fin launch it saves (part4 + combine 29.6 us vs
+    // part4 + fin 24 us per launch, 311-314 K vs 313-321 K graphs/s)
+    const bool combine = v4 && a.cnt && a.gpart && tiles <= 64;
     if (tiles > 0) {
-        if (v4) hipLaunchKernelGGL(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
+        if (v4) {
+            BnBwdArgs b = a;
+            if (!combine) b.cnt = nullptr;
+            hipLaunchKernelGGL(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, b);
+        } else {
+            hipLaunchKernelGGL(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
+        }
     }
     HGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(a.c), dim3(256), 0, s, a);
-    HGNN_LAUNCH_CHECK();
+    if (!combine || tiles == 0) {
+        hipLaunchKernelGGL(k_bn_bwd_fin, dim3(a.c), dim3(256), 0, s, a);
+        HGNN_LAUNCH_CHECK();
+    }
     if (!apply) return 0;
     if (v4) hipLaunchKernelGGL(k_bn_bwd_apply4, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_bn_bwd_apply, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);

@@ -14,11 +14,101 @@
 // done with v_mfma_f32_32x32x2_f32 on 32x32 tiles of (n, m): one workgroup per
 // graph stages the graph's G and X rows in LDS (F in chunks), each wave owns a
 // few (n-tile, m-tile, j) items.
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace hgnn {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+// where only 3 items exist, left one wave per SIMD)
+// Staging of one FC-wide chunk: every load is an unconditional buffer load (out-of-range
+// elements get an out-of-bounds offset and read 0), the padded-row values (readout vector, BN of
+// zero) come from per-chunk LDS constants afterwards.  Loads under per-lane conditions made hipcc
+// wait vmcnt(0) after each one: 132 full waits per launch, ~20 us per launch for ~4 us of work.
+template <int FC, int V>
+__device__ __forceinline__ void dw_stage(const DwDenseArgs& a, int b, int off, int nb, int npad, int f0, int fc,
+                                         float* Gs, float* Xs, int GP, const float* Rs, const float* Bmu,
+                                         const float* Bsc, const float* Bz) {
+    typedef typename std::conditional<V == 4, float4, float>::type vt;
+    constexpr unsigned OOB = 0x7ffffff0u;
+    constexpr int XP = FC + 1;
+    constexpr int FV = FC / V;
+    const int J = a.jt, F = a.f, nmax = a.nmax;
+    // wave-uniform descriptor inputs (readfirstlane): a descriptor the compiler cannot prove uniform
+    // becomes a waterfall loop around every buffer load
+    const int total = __builtin_amdgcn_readfirstlane(a.node_off[a.bs]);
+    const auto rg = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.dA), 0,
+        __builtin_amdgcn_readfirstlane((int)min((long long)total * a.lda * 4, (long long)OOB)), 0x00020000);
+    const uintptr_t xs = reinterpret_cast<uintptr_t>(a.xdense ? a.xdense : a.xp);
+    const uintptr_t xsu = ((uintptr_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(xs >> 32)) << 32) |
+                          (unsigned)__builtin_amdgcn_readfirstlane((int)(xs & 0xffffffffu));
+    const long long xbytes = a.xdense ? (long long)a.bs * F * nmax * 4 : (long long)total * F * 4;
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>(xsu), 0,
+                                                      __builtin_amdgcn_readfirstlane((int)min(xbytes, (long long)OOB)),
+                                                      0x00020000);
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, unsigned o) -> vt {
+        if constexpr (V == 4) return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)o, 0, 0));
+        else return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)o, 0, 0));
+    };
+    auto el = [](vt& v, int q) -> float& { return reinterpret_cast<float*>(&v)[q]; };
+    const int g_n = npad * J * FV, x_n = npad * FV;
+    constexpr int U = 8;
+    // G rows (the dA slices): all U loads of a round issued before any is used, offsets by select
+    for (int base = 0; base < g_n; base += 256 * U) {
+        vt v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + u * 256 + threadIdx.x;
+            const int n = i / (J * FV), rem = i - n * (J * FV), j = rem / FV, f = (rem % FV) * V;
+            const bool live = i < g_n && n < nb && f < fc;
+            v[u] = ld(rg, live ? (unsigned)((long long)(off + n) * a.lda + j * F + f0 + f) * 4u : OOB);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + u * 256 + threadIdx.x;
+            const int n = i / (J * FV), rem = i - n * (J * FV), j = rem / FV, f = (rem % FV) * V;
+            if (i < g_n) {
+                const bool pad_row = Rs != nullptr && n >= nb && n < nmax;
+                float* d = Gs + n * GP + j * FC + f;
+#pragma unroll
+                for (int q = 0; q < V; ++q) {
+                    const float rv = (pad_row && f + q < fc) ? Rs[j * FC + f + q] : 0.f;
+                    d[q] = pad_row ? rv : el(v[u], q);
+                }
+            }
+        }
+    }
+    // X rows (the layer input): BN on load, the BN of 0 at padded rows
+    for (int base = 0; base < x_n; base += 256 * U) {
+        vt v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int ix = base + u * 256 + threadIdx.x;
+            const int m = ix / FV, f = (ix % FV) * V;
+            unsigned o = OOB;
+            if (a.xdense) o = (ix < x_n && f < fc && m < nmax) ? (unsigned)(((long long)b * F + f0 + f) * nmax + m) * 4u : OOB;
+            else o = (ix < x_n && f < fc && m < nb) ? (unsigned)((long long)(off + m) * F + f0 + f) * 4u : OOB;
+            v[u] = ld(rx, o);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int ix = base + u * 256 + threadIdx.x;
+            const int m = ix / FV, f = (ix % FV) * V;
+            if (ix < x_n) {
+                float* d = Xs + m * XP + f;
+#pragma unroll
+                for (int q = 0; q < V; ++q) {
+                    float x = el(v[u], q);
+                    if (Bmu != nullptr && !a.xdense && f + q < fc)
+                        x = m < nb ? bn_z_s(x, Bmu[f + q], Bsc[f + q], *a.pb) : (m < nmax ? Bz[f + q] : 0.f);
+                    d[q] = x;
+                }
+            }
+        }
+    }
+}
 
 // MAXI = (n-tile, m-tile, slice) items per wave kept in registers: sized to the
 // graph so the accumulators do not cap occupancy (5 x 16 AGPRs at Nmax <= 32,
@@ -35,6 +125,10 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     const int GP = J * FC + 1;
     float* Gs = smem;               // [npad][GP]
     float* Xs = smem + npad * GP;   // [npad][XP]
+    float* Rs = Xs + npad * XP;     // [J * FC] readout vector of the chunk
+    float* Bmu = Rs + J * FC;       // [FC] BN mean, scale, and the BN of 0 (padded rows)
+    float* Bsc = Bmu + FC;
+    float* Bz = Bsc + FC;
     const int off = a.node_off[b];
     const int nb = a.node_off[b + 1] - off;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -55,133 +149,30 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     for (int f0 = 0; f0 < F; f0 += FC) {
         const int fc = min(FC, F - f0);
         __syncthreads();
-        // Staging issues U independent loads per thread before touching LDS: the
-        // element-at-a-time loop was bound by one load latency per element.
-        constexpr int U = 8;
-        if (vec) {
-            // G rows (dA slices) and X rows share one index space, so every load of the
-            // chunk is in flight before the first LDS write
-            constexpr int F4 = FC / 4;
-            const int g4 = npad * J * F4;
-            const int t4 = g4 + npad * F4;
-            for (int base = 0; base < t4; base += 256 * U) {
-                float4 v[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int i = base + u * 256 + threadIdx.x;
-                    v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (i < g4) {
-                        const int n = i / (J * F4), j = (i / F4) % J, f = (i % F4) * 4;
-                        if (f < fc && n < nmax) {
-                            const int k = j * F + f0 + f;
-                            if (n < nb) {
-                                v[u] = *reinterpret_cast<const float4*>(a.dA + (long long)(off + n) * a.lda + k);
-                            } else if (a.dout) {
-                                for (int o = 0; o < a.dim_out; ++o) {
-                                    const float d = a.dout[b * a.dim_out + o];
-                                    const float* w = a.fcw + (long long)o * a.kfc + k;
-                                    v[u].x = fmaf(d, w[0], v[u].x);
-                                    v[u].y = fmaf(d, w[1], v[u].y);
-                                    v[u].z = fmaf(d, w[2], v[u].z);
-                                    v[u].w = fmaf(d, w[3], v[u].w);
-                                }
-                            }
-                        }
-                    } else if (i < t4) {
-                        const int ix = i - g4;
-                        const int m = ix / F4, f = (ix % F4) * 4;
-                        if (f < fc && m < nmax) {
-                            const int c = f0 + f;
-                            if (m < nb) {
-                                v[u] = *reinterpret_cast<const float4*>(a.xp + (long long)(off + m) * F + c);
-                                if (a.pmean) {
-                                    v[u].x = bn_z(v[u].x, a.pmean[c], a.pstd[c], *a.pw, *a.pb);
-                                    v[u].y = bn_z(v[u].y, a.pmean[c + 1], a.pstd[c + 1], *a.pw, *a.pb);
-                                    v[u].z = bn_z(v[u].z, a.pmean[c + 2], a.pstd[c + 2], *a.pw, *a.pb);
-                                    v[u].w = bn_z(v[u].w, a.pmean[c + 3], a.pstd[c + 3], *a.pw, *a.pb);
-                                }
-                            } else if (a.pmean) {
-                                float t[4];
-#pragma unroll
-                                for (int q = 0; q < 4; ++q) {
-                                    t[q] = bn_z(0.f, a.pmean[c + q], a.pstd[c + q], *a.pw, *a.pb);
-                                }
-                                v[u] = make_float4(t[0], t[1], t[2], t[3]);
-                            }
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int i = base + u * 256 + threadIdx.x;
-                    float* d = nullptr;
-                    if (i < g4) {
-                        const int n = i / (J * F4), j = (i / F4) % J, f = (i % F4) * 4;
-                        d = Gs + n * GP + j * FC + f;
-                    } else if (i < t4) {
-                        const int ix = i - g4;
-                        d = Xs + (ix / F4) * XP + (ix % F4) * 4;
-                    }
-                    if (d) {
-                        d[0] = v[u].x;
-                        d[1] = v[u].y;
-                        d[2] = v[u].z;
-                        d[3] = v[u].w;
-                    }
-                }
+        // per-chunk constants: readout vector sum_o dout[b, o] fcw[o, j F + f0 + f], BN of the input
+        if (a.dout)
+            for (int t = threadIdx.x; t < J * FC; t += 256) {
+                const int j = t / FC, f = t % FC;
+                float r = 0.f;
+                if (f < fc)
+                    for (int o = 0; o < a.dim_out; ++o)
+                        r = fmaf(a.dout[b * a.dim_out + o], a.fcw[(long long)o * a.kfc + j * F + f0 + f], r);
+                Rs[t] = r;
             }
-        } else {
-            const int gn = npad * J * FC;
-            for (int base = 0; base < gn; base += 256 * U) {
-                float v[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int i = base + u * 256 + threadIdx.x;
-                    v[u] = 0.f;
-                    const int n = i / (J * FC), j = (i / FC) % J, f = i % FC;
-                    if (i < gn && f < fc && n < nmax) {
-                        const int k = j * F + f0 + f;
-                        if (n < nb) {
-                            v[u] = a.dA[(long long)(off + n) * a.lda + k];
-                        } else if (a.dout) {
-                            for (int o = 0; o < a.dim_out; ++o)
-                                v[u] = fmaf(a.dout[b * a.dim_out + o], a.fcw[(long long)o * a.kfc + k], v[u]);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int i = base + u * 256 + threadIdx.x;
-                    if (i < gn) Gs[(i / (J * FC)) * GP + ((i / FC) % J) * FC + i % FC] = v[u];
-                }
+        if (a.pmean)
+            for (int t = threadIdx.x; t < FC; t += 256) {
+                const int c = f0 + min(t, fc - 1);
+                Bmu[t] = a.pmean[c];
+                Bsc[t] = bn_scale(*a.pw, a.pstd[c]);
+                Bz[t] = bn_z(0.f, a.pmean[c], a.pstd[c], *a.pw, *a.pb);
             }
-            const int xn = npad * FC;
-            for (int base = 0; base < xn; base += 256 * U) {
-                float v[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int i = base + u * 256 + threadIdx.x;
-                    v[u] = 0.f;
-                    const int m = i / FC, f = i % FC;
-                    if (i < xn && f < fc && m < nmax) {
-                        const int c = f0 + f;
-                        if (a.xdense) {
-                            v[u] = a.xdense[((long long)b * F + c) * nmax + m];
-                        } else if (m < nb) {
-                            v[u] = a.xp[(long long)(off + m) * F + c];
-                            if (a.pmean) v[u] = bn_z(v[u], a.pmean[c], a.pstd[c], *a.pw, *a.pb);
-                        } else if (a.pmean) {
-                            v[u] = bn_z(0.f, a.pmean[c], a.pstd[c], *a.pw, *a.pb);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int i = base + u * 256 + threadIdx.x;
-                    if (i < xn) Xs[(i / FC) * XP + i % FC] = v[u];
-                }
-            }
-        }
+        __syncthreads();
+        if (vec)
+            dw_stage<FC, 4>(a, b, off, nb, npad, f0, fc, Gs, Xs, GP, a.dout ? Rs : nullptr,
+                            a.pmean ? Bmu : nullptr, Bsc, Bz);
+        else
+            dw_stage<FC, 1>(a, b, off, nb, npad, f0, fc, Gs, Xs, GP, a.dout ? Rs : nullptr,
+                            a.pmean ? Bmu : nullptr, Bsc, Bz);
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < MAXI; ++q) {
@@ -204,12 +195,16 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
         const int m = tm * 32 + l31;
         // read all 16 previous values before any store: a load-add-store per element
         // is serialised by the compiler (possible aliasing) into 16 memory round trips
+        // (clamped unconditional loads, selected after: see dw_stage)
         float old[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int n = tn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            old[r] = (a.accumulate && n < nmax && m < nmax) ? dWb[((long long)n * nmax + m) * J + j] : 0.f;
+            const int n = min(tn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, nmax - 1);
+            old[r] = dWb[((long long)n * nmax + min(m, nmax - 1)) * J + j];
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (!a.accumulate) old[r] = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int n = tn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -229,7 +224,7 @@ static void launch_fc(const DwDenseArgs& a, int maxi, int gy, size_t lds, hipStr
 int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
     const int npad = (a.nmax + 31) / 32 * 32;
     const int fc = npad <= 32 ? 64 : (npad <= 64 ? 32 : 16);
-    const size_t lds = sizeof(float) * (size_t)npad * ((a.jt * fc + 1) + (fc + 1));
+    const size_t lds = sizeof(float) * ((size_t)npad * ((a.jt * fc + 1) + (fc + 1)) + (size_t)a.jt * fc + 3 * fc);
     if (lds > 64 * 1024) return 2;
     const int tiles = npad / 32;
     const int nitems = tiles * tiles * a.jt;
