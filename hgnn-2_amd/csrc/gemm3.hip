@@ -9,7 +9,7 @@
 // MFMA step s contracts k = s (lanes 0-31) and k = BK/2 + s (lanes 32-63); the
 // same permutation on A and B leaves the sum unchanged, and one ds_read_b128
 // per operand then feeds 4 consecutive MFMA steps.  Measured on the box
-// (tools/gemm_lab.hip) against v2 on the config-2 shapes: node fwd 57 -> 30 us,
+// (the round-1 GEMM lab; tools/gemm4_lab.hip is the current one) against v2 on the config-2 shapes: node fwd 57 -> 30 us,
 // edge fwd 79 -> 51 us, edge dA 64 -> 48 us.
 #include "kernels.h"
 
@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
     // loads' range checks are the only masking (the forward GEMM runs over the padded width kp,
     // whose padding columns are zero in both operands).  A per-element tail select in the
     // staging doubled the k-loop's instruction count (321 vs 204 per k-step) and cost ~5 us
-    // per launch (tools/gemm_lab.hip).
+    // per launch (round-1 GEMM lab).
     float4 ra[AF4], rb[BF4];
     float4 rz[EPI == E3_DA_BN ? AF4 : 1];
     // E3_DA_BN: per-channel affine form of the BN backward, dY = ca dz + cb (y - mu) + ce
@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
 // B = the saved aggregate [R][kp].  Both operands are reduction-major, so LDS keeps
 // the natural [k][m] image (float4 copies) and fragments are ds_read_b32, with the
 // same k permutation and a one-step register prefetch of the next fragments.
-// Measured (tools/gemm_lab.hip, config-2 shapes): edge 78 -> 41 us, node 37.5 -> 21 us vs v2.
+// Measured (round-1 GEMM lab, config-2 shapes): edge 78 -> 41 us, node 37.5 -> 21 us vs v2.
 template <int BM, int BN, int BK, int WGM, int WGN>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __restrict__ A, int lda,
                                                              const float* __restrict__ B, int ldb,
@@ -563,7 +563,7 @@ int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int
     p.relu_from = relu_from;
     p.bn_part = bn_part;
     if (n <= 128) {
-        // 64-column tiles up to 2d = 128: twice the blocks of 64 x 128 tiles, measured (tools/gemm_lab.hip)
+        // 64-column tiles up to 2d = 128: twice the blocks of 64 x 128 tiles, measured (round-1 GEMM lab)
         // edge forward 47.7 -> 40.7 us, node forward 34 -> 28 us
         hipLaunchKernelGGL((k_gemm3<64, 64, 32, 2, 2, E3_FWD>), dim3(ceil_div(m_cap, 64), ceil_div(n, 64)), dim3(256),
                            0, s, p);
