@@ -206,10 +206,40 @@ def run_ccn(name, order, graphs, desc, steps, warmup, graph=False):
         name += "g"
         desc += ", plan built once, step replayed from a HIP graph"
     deg = (A > 0).sum(-1).double()
+    sd, sd2, sd3 = float(deg.sum()), float((deg ** 2).sum()), float((deg ** 3).sum())
     return dict(config=name, workload=desc, graphs_per_step=len(graphs), ms_per_step=round(sec * 1e3, 4),
                 value=round(len(graphs) / sec, 2), unit="graphs/s", dtype="fp32",
-                sum_d=int(deg.sum()), sum_d2=int((deg ** 2).sum()), sum_d3=int((deg ** 3).sum()),
-                d_max=int(deg.max()))
+                sum_d=int(sd), sum_d2=int(sd2), sum_d3=int(sd3), d_max=int(deg.max()),
+                roofline=ccn_roofline(order, net, sd, sd2, sd3, sec))
+
+
+def ccn_roofline(order, net, sd, sd2, sd3, sec, bw=8.0e12, peak=157.3e12):
+    """SURVEY.md §8 d CCN formulas over the step's batch (Σd, Σd², Σd³ with the self loop):
+    per layer, CCN-1D bytes 4(Σd·C_in + Σd·h + Σd²), FLOPs 2Σd²·C + 4Σd·C·h; CCN-2D bytes
+    4(Σd²·C_in + Σd²·h + Σd²), FLOPs 2Σd³·C + 36Σd²·C·h (gathered bytes 4Σd³·C reported apart);
+    fwd+bwd = 3x the forward."""
+    c_in, h, layers = net.input_feats, net.hidden_size, net.layers
+    cs = [c_in] + [h] * (layers - 1)
+    byt = flo = gath = 0.0
+    for c in cs:
+        if order == 1:
+            byt += 4 * (sd * c + sd * h + sd2)
+            flo += 2 * sd2 * c + 4 * sd * c * h
+        else:
+            byt += 4 * (sd2 * c + sd2 * h + sd2)
+            flo += 2 * sd3 * c + 36 * sd2 * c * h
+            gath += 4 * sd3 * c
+    byt, flo, gath = 3 * byt, 3 * flo, 3 * gath
+    t_hbm, t_mfma = byt / bw, flo / peak
+    out = dict(bound="hbm" if t_hbm >= t_mfma else "mfma", bytes_per_step=byt, flops_per_step=flo,
+               achieved_gbs=round(byt / sec / 1e9, 3), frac_hbm=round(byt / sec / bw, 5),
+               achieved_tflops=round(flo / sec / 1e12, 4), frac_mfma=round(flo / sec / peak, 5),
+               frac_roofline=round(max(t_hbm, t_mfma) / sec, 5),
+               formula="SURVEY.md §8 d, fwd+bwd = 3x forward")
+    if order == 2:
+        out["gathered_bytes_per_step"] = gath
+        out["gathered_gbs"] = round(gath / sec / 1e9, 3)
+    return out
 
 
 def main():
