@@ -5,15 +5,19 @@ One step = one training pass of the drop-in GNN_lg (order 2, the reference's
 `--update 2`) over a batch of 512 synthetic QM9-shape graphs already resident
 in HBM: dense padded inputs as prepare_batch returns them, forward, MSE loss,
 backward (X and W require grad as in scripts/train_mnb.py:56-57), and with N>1
-GPUs the RCCL all-reduce of the gradient bucket (batch-axis data parallelism,
-512 graphs per GPU: weak scaling).
+GPUs the RCCL all-reduce of the gradients (batch-axis data parallelism, weak
+scaling: each rank takes its Σ(N+M)-balanced shard of a global batch of 512·N
+graphs, hgnn_amd.dp.shard_graphs; per-layer gradient buckets are all-reduced on a
+communication stream while the earlier layers' backward still runs, and the BN
+running statistics are averaged, hgnn_amd.dp.LayerBucketAllReduce).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 Prints ONE JSON line (rank 0) with the BASELINE metric, a live roofline of the
 dominant kernel class and HBM rooflines of the two aggregation classes (HIP
-events around their launches in a second timed region of the same steps), and
-the oracle's CPU time on a bounded sample (rank 0, N=1 only).
+events around their launches in a second timed region of the same steps), a
+forward-only line (roofline_fwd), and the oracle's CPU time on a bounded sample
+with the parity check of the GPU step against it (rank 0, N=1 only).
 """
 
 import argparse
