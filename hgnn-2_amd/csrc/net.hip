@@ -284,6 +284,25 @@ Program build_program(const hgnn_net_config* c) {
     return P;
 }
 
+// Program of a configuration, cached per host thread: built four times per training step
+// otherwise (workspace query, forward, error word, backward), vectors included.
+const Program& program_of(const hgnn_net_config* c) {
+    struct Entry {
+        int key[11];
+        Program P;
+    };
+    thread_local std::vector<Entry> cache;
+    const int key[11] = {c->kind, c->order, c->bs, c->nmax, c->emax, c->f_in, c->d, c->n_layers, c->j_tot,
+                         c->dim_out, c->training};
+    for (const Entry& e : cache)
+        if (memcmp(e.key, key, sizeof(key)) == 0) return e.P;
+    if (cache.size() >= 16) cache.erase(cache.begin());
+    cache.push_back(Entry{});
+    memcpy(cache.back().key, key, sizeof(key));
+    cache.back().P = build_program(c);
+    return cache.back().P;
+}
+
 // The GEMMs address each operand through a 32-bit buffer resource: every operand the
 // program hands them must stay under 2 GB (checked before anything is enqueued).
 bool fits_32bit(const Program& P) {
@@ -463,7 +482,7 @@ static bool split_agg_enabled() {
 
 int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
                 const float* const* prm, float* const* run, void* ws, float* out, hipStream_t s, Timer* tm) {
-    const Program P = build_program(c);
+    const Program& P = program_of(c);
     if (!fits_32bit(P)) return HGNN_ERR_UNSUPPORTED;
     const bool lg = c->kind == 1;
     const Src src = make_src(P, ws, csr);
@@ -751,7 +770,7 @@ static bool fused_da_enabled() {
 int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
                  const float* const* prm, void* ws, const float* dout, float* const* grads, float* dX, float* dW,
                  hipStream_t s, Timer* tm, void* const* ev = nullptr, int n_ev = 0) {
-    const Program P = build_program(c);
+    const Program& P = program_of(c);
     if (!fits_32bit(P)) return HGNN_ERR_UNSUPPORTED;
     const Src src = make_src(P, ws, csr);
     BatchMeta m = src.m;
@@ -1125,13 +1144,13 @@ int hgnn_net_bn_count(const hgnn_net_config* cfg) {
 
 size_t hgnn_net_workspace_bytes(const hgnn_net_config* cfg) {
     if (!valid_config(cfg)) return 0;
-    const Program P = build_program(cfg);
+    const Program& P = program_of(cfg);
     return fits_32bit(P) ? P.bytes : 0;
 }
 
 uint32_t* hgnn_net_error_word(const hgnn_net_config* cfg, void* workspace) {
     if (!valid_config(cfg) || !workspace) return nullptr;
-    return at<uint32_t>(workspace, build_program(cfg).err);
+    return at<uint32_t>(workspace, program_of(cfg).err);
 }
 
 int hgnn_net_forward(const hgnn_net_config* cfg, const hgnn_net_inputs* in, const float* const* params,

@@ -65,17 +65,49 @@ def _raise_bits(bits):
     raise RuntimeError("hgnn_amd: invalid input batch: " + L.deverr_message(bits))
 
 
+class _ErrorRing:
+    """Pinned host slots the forwards' device error words are copied into asynchronously: a
+    check reads a slot only once its copy's event has completed, so it never synchronises the
+    stream (reading a device tensor with .item() waited for everything enqueued before it -- the
+    host could then not run ahead of the GPU, 0.4 ms per step at config 2)."""
+
+    SLOTS = 256
+
+    def __init__(self):
+        self.host = torch.zeros(self.SLOTS, dtype=torch.int32, pin_memory=True)
+        self.next = 0
+
+    def take(self):
+        i = self.next
+        self.next = (i + 1) % self.SLOTS
+        for k, (ev, slot) in enumerate(_pending):  # a slot still in flight: retire its check first
+            if slot == i:
+                ev.synchronize()
+                bits = int(self.host[slot])
+                del _pending[k]
+                if bits:
+                    _pending.clear()
+                    _raise_bits(bits)
+                break
+        return i
+
+
+_ring = None
+
+
 def check_errors(block=True):
     """Raise if any enqueued forward found an invalid input batch."""
     if _capturing():
         return
     keep = []
     bad = 0
-    for ev, err in _pending:
+    for ev, slot in _pending:
+        if block:
+            ev.synchronize()
         if block or ev.query():
-            bad |= int(err.item())
+            bad |= int(_ring.host[slot])
         else:
-            keep.append((ev, err))
+            keep.append((ev, slot))
     _pending[:] = keep
     if bad:
         _pending.clear()
@@ -91,18 +123,23 @@ def _watch_error_word(cfg, ws):
         # inside a HIP graph capture (bench.py --graph): the batch was validated by the eager
         # warm-up steps; no host-visible check can be part of a replayed graph
         return
+    global _ring
     base = ws.data_ptr()
     addr = L.lib().hgnn_net_error_word(ctypes.byref(cfg), ctypes.c_void_p(base))
     off = int(addr) - base
-    err = ws[off:off + 4].view(torch.int32).clone()
+    err = ws[off:off + 4].view(torch.int32)
     if strict():
         v = int(err.item())
         if v:
             _raise_bits(v)
         return
+    if _ring is None:
+        _ring = _ErrorRing()
+    slot = _ring.take()
+    _ring.host[slot:slot + 1].copy_(err, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record()
-    _pending.append((ev, err))
+    _pending.append((ev, slot))
 
 
 def _require_cuda(tensors, what):
@@ -252,7 +289,10 @@ def _grad_targets(spec, params):
             v.shape == p.shape and v.device == p.device for v, p in zip(dp.views, params)):
         evs = (ctypes.c_void_p * max(1, len(dp.event_handles)))(*dp.event_handles)
         return list(dp.views), evs, len(dp.event_handles)
-    return [torch.empty_like(p) for p in params], None, 0
+    # one allocation for all of them (50 empty_like calls were ~0.1 ms of host time per step)
+    sizes = [p.numel() for p in params]
+    flat = torch.empty(sum(sizes), dtype=torch.float32, device=params[0].device)
+    return [v.view(p.shape) for v, p in zip(flat.split(sizes), params)], None, 0
 
 
 def run_net(spec, X, W, N_batch, mask, XL=None, WL=None, Pm=None, Pd=None, E_batch=None, mask_lg=None):

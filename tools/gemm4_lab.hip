@@ -163,6 +163,123 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_g4(const float* __restrict__
         }
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// The same pipeline on v_mfma_f32_16x16x4_f32: MI355X_MICROARCH.md (DVFS give-back, item 7) measures
+// the 16x16 MFMA shape holding a higher clock than the 32x32 one at equal cycles per FLOP.
+// Wave tile 32x32 = 2 x 2 tiles of 16x16; lane (l15, g = lane >> 4) reads 4 consecutive k of its
+// row (16-B slot hh * 4 + g of the 128-B row) and feeds element s to MFMA step s, so step s of half
+// hh contracts k = 16 hh + 4 g + s over the 4 lane groups -- the same permutation on A and B.
+template <int BM, int BN, int WGM, int WGN, int ST>
+__global__ void __launch_bounds__(64 * WGM * WGN) k_g5(const float* __restrict__ A, int lda,
+                                                       const float* __restrict__ B, int ldb, int M, int N, int K,
+                                                       float* __restrict__ C, int ldc) {
+    constexpr int BK = 32, NW = WGM * WGN;
+    constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 16, AN = TN / 16;
+    constexpr int AI = BM * BK * 4 / 1024, BI = BN * BK * 4 / 1024;
+    static_assert(AI % NW == 0 && BI % NW == 0, "staging split");
+    constexpr int APW = AI / NW, BPW = BI / NW, PER = APW + BPW;
+    constexpr int SF = (BM + BN) * BK;
+    __shared__ __attribute__((aligned(1024))) float lds[ST * SF];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wv / WGN, wn = wv % WGN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    if (m0 >= M) return;
+    constexpr unsigned OOB = 0x7ffffff0u;
+    const i32x4 ra = rsrc(A, M * lda * 4), rb = rsrc(B, N * ldb * 4);
+    const int lrow = lane >> 3, lslot = lane & 7;
+    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
+    auto issue = [&](int st, int k0) {
+        const unsigned base = lds0 + st * SF * 4;
+#pragma unroll
+        for (int i = 0; i < APW; ++i) {
+            const int inst = wv * APW + i, row = inst * 8 + lrow;
+            const int s = lslot ^ ((row >> 1) & 7), gm = m0 + row, gk = k0 + 4 * s;
+            const unsigned off = (gm < M && gk < K) ? (unsigned)(gm * lda + gk) * 4u : OOB;
+            dma16(ra, off, base + inst * 1024);
+        }
+#pragma unroll
+        for (int i = 0; i < BPW; ++i) {
+            const int inst = wv * BPW + i, row = inst * 8 + lrow;
+            const int s = lslot ^ ((row >> 1) & 7), gn = n0 + row, gk = k0 + 4 * s;
+            const unsigned off = (gn < N && gk < K) ? (unsigned)(gn * ldb + gk) * 4u : OOB;
+            dma16(rb, off, base + BM * BK * 4 + inst * 1024);
+        }
+    };
+    f32x4 acc[AM][AN], tacc[AM][AN];
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+    const int nt = (K + BK - 1) / BK;
+    const int g = lane >> 4, l15 = lane & 15;
+#pragma unroll
+    for (int p = 0; p < ST - 1; ++p)
+        if (p < nt) issue(p, p * BK);
+    if (nt > 1) stage_barrier<(ST - 2) * PER>();
+    else stage_barrier<0>();
+    for (int t = 0; t < nt; ++t) {
+        if (t + ST - 1 < nt) issue((t + ST - 1) % ST, (t + ST - 1) * BK);
+        const float* as = lds + (t % ST) * SF;
+        const float* bs = as + BM * BK;
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int j = 0; j < AN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tacc[i][j][r] = 0.f;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            float4 a[AM], b[AN];
+#pragma unroll
+            for (int i = 0; i < AM; ++i) {
+                const int row = wm * TM + i * 16 + l15;
+                const int slot = (hh * 4 + g) ^ ((row >> 1) & 7);
+                a[i] = *reinterpret_cast<const float4*>(as + row * BK + 4 * slot);
+            }
+#pragma unroll
+            for (int j = 0; j < AN; ++j) {
+                const int row = wn * TN + j * 16 + l15;
+                const int slot = (hh * 4 + g) ^ ((row >> 1) & 7);
+                b[j] = *reinterpret_cast<const float4*>(bs + row * BK + 4 * slot);
+            }
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+#pragma unroll
+                for (int j = 0; j < AN; ++j) {
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[j].x, tacc[i][j], 0, 0, 0);
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b[j].y, tacc[i][j], 0, 0, 0);
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b[j].z, tacc[i][j], 0, 0, 0);
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b[j].w, tacc[i][j], 0, 0, 0);
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int j = 0; j < AN; ++j) acc[i][j] += tacc[i][j];
+        if constexpr (ST >= 3) {
+            if (t + ST - 1 < nt) stage_barrier<(ST - 2) * PER>();
+            else stage_barrier<0>();
+        } else {
+            stage_barrier<0>();
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j) {
+            const int gn = n0 + wn * TN + j * 16 + l15;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gm = m0 + wm * TM + i * 16 + 4 * g + r;
+                if (gm < M && gn < N) C[(long long)gm * ldc + gn] = acc[i][j][r];
+            }
+        }
+}
+
 __global__ void k_ref(const float* A, const float* B, float* C, int M, int N, int K) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (long long)M * N) return;
@@ -216,6 +333,20 @@ static void run_g4(const char* tag, const Shape& sh, const float* A, const float
            2.0 * sh.M * sh.N * sh.K / (us * 1e-6) / 1e12, maxerr(C, R, (long long)sh.M * sh.N));
 }
 
+template <int BM, int BN, int WGM, int WGN, int ST>
+static void run_g5(const char* tag, const Shape& sh, const float* A, const float* B, float* C, const float* R,
+                   hipStream_t s) {
+    CK(hipMemset(C, 0, (size_t)sh.M * sh.N * 4));
+    const dim3 g((sh.M + BM - 1) / BM, (sh.N + BN - 1) / BN);
+    auto f = [&]() {
+        hipLaunchKernelGGL((k_g5<BM, BN, WGM, WGN, ST>), g, dim3(64 * WGM * WGN), 0, s, A, sh.K, B, sh.K, sh.M, sh.N,
+                           sh.K, C, sh.N);
+    };
+    const double us = timeit(f, s);
+    printf("%-9s %-34s blocks=%5d %7.1f us %6.1f TF/s err=%.2e\n", sh.name, tag, g.x * g.y, us,
+           2.0 * sh.M * sh.N * sh.K / (us * 1e-6) / 1e12, maxerr(C, R, (long long)sh.M * sh.N));
+}
+
 int main() {
     hipStream_t s;
     CK(hipStreamCreate(&s));
@@ -261,9 +392,25 @@ int main() {
         run_g4<64, 64, 2, 2, 2>("g4<64,64,2x2> 2st", sh, A, B, C, R, s);
         run_g4<64, 64, 2, 2, 2, 1>("g4<64,64,2x2> 2st PROBE mfma+lds", sh, A, B, C, R, s);
         run_g4<64, 64, 2, 2, 2, 2>("g4<64,64,2x2> 2st PROBE staging", sh, A, B, C, R, s);
+        if (sh.N > 128) {  // the library's dA kernel on 64 x 64 tiles
+            CK(hipMemset(C, 0, nc * 4));
+            G3 p{};
+            p.a = A; p.lda = sh.K; p.b = B; p.ldb = sh.K; p.m_cap = sh.M; p.m_valid = mv; p.k = sh.K; p.n = sh.N;
+            p.c = C; p.ldc = sh.N;
+            auto f = [&]() {
+                hipLaunchKernelGGL((k_gemm3<64, 64, 32, 2, 2, E3_STORE>), dim3((sh.M + 63) / 64, (sh.N + 63) / 64),
+                                   dim3(256), 0, s, p);
+            };
+            const double us = timeit(f, s);
+            printf("%-9s %-34s              %7.1f us %6.1f TF/s err=%.2e\n", sh.name, "lib k_gemm3<64,64> E3_STORE", us,
+                   2.0 * sh.M * sh.N * sh.K / (us * 1e-6) / 1e12, maxerr(C, R, nc));
+        }
+        run_g5<64, 64, 2, 2, 2>("g5 16x16x4 <64,64,2x2> 2st", sh, A, B, C, R, s);
+        run_g5<64, 64, 2, 2, 3>("g5 16x16x4 <64,64,2x2> 3st", sh, A, B, C, R, s);
+        run_g5<32, 64, 1, 2, 2>("g5 16x16x4 <32,64,1x2> 2st", sh, A, B, C, R, s);
+        run_g5<64, 128, 2, 2, 2>("g5 16x16x4 <64,128,2x2> 2st", sh, A, B, C, R, s);
         run_g4<64, 128, 2, 2, 2>("g4<64,128,2x2> 2st", sh, A, B, C, R, s);
-        run_g4<64, 128, 2, 2, 2, 1>("g4<64,128,2x2> 2st PROBE mfma+lds", sh, A, B, C, R, s);
-        run_g4<128, 128, 2, 2, 2, 1>("g4<128,128,2x2> 2st PROBE mfma+lds", sh, A, B, C, R, s);
+
         CK(hipFree(A));
         CK(hipFree(B));
         CK(hipFree(C));
