@@ -11,6 +11,8 @@
 // per operand then feeds 4 consecutive MFMA steps.  Measured on the box
 // (the round-1 GEMM lab; tools/gemm4_lab.hip is the current one) against v2 on the config-2 shapes: node fwd 57 -> 30 us,
 // edge fwd 79 -> 51 us, edge dA 64 -> 48 us.
+#include <stdlib.h>
+
 #include "kernels.h"
 
 namespace hgnn {
@@ -465,6 +467,154 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
         }
 }
 
+// ---- dA on v_mfma_f32_16x16x4_f32 with LDS-DMA staging (tools/gemm4_lab.hip, "g5")
+// C[M][N] = A[M][K] . B[N][K]^T, both k-contiguous, plain store.  Each stage of BK = 32 k is
+// filled by buffer_load ... lds (16 B per lane, 1 KB per wave instruction, rows of 128 B with the
+// 16-B slots XOR-swizzled by (row >> 1) & 7 so the fragment reads are conflict-free) and consumed
+// after a counted vmcnt + s_barrier; lane (l15, g) reads 4 consecutive k of its row and step s of
+// half hh contracts k = 16 hh + 4 g + s (same permutation on A and B).  Measured on the config-2
+// dA shapes: edge 50.2 -> 47.5 us, node 23.8 -> 21.1 us against k_gemm3<64,128,...,E3_STORE>; step
+// 338-339 K -> 342-345 K graphs/s.  Not used for the forward: the 16x16 MFMA's different k order
+// put GNN_simple's 20-layer fixture output 1.2e-5 relative from the reference (bound 1e-5), against
+// k_gemm3's inside it, for ~10 us per step.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x4 rsrc4(const void* p, int bytes) {
+    const unsigned long long a = (unsigned long long)(uintptr_t)p;
+    i32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
+    r.y = __builtin_amdgcn_readfirstlane((int)(a >> 32) & 0xffff);
+    r.z = __builtin_amdgcn_readfirstlane(bytes);
+    r.w = 0x00020000;
+    return r;
+}
+
+// 16 B per lane, global -> LDS at the wave-uniform LDS byte address + lane * 16.  Inline asm keeps
+// the load out of hipcc's waitcnt bookkeeping (a builtin form made it wait vmcnt(0) before every
+// LDS read); the kernel counts it with its own vmcnt.
+__device__ __forceinline__ void dma16(i32x4 r, unsigned voff, unsigned lds_addr) {
+    int keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(r), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+        : "memory");
+}
+
+// vmcnt(n) + lgkmcnt(0) + s_barrier in one statement (a compiler memory barrier too)
+template <int N>
+__device__ __forceinline__ void stage_barrier() {
+    static_assert(N >= 0 && N < 16, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ void __launch_bounds__(64 * WGM * WGN) k_gemm5(const float* __restrict__ A, int lda,
+                                                          const float* __restrict__ B, int ldb,
+                                                          const int* __restrict__ m_valid, int m_cap, int N, int K,
+                                                          float* __restrict__ C, int ldc) {
+    constexpr int BK = 32, NW = WGM * WGN, ST = 2;
+    constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 16, AN = TN / 16;
+    constexpr int AI = BM * BK * 4 / 1024, BI = BN * BK * 4 / 1024;  // 1-KB wave instructions per stage
+    static_assert(AI % NW == 0 && BI % NW == 0, "staging split");
+    constexpr int APW = AI / NW, BPW = BI / NW;
+    constexpr int SF = (BM + BN) * BK;  // floats per stage
+    __shared__ __attribute__((aligned(1024))) float lds[ST * SF];
+    const int M = __builtin_amdgcn_readfirstlane(m_valid ? *m_valid : m_cap);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wv / WGN, wn = wv % WGN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    if (m0 >= M) return;
+    constexpr unsigned OOB = 0x7ffffff0u;
+    const i32x4 ra = rsrc4(A, M * lda * 4), rb = rsrc4(B, N * ldb * 4);
+    const int lrow = lane >> 3, lslot = lane & 7;
+    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
+    auto issue = [&](int st, int k0) {
+        const unsigned base = lds0 + st * SF * 4;
+#pragma unroll
+        for (int i = 0; i < APW; ++i) {
+            const int inst = wv * APW + i, row = inst * 8 + lrow;
+            const int sl = lslot ^ ((row >> 1) & 7), gm = m0 + row, gk = k0 + 4 * sl;
+            dma16(ra, (gm < M && gk < K) ? (unsigned)(gm * lda + gk) * 4u : OOB, base + inst * 1024);
+        }
+#pragma unroll
+        for (int i = 0; i < BPW; ++i) {
+            const int inst = wv * BPW + i, row = inst * 8 + lrow;
+            const int sl = lslot ^ ((row >> 1) & 7), gn = n0 + row, gk = k0 + 4 * sl;
+            dma16(rb, (gn < N && gk < K) ? (unsigned)(gn * ldb + gk) * 4u : OOB, base + BM * BK * 4 + inst * 1024);
+        }
+    };
+    // per-k-tile accumulators added to acc (parity: fma chains of BK terms, as k_gemm3)
+    f32x4 acc[AM][AN], tacc[AM][AN];
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+    const int nt = (K + BK - 1) / BK;
+    const int g = lane >> 4, l15 = lane & 15;
+    issue(0, 0);
+    stage_barrier<0>();
+    for (int t = 0; t < nt; ++t) {
+        if (t + 1 < nt) issue((t + 1) & 1, (t + 1) * BK);
+        const float* as = lds + (t & 1) * SF;
+        const float* bs = as + BM * BK;
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int j = 0; j < AN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tacc[i][j][r] = 0.f;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            float4 a[AM], b[AN];
+#pragma unroll
+            for (int i = 0; i < AM; ++i) {
+                const int row = wm * TM + i * 16 + l15;
+                a[i] = *reinterpret_cast<const float4*>(as + row * BK + 4 * ((hh * 4 + g) ^ ((row >> 1) & 7)));
+            }
+#pragma unroll
+            for (int j = 0; j < AN; ++j) {
+                const int row = wn * TN + j * 16 + l15;
+                b[j] = *reinterpret_cast<const float4*>(bs + row * BK + 4 * ((hh * 4 + g) ^ ((row >> 1) & 7)));
+            }
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+#pragma unroll
+                for (int j = 0; j < AN; ++j) {
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[j].x, tacc[i][j], 0, 0, 0);
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b[j].y, tacc[i][j], 0, 0, 0);
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b[j].z, tacc[i][j], 0, 0, 0);
+                    tacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b[j].w, tacc[i][j], 0, 0, 0);
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int j = 0; j < AN; ++j) acc[i][j] += tacc[i][j];
+        stage_barrier<0>();  // tile t + 1 landed; every wave is done with tile t's buffer
+    }
+    // C layout of the 16x16 MFMA: col = lane & 15, row = 4 (lane >> 4) + r
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j) {
+            const int gn = n0 + wn * TN + j * 16 + l15;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gm = m0 + wm * TM + i * 16 + 4 * g + r;
+                if (gm < M && gn < N) C[(long long)gm * ldc + gn] = acc[i][j][r];
+            }
+        }
+}
+
 }  // namespace
 
 // Row chunk of the dW slabs: ~dw3_target_blocks() blocks of 128 x 128 output tiles, multiple of 32 rows.
@@ -581,6 +731,17 @@ int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, in
     if (m_cap <= 0) return 0;
     if (o % 4 != 0) return HGNN_ERR_UNSUPPORTED;
     if ((long long)m_cap * lddy * 4 >= (1ll << 31) || (long long)kout * ldw * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    static const bool dma = [] {
+        const char* e = getenv("HGNN_GEMM_DMA");
+        return !(e && e[0] == '0');
+    }();
+    auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    if (dma && lddy % 4 == 0 && ldw % 4 == 0 && al(dy) && al(wt)) {
+        hipLaunchKernelGGL((k_gemm5<64, 64, 2, 2>), dim3(ceil_div(m_cap, 64), ceil_div(kout, 64)), dim3(256), 0, s,
+                           dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda);
+        HGNN_LAUNCH_CHECK();
+        return 0;
+    }
     G3 p{};
     p.a = dy;
     p.lda = lddy;
