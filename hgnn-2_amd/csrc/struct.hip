@@ -345,6 +345,143 @@ __global__ void __launch_bounds__(X_THREADS) k_extract(ExtractArgs a) {
     }
 }
 
+// ---- LDS-staged extraction: one 1024-thread block per (graph, family) loads the graph's dense
+// blocks into LDS in one round of unconditional loads (16 per thread in flight), then builds the
+// row lists of both orientations and checks the padding from LDS.  Families: 0 = WL (line graph
+// only), 1 = W + Pm/Pd.  Same lists, entry for entry, as k_extract (ascending columns per row).
+constexpr int XL_THREADS = 1024;
+
+__device__ __forceinline__ void lds_fill(float* __restrict__ dst, const float* __restrict__ src, int n) {
+    constexpr int U = 16;
+    for (int base = 0; base < n; base += XL_THREADS * U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[min(base + u * XL_THREADS + (int)threadIdx.x, n - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + u * XL_THREADS + threadIdx.x;
+            if (i < n) dst[i] = v[u];
+        }
+    }
+}
+
+// Rows of an LDS block: element (r, c, j) at S0[r * rs + c * cs + j * js] (NC == 2: S0 / S1 hold the
+// two coefficients).  Wave per output row, lanes over 64-column chunks, ballot compaction.
+template <int NC>
+__device__ void lds_rows(const float* S0, const float* S1, int rows, int cols, int rs, int cs, int js,
+                         int row_packed0, int col_packed0, long long slot0, int cap, RowInfo* __restrict__ out_rows,
+                         float* __restrict__ entries, int stride) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = XL_THREADS / 64;
+    for (int r = wv; r < rows; r += nw) {
+        const long long slot = slot0 + (long long)r * cap;
+        int cnt = 0;
+        for (int c0 = 0; c0 < cols; c0 += 64) {
+            const int c = c0 + lane;
+            float v[NC];
+            bool nz = false;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                v[j] = 0.f;
+                if (c < cols) v[j] = NC == 2 ? (j == 0 ? S0 : S1)[r * rs + c * cs] : S0[r * rs + c * cs + j * js];
+                nz |= v[j] != 0.f;
+            }
+            const unsigned long long mask = __ballot(nz);
+            if (nz) {
+                float* e = entries + (slot + cnt + __popcll(mask & ((1ull << lane) - 1ull))) * stride;
+                e[0] = __int_as_float(col_packed0 + c);
+#pragma unroll
+                for (int j = 0; j < NC; ++j) e[1 + j] = v[j];
+            }
+            cnt += __popcll(mask);
+        }
+        if (lane == 0) out_rows[row_packed0 + r] = RowInfo{(int)slot, cnt};
+    }
+}
+
+// Any nonzero of an LDS (R, C, NC) block outside [0, rr) x [0, rc) (NC = 1 per array for Pm / Pd).
+__device__ void lds_validate(const float* S, int R, int C, int NC, int rr, int rc, uint32_t* err) {
+    bool bad = false;
+    const int n = R * C * NC;
+    for (int i = threadIdx.x; i < n; i += XL_THREADS) {
+        const int r = i / (C * NC), c = (i / NC) % C;
+        if ((r >= rr || c >= rc) && S[i] != 0.f) bad = true;
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, (uint32_t)ERR_PAD_NONZERO);
+}
+
+template <int JT>
+__global__ void __launch_bounds__(XL_THREADS) k_extract_lds(ExtractArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float S[];
+    const int b = blockIdx.x;
+    const int fam = a.dual ? (int)blockIdx.y : 1;
+    const int n0 = a.meta.node_off[b], nb = a.meta.node_off[b + 1] - n0;
+    const int nmax = a.nmax, emax = a.emax;
+    if (fam == 0) {
+        const int e0 = a.meta.edge_off[b], eb = a.meta.edge_off[b + 1] - e0;
+        const int n = emax * emax * JT;
+        lds_fill(S, a.WL + (long long)b * n, n);
+        __syncthreads();
+        const long long slot0 = (long long)b * emax * emax;
+        // WL rows e (cols e'), and the transpose: rows e' (cols e) read down the LDS columns
+        lds_rows<JT>(S, nullptr, eb, eb, emax * JT, JT, 1, e0, e0, slot0, emax, a.rows[S_WL], a.entries[S_WL],
+                     a.entry_stride_w);
+        lds_rows<JT>(S, nullptr, eb, eb, JT, emax * JT, 1, e0, e0, slot0, emax, a.rows[S_WLT], a.entries[S_WLT],
+                     a.entry_stride_w);
+        if (a.validate) {
+            lds_validate(S, emax, emax, JT, eb, eb, a.meta.err);
+            validate_mask(a.mask_lg + (long long)b * emax * emax, emax, eb, a.meta.err);
+        }
+        return;
+    }
+    const int nw_ = nmax * nmax * JT, np = nmax * emax;
+    float* SW = S;
+    float* SM = S + nw_;
+    float* SD = SM + np;
+    lds_fill(SW, a.W + (long long)b * nw_, nw_);
+    if (a.dual) {
+        lds_fill(SM, a.Pm + (long long)b * np, np);
+        lds_fill(SD, a.Pd + (long long)b * np, np);
+    }
+    __syncthreads();
+    const long long slotw = (long long)b * nmax * nmax;
+    lds_rows<JT>(SW, nullptr, nb, nb, nmax * JT, JT, 1, n0, n0, slotw, nmax, a.rows[S_W], a.entries[S_W],
+                 a.entry_stride_w);
+    lds_rows<JT>(SW, nullptr, nb, nb, JT, nmax * JT, 1, n0, n0, slotw, nmax, a.rows[S_WT], a.entries[S_WT],
+                 a.entry_stride_w);
+    if (a.validate) {
+        lds_validate(SW, nmax, nmax, JT, nb, nb, a.meta.err);
+        validate_mask(a.mask + (long long)b * nmax * nmax, nmax, nb, a.meta.err);
+    }
+    if (!a.dual) return;
+    const int e0 = a.meta.edge_off[b], eb = a.meta.edge_off[b + 1] - e0;
+    // Pm/Pd (n, e): node rows over edge cols, and edge rows over node cols
+    lds_rows<2>(SM, SD, nb, eb, emax, 1, 0, n0, e0, (long long)b * nmax * emax, emax, a.rows[S_PN], a.entries[S_PN], 4);
+    lds_rows<2>(SM, SD, eb, nb, 1, emax, 0, e0, n0, (long long)b * emax * nmax, nmax, a.rows[S_PE], a.entries[S_PE], 4);
+    if (a.validate) {
+        lds_validate(SM, nmax, emax, 1, nb, eb, a.meta.err);
+        lds_validate(SD, nmax, emax, 1, nb, eb, a.meta.err);
+    }
+}
+
+// LDS bytes of the staged extraction (0: does not fit, use k_extract)
+static size_t extract_lds_bytes(const ExtractArgs& a) {
+    const size_t wl = a.dual ? (size_t)a.emax * a.emax * a.jtot : 0;
+    const size_t wp = (size_t)a.nmax * a.nmax * a.jtot + (a.dual ? 2 * (size_t)a.nmax * a.emax : 0);
+    const size_t b = 4 * (wl > wp ? wl : wp);
+    return b <= 96 * 1024 ? b : 0;
+}
+
+template <int JT>
+static void extract_lds_launch(const ExtractArgs& a, size_t lds, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_extract_lds<JT>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_extract_lds<JT>, dim3(a.bs, a.dual ? 2 : 1), dim3(XL_THREADS), lds, s, a);
+}
+
 static int extract_one(const ExtractArgs& a, dim3 grid, hipStream_t s) {
     switch (a.jtot) {
         case 3: hipLaunchKernelGGL(k_extract<3>, grid, dim3(X_THREADS), 0, s, a); break;
@@ -357,6 +494,21 @@ static int extract_one(const ExtractArgs& a, dim3 grid, hipStream_t s) {
 }
 
 int launch_extract(const ExtractArgs& a, hipStream_t s) {
+    static const bool staged = [] {
+        const char* e = getenv("HGNN_EXTRACT_LDS");
+        return !(e && e[0] == '0');
+    }();
+    const size_t lds = extract_lds_bytes(a);
+    if (staged && lds > 0 && a.kind0 == 0) {
+        switch (a.jtot) {
+            case 3: extract_lds_launch<3>(a, lds, s); break;
+            case 4: extract_lds_launch<4>(a, lds, s); break;
+            case 5: extract_lds_launch<5>(a, lds, s); break;
+            default: return 2;
+        }
+        HGNN_LAUNCH_CHECK();
+        return 0;
+    }
     const int kinds = a.dual ? X_SLOTS : 2;
     // HGNN_EXTRACT_SPLIT=1 (diagnostics): one launch per block slot, so a kernel trace times
     // each slot
