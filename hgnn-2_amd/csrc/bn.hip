@@ -207,31 +207,21 @@ __device__ __forceinline__ float& f4c(float4& v, int i) { return reinterpret_cas
 // Last-arriver combine of the per-tile partials (replaces k_bn_bwd_fin): the last block of each
 // group of BN_GROUP tiles sums the group's partials in tile order (fp64), the last group sums
 // the groups in order -- deterministic, and one kernel boundary fewer per BN backward.
-// Hand-off (the counter form of the guide's publish/consume recipe; the XCDs' L2s are not
-// coherent): partials stored write-through (sc1), every storing wave drains its stores, the
-// block's barrier, one relaxed agent-scope ticket; the block drawing the last ticket takes one
-// agent-scope acquire before reading.  Counters are zeroed by the forward's memset and reset by
-// their last user.
-__device__ __forceinline__ void store_sc1(float* base, long long idx, float4 v) {
-    const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r,
-                                           (int)(idx * 4), 0, 16);  // aux 16 = sc1 (write-through)
-}
-
+// Hand-off (the XCDs' L2s are not coherent): partials stored with plain stores, the block's
+// barrier, one thread's device-scope fence (release: the block's stores are in its L2 after the
+// barrier, the fence writes them back) and relaxed ticket; the block drawing the last ticket
+// fences again (acquire) before reading.  Counters are zeroed by the forward's memset and reset
+// by their last user (plain stores: the next reader is a later launch).
 typedef __attribute__((address_space(1))) int gi32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 __device__ bool bn_bwd_ticket(int* cnt, int want) {
     __shared__ int last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (sc1 stores)
     __syncthreads();
     if (threadIdx.x == 0) {
+        __threadfence();
         const int t = __hip_atomic_fetch_add((gi32*)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = t == want - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (last) __threadfence();
     }
     __syncthreads();
     return last;
@@ -251,10 +241,9 @@ __device__ void bn_bwd_combine(const BnBwdArgs& a, int tile, int tiles) {
         double t = 0.0;
 #pragma unroll
         for (int k = 0; k < BN_GROUP; ++k) t += k < gsize ? (double)v[k] : 0.0;
-        __hip_atomic_store((gu64*)a.gpart + (long long)grp * n4 + i, __builtin_bit_cast(unsigned long long, t),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.gpart[(long long)grp * n4 + i] = t;
     }
-    if (threadIdx.x == 0) __hip_atomic_store((gi32*)&a.cnt[1 + grp], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) a.cnt[1 + grp] = 0;
     if (!bn_bwd_ticket(&a.cnt[0], ngrp)) return;
     for (int i = threadIdx.x; i < n4; i += blockDim.x) {
         double t = 0.0;
@@ -267,7 +256,7 @@ __device__ void bn_bwd_combine(const BnBwdArgs& a, int tile, int tiles) {
         }
         a.sums[i] = (float)t;
     }
-    if (threadIdx.x == 0) __hip_atomic_store((gi32*)&a.cnt[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) a.cnt[0] = 0;
 }
 
 __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
@@ -336,8 +325,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
             f4c(t4, j) = t;
         }
         const long long idx = ((long long)tile * a.c + ch) * 4;
-        if (a.cnt) store_sc1(a.part, idx, t4);  // handed to the combining block (bn_bwd_combine)
-        else *reinterpret_cast<float4*>(a.part + idx) = t4;
+        *reinterpret_cast<float4*>(a.part + idx) = t4;
     }
     if (a.cnt) bn_bwd_combine(a, tile, ceil_div(total, 64));
 }
