@@ -91,6 +91,18 @@ __device__ __forceinline__ float4 lane_entry(const float* __restrict__ entries, 
     return make_float4(__int_as_float(0), 0.f, 0.f, 0.f);
 }
 
+// Row info through the constant address space: a wave-uniform index then becomes one scalar
+// load (lgkmcnt, not the vector counter the gathers wait on) and the row's counts live in SGPRs.
+// The lists are written by an earlier launch and only read here.
+__device__ __forceinline__ RowInfo row_info(const RowInfo* rows, int r) {
+    typedef const __attribute__((address_space(4))) int* ConstInts;
+    const ConstInts q = (ConstInts)(reinterpret_cast<const int*>(rows) + 2 * (long long)r);
+    RowInfo v;
+    v.start = q[0];
+    v.count = q[1];
+    return v;
+}
+
 __device__ __forceinline__ float bcast(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -139,8 +151,8 @@ __global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
     // row infos, then both entry chunks, then the gathers of both lists in one batch, so a
     // row costs ~3 dependent memory round trips instead of 6.
     RowInfo rg{0, 0}, rp{0, 0};
-    if constexpr (CG > 0) rg = a.g.rows[r];
-    if constexpr (CP > 0) rp = a.p.rows[r];
+    if constexpr (CG > 0) rg = row_info(a.g.rows, r);
+    if constexpr (CP > 0) rp = row_info(a.p.rows, r);
     LaneBn<CGx> bng;
     LaneBn<CPx> bnp;
     if constexpr (CG > 0) bng.init(a.gbn, a.cg, lane);
@@ -352,7 +364,7 @@ __device__ __forceinline__ void agg_bwd_g(const AggBwdArgs& a, int r, int lane) 
 #pragma unroll
         for (int i = 0; i < C; ++i) acc[i] = 0.f;
     }
-    const RowInfo ri = a.g.rows[r];
+    const RowInfo ri = row_info(a.g.rows, r);
     const int stride = a.g.stride;
     for (int e0 = 0; e0 < ri.count; e0 += 64) {
         const int n = min(64, ri.count - e0);
@@ -380,7 +392,7 @@ __device__ __forceinline__ void agg_bwd_p(const AggBwdArgs& a, int r, int lane) 
 #pragma unroll
         for (int i = 0; i < C; ++i) acc[i] = 0.f;
     }
-    const RowInfo ri = a.p.rows[r];
+    const RowInfo ri = row_info(a.p.rows, r);
     for (int e0 = 0; e0 < ri.count; e0 += 64) {
         const int n = min(64, ri.count - e0);
         const float4 me = lane_entry(a.p.entries, 4, ri.start + e0, n, lane);

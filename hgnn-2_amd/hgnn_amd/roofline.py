@@ -117,6 +117,31 @@ def class_work(kcls, counts, order, f_in, d, n_layers, jt=3):
     return fl, by
 
 
+def agg_requested_bytes(kcls, counts, order, f_in, d, n_layers, jt=3):
+    """Bytes the aggregation kernels of one step request from the memory system, on-chip reuse
+    not subtracted: one source row per list entry (forward: the row feeds all J+2 coefficients;
+    backward: one row slice per nonzero coefficient -- the diagonal entry's I and D slices, one
+    A slice per other entry), every output row written once, the row lists read once.  The
+    gap to class_work's compulsory bytes is what the L2 / MALL serve."""
+    all_halves, k_last = lg_halves(order, f_in, d, n_layers, jt)
+    halves = [h for h in all_halves if not fused_half(d, h[2], h[3])]
+    c2 = 2 * d
+    rows = lambda edge: counts["edges"] if edge else counts["nodes"]  # noqa: E731
+    nnz_g = lambda edge: counts["nnz_wl"] if edge else counts["nnz_w"]  # noqa: E731
+    by = 0.0
+    if kcls == K_AGG_FWD:
+        for edge, k, cg, cp in halves + [(False, k_last, c2, c2)]:
+            r = rows(edge)
+            by += 4.0 * (nnz_g(edge) * cg + counts["nnz_p"] * cp + r * k) + 8.0 * 2 * r + 16.0 * (
+                nnz_g(edge) + counts["nnz_p"])
+    elif kcls == K_AGG_BWD and not fused_bwd(d):
+        for edge, k, cg, cp in all_halves + [(False, k_last, c2, c2)]:
+            r, ro = rows(edge), rows(not edge)
+            by += 4.0 * ((nnz_g(edge) + r) * cg + 2 * counts["nnz_p"] * cp + r * cg + ro * cp) + 8.0 * (r + ro) + 16.0 * (
+                nnz_g(edge) + counts["nnz_p"])
+    return by
+
+
 def forward_work(counts, order, f_in, d, n_layers, jt=3):
     """(flops, compulsory bytes) of one LG-GNN forward (SURVEY.md §8 d 'LG-GNN forward bytes / FLOPs'):
     every layer reads its input features once and writes its pre-BN output once; the structure
@@ -198,7 +223,13 @@ def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, s
         achieved = by * steps / sec / 1e9
         peak, unit, bound = PEAK_HBM_GBS, "GB/s", "hbm"
     per_launch = launches / max(steps, 1)
-    return {
+    extra = {}
+    if kcls in (K_AGG_FWD, K_AGG_BWD):
+        rq = agg_requested_bytes(kcls, counts, order, f_in, d, n_layers, jt)
+        rq_gbs = rq * steps / sec / 1e9
+        extra = {"requested_bytes_per_launch": rq / max(per_launch, 1e-9), "requested_gbs": round(rq_gbs, 1),
+                 "requested_frac": round(rq_gbs / PEAK_HBM_GBS, 4)}
+    return {**extra, **{
         "kernel": NAMES[kcls],
         "bound": bound,
         "achieved": round(achieved, 3),
@@ -211,7 +242,7 @@ def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, s
         "launches_per_step": per_launch,
         "avg_launch_us": round(ms_total * 1e3 / max(launches, 1), 3),
         "algorithmic_per_step": {"flops": fl, "bytes": by},
-    }
+    }}
 
 
 def to_device_counts(batch):
