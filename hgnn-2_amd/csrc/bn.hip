@@ -128,8 +128,6 @@ int launch_bn_apply(const float* y, const int* total_rows, int cap_rows, int c, 
 
 // ---------------------------------------------------------------- BN backward
 int bn_bwd_tiles(int cap_rows) { return ceil_div(cap_rows, 64); }
-constexpr int BN_GROUP = 16;  // tiles per first-level group of the last-arriver reduction
-int bn_bwd_groups(int cap_rows) { return ceil_div(bn_bwd_tiles(cap_rows), BN_GROUP); }
 
 // Per 64-row tile and channel: {sum g, sum g h, sum dz h, sum dz}, g = w dz, h = (y - mean) / std.
 __global__ void __launch_bounds__(256) k_bn_bwd_part(BnBwdArgs a) {
@@ -204,67 +202,10 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part(BnBwdArgs a) {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float& f4c(float4& v, int i) { return reinterpret_cast<float*>(&v)[i]; }
 
-// Last-arriver combine of the per-tile partials (replaces k_bn_bwd_fin): the last block of each
-// group of BN_GROUP tiles sums the group's partials in tile order (fp64), the last group sums
-// the groups in order -- deterministic, and one kernel boundary fewer per BN backward.
-// Hand-off (the XCDs' L2s are not coherent): partials stored with plain stores, the block's
-// barrier, one thread's device-scope fence (release: the block's stores are in its L2 after the
-// barrier, the fence writes them back) and relaxed ticket; the block drawing the last ticket
-// fences again (acquire) before reading.  Counters are zeroed by the forward's memset and reset
-// by their last user (plain stores: the next reader is a later launch).
-typedef __attribute__((address_space(1))) int gi32;
-
-__device__ bool bn_bwd_ticket(int* cnt, int want) {
-    __shared__ int last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        const int t = __hip_atomic_fetch_add((gi32*)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = t == want - 1;
-        if (last) __threadfence();
-    }
-    __syncthreads();
-    return last;
-}
-
-__device__ void bn_bwd_combine(const BnBwdArgs& a, int tile, int tiles) {
-    const int grp = tile / BN_GROUP, ngrp = ceil_div(tiles, BN_GROUP);
-    const int gsize = min(BN_GROUP, tiles - grp * BN_GROUP);
-    if (!bn_bwd_ticket(&a.cnt[1 + grp], gsize)) return;
-    const int n4 = a.c * 4;
-    // all of a column's loads in flight before the first add (clamped, selected after)
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
-        float v[BN_GROUP];
-#pragma unroll
-        for (int k = 0; k < BN_GROUP; ++k)
-            v[k] = a.part[(long long)(grp * BN_GROUP + min(k, gsize - 1)) * n4 + i];
-        double t = 0.0;
-#pragma unroll
-        for (int k = 0; k < BN_GROUP; ++k) t += k < gsize ? (double)v[k] : 0.0;
-        a.gpart[(long long)grp * n4 + i] = t;
-    }
-    if (threadIdx.x == 0) a.cnt[1 + grp] = 0;
-    if (!bn_bwd_ticket(&a.cnt[0], ngrp)) return;
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
-        double t = 0.0;
-        for (int g0 = 0; g0 < ngrp; g0 += BN_GROUP) {
-            double v[BN_GROUP];
-#pragma unroll
-            for (int k = 0; k < BN_GROUP; ++k) v[k] = a.gpart[(long long)min(g0 + k, ngrp - 1) * n4 + i];
-#pragma unroll
-            for (int k = 0; k < BN_GROUP; ++k) t += g0 + k < ngrp ? v[k] : 0.0;
-        }
-        a.sums[i] = (float)t;
-    }
-    if (threadIdx.x == 0) a.cnt[0] = 0;
-}
-
 __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
     const int tile = blockIdx.x;
     const int total = *a.total_rows;
     const int r0 = tile * 64;
-    if (a.cnt && total <= 0 && tile == 0)  // no rows: the statistics are zero (k_bn_bwd_fin's result)
-        for (int i = threadIdx.x; i < a.c * 4; i += blockDim.x) a.sums[i] = 0.f;
     if (r0 >= total) return;
     const int r1 = min(total, r0 + 64);
     const float wv = *a.w;
@@ -327,7 +268,6 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
         const long long idx = ((long long)tile * a.c + ch) * 4;
         *reinterpret_cast<float4*>(a.part + idx) = t4;
     }
-    if (a.cnt) bn_bwd_combine(a, tile, ceil_div(total, 64));
 }
 
 __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
@@ -519,27 +459,136 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
     }
 }
 
+// The whole BN backward of a small input (c <= 16 channels, <= 64 row tiles: the GNN_simple
+// layers of config 1) in ONE block: statistics over all rows, then dY and the per-tile column sums
+// of dY, separated by the block's barriers -- one launch instead of part4 + fin + apply4.  The same
+// formulas as those three kernels; the statistics are summed per thread in fp32 (a few rows each)
+// and across threads in fp64.
+constexpr int BN_SMALL_THREADS = 1024, BN_SMALL_TILES = 64, BN_SMALL_C = 16;
+
+__global__ void __launch_bounds__(BN_SMALL_THREADS) k_bn_bwd_small(BnBwdArgs a) {
+    const int total = *a.total_rows;
+    const int L = a.c >> 2, RG = BN_SMALL_THREADS / L;
+    const int lane = threadIdx.x % L, rg = threadIdx.x / L;
+    const float wv = *a.w;
+    float mu[4], isd[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        mu[i] = a.mean[4 * lane + i];
+        isd[i] = 1.0f / a.std[4 * lane + i];
+    }
+    // pass 1: the four per-channel sums of k_bn_bwd_part4
+    float4 st[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = rg; r < total; r += RG) {
+        const long long i = (long long)r * a.c + 4 * lane;
+        float4 dz = ld4(a.dz + i), yv = ld4(a.y + i);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float h = (f4c(yv, k) - mu[k]) * isd[k];
+            const float d = f4c(dz, k);
+            const float g = wv * d;
+            f4c(st[0], k) += g;
+            f4c(st[1], k) = fmaf(g, h, f4c(st[1], k));
+            f4c(st[2], k) = fmaf(d, h, f4c(st[2], k));
+            f4c(st[3], k) += d;
+        }
+    }
+    // fp64 reduction: over the lanes of a wave holding the same channels (threads t, t + L, ...),
+    // then over the 16 waves
+    __shared__ double wred[BN_SMALL_THREADS / 64][BN_SMALL_C][4];
+    const int w = threadIdx.x >> 6, wl = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            double v = (double)f4c(st[j], k);
+            for (int o = 32; o >= L; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (wl < L) wred[w][4 * wl + k][j] = v;
+        }
+    __syncthreads();
+    __shared__ float sums[BN_SMALL_C][4];
+    if (threadIdx.x < a.c * 4) {
+        const int ch = threadIdx.x >> 2, j = threadIdx.x & 3;
+        double t = 0.0;
+        for (int q = 0; q < BN_SMALL_THREADS / 64; ++q) t += wred[q][ch][j];
+        sums[ch][j] = (float)t;
+        a.sums[ch * 4 + j] = (float)t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t1 = 0.0, t2 = 0.0;
+        for (int ch = 0; ch < a.c; ++ch) {
+            t1 += (double)sums[ch][2];
+            t2 += (double)sums[ch][3];
+        }
+        *a.dw = (float)t1;
+        *a.db = (float)t2;
+    }
+    // pass 2: dY (k_bn_bwd_apply4) and the per-64-row-tile column sums of dY; thread -> (tile slot,
+    // row of the tile, lane), 64 * L threads per tile
+    const float inv_n = total > 0 ? 1.0f / (float)total : 0.f;
+    float m1[4], m2[4];
+    bool relu[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int ch = 4 * lane + i;
+        m1[i] = sums[ch][0] * inv_n;
+        m2[i] = sums[ch][1] * inv_n;
+        relu[i] = ch >= a.relu_from;
+    }
+    const int per_tile = 64 * L, slots = BN_SMALL_THREADS / per_tile;
+    const int slot = threadIdx.x / per_tile, row = (threadIdx.x % per_tile) / L;
+    __shared__ float4 cred[BN_SMALL_THREADS];
+    const int tiles = ceil_div(total, 64);
+    for (int t0 = 0; t0 < tiles; t0 += slots) {
+        const int tile = t0 + slot, r = tile * 64 + row;
+        float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (tile < tiles && r < total) {
+            const long long i = (long long)r * a.c + 4 * lane;
+            float4 yv = ld4(a.y + i), dz = ld4(a.dz + i);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                f4c(d, k) = bn_bwd_dy_inv(f4c(yv, k), f4c(dz, k), mu[k], isd[k], wv, m1[k], m2[k], a.training != 0,
+                                          relu[k]);
+            *reinterpret_cast<float4*>(a.dy + i) = d;
+        }
+        if (a.dbpart) {
+            cred[threadIdx.x] = d;
+            __syncthreads();
+            if (threadIdx.x < slots * a.c) {
+                const int sl = threadIdx.x / a.c, ch = threadIdx.x % a.c, tl = t0 + sl;
+                if (tl < tiles) {
+                    float acc = 0.f;
+                    for (int q = 0; q < 64; ++q) {
+                        float4 v = cred[sl * per_tile + q * L + (ch >> 2)];
+                        acc += f4c(v, ch & 3);
+                    }
+                    a.dbpart[(long long)tl * a.c + ch] = acc;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     const int tiles = bn_bwd_tiles(a.cap_rows);
     const bool v4 = bn_vec4(a);
-    // the last-arriver combine only for small batches (<= 64 tiles): at the config-2 sizes (364 edge
-    // tiles) the combining tail cost more than the fin launch it saves (part4 + combine 29.6 us vs
-    // part4 + fin 24 us per launch, 311-314 K vs 313-321 K graphs/s)
-    const bool combine = v4 && a.cnt && a.gpart && tiles <= 64;
+    // (c / 4 a power of two: the per-wave shuffle reduction pairs the lanes of one channel group)
+    if (apply && v4 && (a.c == 4 || a.c == 8 || a.c == 16) && tiles <= BN_SMALL_TILES) {
+        hipLaunchKernelGGL(k_bn_bwd_small, dim3(1), dim3(BN_SMALL_THREADS), 0, s, a);
+        HGNN_LAUNCH_CHECK();
+        return 0;
+    }
     if (tiles > 0) {
-        if (v4) {
-            BnBwdArgs b = a;
-            if (!combine) b.cnt = nullptr;
-            hipLaunchKernelGGL(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, b);
-        } else {
-            hipLaunchKernelGGL(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
-        }
+        if (v4) hipLaunchKernelGGL(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
     }
     HGNN_LAUNCH_CHECK();
-    if (!combine || tiles == 0) {
-        hipLaunchKernelGGL(k_bn_bwd_fin, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, a);
-        HGNN_LAUNCH_CHECK();
-    }
+    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, a);
+    HGNN_LAUNCH_CHECK();
     if (!apply) return 0;
     if (v4) hipLaunchKernelGGL(k_bn_bwd_apply4, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_bn_bwd_apply, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);

@@ -276,13 +276,7 @@ struct BnBwdArgs {
     float* dw;             // scalar out
     float* db;             // scalar out
     float* dbpart;         // optional out: per-64-row-tile column sums of dy [tiles][c]
-    // optional (float4 path): the tile partials are combined by the last-arriving blocks instead
-    // of a separate k_bn_bwd_fin launch -- cnt: 1 + bn_bwd_groups(cap) counters, zero on entry
-    // (left zero on exit); gpart: [bn_bwd_groups(cap)][c][4] fp64 group sums
-    int* cnt;
-    double* gpart;
 };
-int bn_bwd_groups(int cap_rows);
 // apply = 0: only the statistics (part + fin); dY is then produced by the dA GEMM
 // (launch_gemm3_da_bn), which applies the BN backward while staging its A operand.
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply = 1);

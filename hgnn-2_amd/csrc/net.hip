@@ -52,7 +52,7 @@ struct Program {
     size_t node_off = 0, edge_off = 0, totals = 0, err = 0;
     size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
     int entry_stride_w = 4;
-    size_t dy = 0, dy2 = 0, da = 0, da2 = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, bnb_cnt = 0, bnb_gpart = 0, bnb_cnt_bytes = 0, rb_scratch = 0, dbpart = 0, dbpart2 = 0;
+    size_t dy = 0, dy2 = 0, da = 0, da2 = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0, dbpart2 = 0;
     bool v2 = false;  // GEMM v2 path (2d % 4 == 0); gemm.hip otherwise
     bool fused = false;      // fused aggregation + GEMM forward (fused.hip): 2d % 16 == 0, 2d <= 256
     bool fused_bwd = false;  // fused backward dX (HGNN_FUSED_BWD=1; see DESIGN.md §8 for why it is off)
@@ -218,11 +218,6 @@ Program build_program(const hgnn_net_config* c) {
     P.edge_off = B.take(sizeof(int) * (c->bs + 1));
     P.totals = B.take(sizeof(int) * 4);
     P.err = B.take(sizeof(uint32_t) * 4);
-    // right after the error word: the forward's one memset zeroes both (the BN backward's
-    // last-arriver counters, left zero by every launch that uses them)
-    P.bnb_cnt_bytes = (size_t)(1 + bn_bwd_groups(std::max(P.cap_n, P.cap_e) > 0 ? std::max(P.cap_n, P.cap_e) : 1)) *
-                      sizeof(int);
-    P.bnb_cnt = B.take(P.bnb_cnt_bytes);
     const int nmax = c->nmax, emax = lg ? c->emax : 0;
     const size_t sw = P.entry_stride_w * sizeof(float);
     P.rows[S_W] = B.take(sizeof(RowInfo) * P.cap_n);
@@ -278,7 +273,6 @@ Program build_program(const hgnn_net_config* c) {
     P.slabs = B.take(max_slab * sizeof(float));
     P.bnb_part = B.take((size_t)bn_bwd_tiles(max_cap) * P.c2 * 4 * sizeof(float));
     P.bnb_sums = B.take((size_t)P.c2 * 4 * sizeof(float));
-    P.bnb_gpart = B.take((size_t)bn_bwd_groups(max_cap > 0 ? max_cap : 1) * P.c2 * 4 * sizeof(double));
     P.rb_scratch = B.take(readout_bwd_scratch_bytes(c->dim_out, P.k_last));
     P.bytes = B.top;
     return P;
@@ -487,8 +481,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
     const bool lg = c->kind == 1;
     const Src src = make_src(P, ws, csr);
     BatchMeta m = src.m;
-    // the error word and the BN-backward counters behind it (build_program)
-    HGNN_HOST_CHECK(hipMemsetAsync(m.err, 0, P.bnb_cnt + P.bnb_cnt_bytes - P.err, s));
+    HGNN_HOST_CHECK(hipMemsetAsync(m.err, 0, sizeof(uint32_t), s));
     if (!csr) {
     TL(HGNN_K_STRUCT, launch_plan(in->d_N_batch, lg ? in->d_E_batch : nullptr, c->bs, c->nmax, lg ? c->emax : 0, m, s));
 
@@ -937,8 +930,6 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         bb.training = c->training;
         bb.part = at<float>(ws, P.bnb_part);
         bb.sums = at<float>(ws, P.bnb_sums);
-        bb.cnt = at<int>(ws, P.bnb_cnt);
-        bb.gpart = at<double>(ws, P.bnb_gpart);
         bb.dy = dyb;
         bb.dw = grads[h.pbn_w];
         bb.db = grads[h.pbn_b];
