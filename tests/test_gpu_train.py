@@ -87,6 +87,49 @@ def test_train_step_matches_torch_adamax_loop(csr):
         noisy = {}
 
 
+def test_train_step_vs_fp64_oracle_two_steps():
+    """TrainStep against the fp64 oracle (oracle/ref_mnb.py) with torch's Adamax on the oracle's
+    parameters: two steps of scripts/train_mnb.py:41-91 on different batches, no re-synchronisation.
+    Adamax's first steps move a parameter by ~lr * sign(g): every element whose oracle gradient is
+    above the noise floor (1e-4 max|g|) must land within 1e-5 * max(1, |p|) of the oracle's; the
+    others (analytically zero gradients) within 2 lr per step."""
+    import hgnn_amd.datagen as dg
+    from functions.utils import normalize_data
+    from hgnn_amd.train import TrainStep
+    from models.gnns.model_mnb import GNN_lg
+    from oracle import ref_mnb as R
+    torch.manual_seed(31)
+    L, order, mean, std, lr = 4, 2, 0.3, 1.7, 1e-3
+    model = GNN_lg(0, 16, L, 5, 1, 1, order).cuda()
+    p64 = {k: v.detach().cpu().double().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    names = [k for k, _ in model.named_parameters()]
+    opt = torch.optim.Adamax([p64[k] for k in names], lr=lr)
+    st = R.bn_states(L, 2 * model.n_features, dtype=torch.float64)
+    step = TrainStep(model, lr=lr, t_mean=mean, t_std=std)
+    noisy = {k: torch.zeros_like(p64[k], dtype=torch.bool) for k in names}
+    for i in range(2):
+        b = _batch(dg.qm9_shape_dataset(48, seed=900 + i))
+        X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = [t.cpu() for t in b]
+        opt.zero_grad()
+        out = R.gnn_lg(p64, [X.double(), XL.double(), W.double(), WL.double(), Pm.double(), Pd.double()], Nb,
+                       mask.double(), Eb, mask_lg.double(), L, order, st, True)
+        loss = torch.nn.MSELoss()(out, normalize_data(T.double(), mean, std))
+        loss.backward()
+        gmax = max(p64[k].grad.abs().max().item() for k in names)
+        for k in names:
+            noisy[k] |= p64[k].grad.abs() <= 1e-4 * gmax
+        opt.step()
+        s = step(b).cpu()
+        assert abs(s[0].item() - loss.item()) <= 1e-5 * max(1.0, abs(loss.item())), (i, s[0].item(), loss.item())
+        for k, p in model.named_parameters():
+            q = p64[k].detach()
+            err = (p.detach().cpu().double() - q).abs()
+            tight = err[~noisy[k]]
+            assert tight.numel() == 0 or tight.max().item() <= 1e-5 * max(1.0, q.abs().max().item()), \
+                (i, k, tight.max().item())
+            assert err.max().item() <= 2 * lr * (i + 1) + 1e-6, (i, k, err.max().item())
+
+
 def test_adamax_kernel_matches_torch_exactly_on_fixed_grads():
     """The optimizer alone, on identical gradients: elementwise agreement to 1 ulp-scale."""
     from hgnn_amd import _lib as L
