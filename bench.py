@@ -276,7 +276,8 @@ def main():
             e = RF.roofline_entry(k, kms, kn, counts, args.order, 5, args.d, args.layers, args.steps,
                                   pmc_path=os.path.join(REPO, "profiles", "pmc_traffic.json"))
             ent = {x: e[x] for x in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                                     "algorithmic_bytes_per_launch", "launches_per_step", "avg_launch_us")}
+                                     "algorithmic_bytes_per_launch", "launches_per_step", "avg_launch_us",
+                                     "requested_bytes_per_launch", "requested_gbs", "requested_frac") if x in e}
             if e["bound"] == "hbm":
                 roof_hbm[RF.NAMES[k]] = ent
             else:
@@ -316,7 +317,8 @@ def main():
                     "frac_mfma": round(ffl / fms / 1e9 / RF.PEAK_FP32_MFMA_TFS, 4),
                     "achieved_gbs": round(fby / fms / 1e6, 2),
                     "frac_hbm": round(fby / fms / 1e6 / RF.PEAK_HBM_GBS, 4),
-                    "agg_fwd": {x: agg[x] for x in ("achieved", "unit", "frac", "launches_per_step", "avg_launch_us")}}
+                    "agg_fwd": {x: agg[x] for x in ("achieved", "unit", "frac", "launches_per_step", "avg_launch_us",
+                                                    "requested_gbs", "requested_frac")}}
         if fn_f:
             fe = RF.roofline_entry(RF.K_FUSED_FWD, fms_f, fn_f, counts_f, args.order, 5, args.d, args.layers, args.steps)
             roof_fwd["fused_fwd"] = {x: fe[x] for x in ("achieved", "unit", "frac", "launches_per_step", "avg_launch_us")}
