@@ -318,6 +318,17 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
             *reinterpret_cast<float4*>(a.dy + i) = d;
         };
         int r = r0 + rg;
+        for (; r + 7 * RG < r1; r += 8 * RG) {
+            float4 dz[8], yv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const long long i = (long long)(r + u * RG) * a.c + 4 * lane;
+                dz[u] = ld4(a.dz + i);
+                yv[u] = ld4(a.y + i);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) one((long long)(r + u * RG) * a.c + 4 * lane, yv[u], dz[u]);
+        }
         for (; r + 3 * RG < r1; r += 4 * RG) {
             float4 dz[4], yv[4];
 #pragma unroll
