@@ -584,12 +584,236 @@ __global__ void __launch_bounds__(BN_SMALL_THREADS) k_bn_bwd_small(BnBwdArgs a) 
     }
 }
 
+// ---- Two-launch BN backward (c = 4L, L in {16, 32, 64}: 2d = 64 / 128 / 256).  The three-launch
+// form above spends ~6 us of a ~20 us half on k_bn_bwd_fin, a launch that only sums the tile
+// partials.  Here the statistics pass uses 256-row tiles (1024 threads, 8-16 rows in flight per
+// thread), so there are few enough partials (91 at config 2's edge half) that every block of the
+// apply pass sums them itself in its prologue (same fixed order in every block: identical sums,
+// deterministic), and k_bn_bwd_fin disappears.  dbpart keeps its 64-row tiles.
+constexpr int BN2_THREADS = 1024, BN2_ROWS = 256;
+
+__device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+template <int L>
+__global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_part2(BnBwdArgs a) {
+    constexpr int RG = BN2_THREADS / L, RPT = BN2_ROWS / RG, C = 4 * L;
+    const int tile = blockIdx.x;
+    const int total = *a.total_rows;
+    const int r0 = tile * BN2_ROWS;
+    if (r0 >= total) return;
+    const int r1 = min(total, r0 + BN2_ROWS);
+    const float wv = *a.w;
+    const int lane = threadIdx.x % L, rg = threadIdx.x / L;
+    float mu[4], isd[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        mu[i] = a.mean[4 * lane + i];
+        isd[i] = 1.0f / a.std[4 * lane + i];
+    }
+    float4 st[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[j] = f4_zero();
+    constexpr int U = RPT < 8 ? RPT : 8;
+#pragma unroll
+    for (int i0 = 0; i0 < RPT; i0 += U) {
+        float4 dz[U], yv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long r = min(r0 + rg + RG * (i0 + u), r1 - 1);  // clamped: unconditional loads
+            dz[u] = ld4(a.dz + r * C + 4 * lane);
+            yv[u] = ld4(a.y + r * C + 4 * lane);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (r0 + rg + RG * (i0 + u) >= r1) continue;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float h = (f4c(yv[u], k) - mu[k]) * isd[k];
+                const float d = f4c(dz[u], k);
+                const float g = wv * d;
+                f4c(st[0], k) += g;
+                f4c(st[1], k) = fmaf(g, h, f4c(st[1], k));
+                f4c(st[2], k) = fmaf(d, h, f4c(st[2], k));
+                f4c(st[3], k) += d;
+            }
+        }
+    }
+    // over the RG row groups, in order
+    __shared__ float4 red[BN2_THREADS];
+    float out[4] = {0.f, 0.f, 0.f, 0.f};
+    const int ch = threadIdx.x;  // < C: the channel this thread finishes
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        red[threadIdx.x] = st[j];
+        __syncthreads();
+        if (ch < C) {
+            float t = 0.f;
+            for (int q = 0; q < RG; ++q) t += f4c(red[q * L + (ch >> 2)], ch & 3);
+            out[j] = t;
+        }
+        __syncthreads();
+    }
+    if (ch < C)
+        *reinterpret_cast<float4*>(a.part + ((long long)tile * C + ch) * 4) = make_float4(out[0], out[1], out[2], out[3]);
+}
+
+template <int L>
+__global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_apply2(BnBwdArgs a) {
+    constexpr int RG = BN2_THREADS / L, RPT = BN2_ROWS / RG, C = 4 * L, SUB = BN2_THREADS / C;
+    constexpr int RPQ = 64 / RG;  // rows of a thread per 64-row dbpart tile
+    const int total = *a.total_rows;
+    const int r0 = blockIdx.x * BN2_ROWS;
+    const bool first = blockIdx.x == 0;
+    if (r0 >= total && !first) return;
+    const int tiles = ceil_div(total, BN2_ROWS);
+    // prologue: the per-channel sums over all tile partials, fp64, fixed order (thread (ch, sub)
+    // sums tiles sub, sub + SUB, ...; then the SUB sub-sums in order)
+    __shared__ double2 pr[BN2_THREADS];
+    __shared__ double2 pt[BN2_THREADS];
+    __shared__ float sm1[C], sm2[C];
+    {
+        const int ch = threadIdx.x % C, sub = threadIdx.x / C;
+        double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+        int t = sub;
+        for (; t + 3 * SUB < tiles; t += 4 * SUB) {
+            float4 q[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) q[u] = ld4(a.part + ((long long)(t + u * SUB) * C + ch) * 4);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                v0 += (double)q[u].x;
+                v1 += (double)q[u].y;
+                v2 += (double)q[u].z;
+                v3 += (double)q[u].w;
+            }
+        }
+        for (; t < tiles; t += SUB) {
+            const float4 q = ld4(a.part + ((long long)t * C + ch) * 4);
+            v0 += (double)q.x;
+            v1 += (double)q.y;
+            v2 += (double)q.z;
+            v3 += (double)q.w;
+        }
+        pr[threadIdx.x] = make_double2(v0, v1);
+        pt[threadIdx.x] = make_double2(v2, v3);
+    }
+    __syncthreads();
+    const float inv_n = total > 0 ? 1.0f / (float)total : 0.f;
+    if (threadIdx.x < C) {
+        double s1 = 0.0, s2 = 0.0;
+        for (int q = 0; q < SUB; ++q) {
+            s1 += pr[q * C + threadIdx.x].x;
+            s2 += pr[q * C + threadIdx.x].y;
+        }
+        sm1[threadIdx.x] = (float)s1 * inv_n;
+        sm2[threadIdx.x] = (float)s2 * inv_n;
+        if (first) {  // BN scalar grads: dw = sum_c sum dz h, db = sum_c sum dz (per channel rounded, as k_bn_bwd_fin)
+            double t1 = 0.0, t2 = 0.0;
+            for (int q = 0; q < SUB; ++q) {
+                t1 += pt[q * C + threadIdx.x].x;
+                t2 += pt[q * C + threadIdx.x].y;
+            }
+            pt[threadIdx.x] = make_double2((double)(float)t1, (double)(float)t2);
+        }
+    }
+    __syncthreads();
+    if (first && threadIdx.x == 0) {
+        double T1 = 0.0, T2 = 0.0;
+        for (int c = 0; c < C; ++c) {
+            T1 += pt[c].x;
+            T2 += pt[c].y;
+        }
+        *a.dw = (float)T1;
+        *a.db = (float)T2;
+    }
+    if (r0 >= total) return;
+    const int r1 = min(total, r0 + BN2_ROWS);
+    const float wv = *a.w;
+    const int lane = threadIdx.x % L, rg = threadIdx.x / L;
+    float mu[4], isd[4], m1[4], m2[4];
+    bool relu[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int ch = 4 * lane + i;
+        mu[i] = a.mean[ch];
+        isd[i] = 1.0f / a.std[ch];
+        m1[i] = sm1[ch];
+        m2[i] = sm2[ch];
+        relu[i] = ch >= a.relu_from;
+    }
+    float4 cs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cs[q] = f4_zero();
+    constexpr int U = RPT < 8 ? RPT : 8;
+#pragma unroll
+    for (int i0 = 0; i0 < RPT; i0 += U) {
+        float4 dz[U], yv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long r = min(r0 + rg + RG * (i0 + u), r1 - 1);
+            dz[u] = ld4(a.dz + r * C + 4 * lane);
+            yv[u] = ld4(a.y + r * C + 4 * lane);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = r0 + rg + RG * (i0 + u);
+            if (r >= r1) continue;
+            float4 d;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                f4c(d, k) = bn_bwd_dy_inv(f4c(yv[u], k), f4c(dz[u], k), mu[k], isd[k], wv, m1[k], m2[k],
+                                          a.training != 0, relu[k]);
+                f4c(cs[(i0 + u) / RPQ], k) += f4c(d, k);
+            }
+            *reinterpret_cast<float4*>(a.dy + (long long)r * C + 4 * lane) = d;
+        }
+    }
+    if (!a.dbpart) return;
+    // per-64-row-tile column sums of dY (the conv bias gradients), over the row groups in order
+    __shared__ float4 red[BN2_THREADS];
+    const int t64 = ceil_div(total, 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        red[threadIdx.x] = cs[q];
+        __syncthreads();
+        const int tq = blockIdx.x * 4 + q;
+        if (threadIdx.x < C && tq < t64) {
+            float t = 0.f;
+            for (int g = 0; g < RG; ++g) t += f4c(red[g * L + (threadIdx.x >> 2)], threadIdx.x & 3);
+            a.dbpart[(long long)tq * C + threadIdx.x] = t;
+        }
+        __syncthreads();
+    }
+}
+
+static bool bn2_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("HGNN_BN_BWD2");
+        return !e || e[0] != '0';
+    }();
+    return on;
+}
+
+template <int L>
+static void bn2_launch(const BnBwdArgs& a, hipStream_t s) {
+    const int t2 = ceil_div(a.cap_rows, BN2_ROWS);
+    hipLaunchKernelGGL(k_bn_bwd_part2<L>, dim3(t2), dim3(BN2_THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_bn_bwd_apply2<L>, dim3(t2), dim3(BN2_THREADS), 0, s, a);
+}
+
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     const int tiles = bn_bwd_tiles(a.cap_rows);
     const bool v4 = bn_vec4(a);
     // (c / 4 a power of two: the per-wave shuffle reduction pairs the lanes of one channel group)
     if (apply && v4 && (a.c == 4 || a.c == 8 || a.c == 16) && tiles <= BN_SMALL_TILES) {
         hipLaunchKernelGGL(k_bn_bwd_small, dim3(1), dim3(BN_SMALL_THREADS), 0, s, a);
+        HGNN_LAUNCH_CHECK();
+        return 0;
+    }
+    if (apply && v4 && tiles > 0 && bn2_enabled() && (a.c == 64 || a.c == 128 || a.c == 256)) {
+        if (a.c == 64) bn2_launch<16>(a, s);
+        else if (a.c == 128) bn2_launch<32>(a, s);
+        else bn2_launch<64>(a, s);
         HGNN_LAUNCH_CHECK();
         return 0;
     }

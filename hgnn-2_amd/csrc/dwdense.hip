@@ -26,15 +26,16 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // elements get an out-of-bounds offset and read 0), the padded-row values (readout vector, BN of
 // zero) come from per-chunk LDS constants afterwards.  Loads under per-lane conditions made hipcc
 // wait vmcnt(0) after each one: 132 full waits per launch, ~20 us per launch for ~4 us of work.
+// Slices [j0, j0 + J) of the G rows are staged (J = a.jt, or 1 for a per-slice block).
 template <int FC, int V>
 __device__ __forceinline__ void dw_stage(const DwDenseArgs& a, int b, int off, int nb, int npad, int f0, int fc,
-                                         float* Gs, float* Xs, int GP, const float* Rs, const float* Bmu,
-                                         const float* Bsc, const float* Bz) {
+                                         int j0, int J, float* Gs, float* Xs, int GP, const float* Rs,
+                                         const float* Bmu, const float* Bsc, const float* Bz) {
     typedef typename std::conditional<V == 4, float4, float>::type vt;
     constexpr unsigned OOB = 0x7ffffff0u;
     constexpr int XP = FC + 1;
     constexpr int FV = FC / V;
-    const int J = a.jt, F = a.f, nmax = a.nmax;
+    const int F = a.f, nmax = a.nmax;
     // wave-uniform descriptor inputs (readfirstlane): a descriptor the compiler cannot prove uniform
     // becomes a waterfall loop around every buffer load
     const int total = __builtin_amdgcn_readfirstlane(a.node_off[a.bs]);
@@ -63,7 +64,7 @@ __device__ __forceinline__ void dw_stage(const DwDenseArgs& a, int b, int off, i
             const int i = base + u * 256 + threadIdx.x;
             const int n = i / (J * FV), rem = i - n * (J * FV), j = rem / FV, f = (rem % FV) * V;
             const bool live = i < g_n && n < nb && f < fc;
-            v[u] = ld(rg, live ? (unsigned)((long long)(off + n) * a.lda + j * F + f0 + f) * 4u : OOB);
+            v[u] = ld(rg, live ? (unsigned)((long long)(off + n) * a.lda + (j0 + j) * F + f0 + f) * 4u : OOB);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -113,11 +114,16 @@ __device__ __forceinline__ void dw_stage(const DwDenseArgs& a, int b, int off, i
 // MAXI = (n-tile, m-tile, slice) items per wave kept in registers: sized to the
 // graph so the accumulators do not cap occupancy (5 x 16 AGPRs at Nmax <= 32,
 // where only 3 items exist, left one wave per SIMD)
-template <int FC, int MAXI>
+// JSPLIT: one block per (graph, slice) -- blockIdx.y is the slice; the block stages only that
+// slice's G rows (half the LDS, a third of the loads per block, 3x the blocks).  One block per
+// graph left ~18 us per launch at config 2 for ~4 us of traffic: the per-block chain of staging,
+// MFMA and read-modify-write was the whole kernel.
+template <int FC, int MAXI, bool JSPLIT>
 __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int b = blockIdx.x;
-    const int nmax = a.nmax, J = a.jt, F = a.f;
+    const int nmax = a.nmax, F = a.f;
+    const int J = JSPLIT ? 1 : a.jt, j0 = JSPLIT ? (int)blockIdx.y : 0, JA = a.jt;
     const int npad = (nmax + 31) / 32 * 32;
     const int tiles = npad / 32;
     const int nitems = tiles * tiles * J;
@@ -137,9 +143,10 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     const bool vec = !a.xdense && F % 4 == 0 && a.lda % 4 == 0 &&
                      ((reinterpret_cast<uintptr_t>(a.dA) | reinterpret_cast<uintptr_t>(a.xp)) & 15) == 0;
 
-    float* dWb = a.dW + (long long)b * nmax * nmax * J;
+    float* dWb = a.dW + (long long)b * nmax * nmax * JA;
     // block-uniform passes over the items; gridDim.y blocks of a graph share them
-    for (int base = blockIdx.y * 4 * MAXI; base < nitems; base += gridDim.y * 4 * MAXI) {
+    const int ystart = JSPLIT ? 0 : (int)blockIdx.y, ystep = JSPLIT ? 1 : (int)gridDim.y;
+    for (int base = ystart * 4 * MAXI; base < nitems; base += ystep * 4 * MAXI) {
     f32x16 acc[MAXI];
 #pragma unroll
     for (int q = 0; q < MAXI; ++q)
@@ -156,7 +163,7 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
                 float r = 0.f;
                 if (f < fc)
                     for (int o = 0; o < a.dim_out; ++o)
-                        r = fmaf(a.dout[b * a.dim_out + o], a.fcw[(long long)o * a.kfc + j * F + f0 + f], r);
+                        r = fmaf(a.dout[b * a.dim_out + o], a.fcw[(long long)o * a.kfc + (j0 + j) * F + f0 + f], r);
                 Rs[t] = r;
             }
         if (a.pmean)
@@ -168,10 +175,10 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
             }
         __syncthreads();
         if (vec)
-            dw_stage<FC, 4>(a, b, off, nb, npad, f0, fc, Gs, Xs, GP, a.dout ? Rs : nullptr,
+            dw_stage<FC, 4>(a, b, off, nb, npad, f0, fc, j0, J, Gs, Xs, GP, a.dout ? Rs : nullptr,
                             a.pmean ? Bmu : nullptr, Bsc, Bz);
         else
-            dw_stage<FC, 1>(a, b, off, nb, npad, f0, fc, Gs, Xs, GP, a.dout ? Rs : nullptr,
+            dw_stage<FC, 1>(a, b, off, nb, npad, f0, fc, j0, J, Gs, Xs, GP, a.dout ? Rs : nullptr,
                             a.pmean ? Bmu : nullptr, Bsc, Bz);
         __syncthreads();
 #pragma unroll
@@ -192,6 +199,7 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
         const int it = base + wv + 4 * q;
         if (it >= nitems) continue;
         const int j = it % J, tm = (it / J) % tiles, tn = it / (J * tiles);
+        const int jo = j0 + j;
         const int m = tm * 32 + l31;
         // read all 16 previous values before any store: a load-add-store per element
         // is serialised by the compiler (possible aliasing) into 16 memory round trips
@@ -200,7 +208,7 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int n = min(tn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, nmax - 1);
-            old[r] = dWb[((long long)n * nmax + min(m, nmax - 1)) * J + j];
+            old[r] = dWb[((long long)n * nmax + min(m, nmax - 1)) * JA + jo];
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -208,52 +216,72 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int n = tn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (n < nmax && m < nmax) dWb[((long long)n * nmax + m) * J + j] = old[r] + acc[q][r];
+            if (n < nmax && m < nmax) dWb[((long long)n * nmax + m) * JA + jo] = old[r] + acc[q][r];
         }
     }
     }
 }
 
-template <int FC, int MAXI>
+template <int FC, int MAXI, bool JS>
 static void allow_lds(size_t lds) {
     // dynamic LDS beyond 64 KB must be allowed per kernel (gfx950: 160 KB per CU)
     static bool done = false;
     if (!done && lds > 64 * 1024) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_dense<FC, MAXI>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_dense<FC, MAXI, JS>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         done = true;
     }
 }
 
-template <int FC>
+template <int FC, bool JS>
 static void launch_fc(const DwDenseArgs& a, int maxi, int gy, size_t lds, hipStream_t s) {
-    allow_lds<FC, 1>(lds);
-    allow_lds<FC, 3>(lds);
-    allow_lds<FC, 5>(lds);
-    if (maxi <= 1) hipLaunchKernelGGL((k_dw_dense<FC, 1>), dim3(a.bs, gy), dim3(256), lds, s, a);
-    else if (maxi <= 3) hipLaunchKernelGGL((k_dw_dense<FC, 3>), dim3(a.bs, gy), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL((k_dw_dense<FC, 5>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    allow_lds<FC, 1, JS>(lds);
+    allow_lds<FC, 3, JS>(lds);
+    allow_lds<FC, 5, JS>(lds);
+    if (maxi <= 1) hipLaunchKernelGGL((k_dw_dense<FC, 1, JS>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    else if (maxi <= 3) hipLaunchKernelGGL((k_dw_dense<FC, 3, JS>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((k_dw_dense<FC, 5, JS>), dim3(a.bs, gy), dim3(256), lds, s, a);
+}
+
+// HGNN_DW_JSPLIT=1: one block per (graph, slice).  Measured on the box (alternating bench runs):
+// 350 K vs 366 K graphs/s with one block per graph -- this kernel runs on the side stream, and 3x
+// the blocks crowd the main stream's backward more than the shorter kernel saves.  Off by default.
+static bool jsplit_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("HGNN_DW_JSPLIT");
+        return e && e[0] == '1';
+    }();
+    return on;
 }
 
 int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
     const int npad = (a.nmax + 31) / 32 * 32;
     // one F chunk when it fits (F = 2d = 128 at config 2): 19.1 -> 18.3 us per launch
     const int fc = npad <= 32 ? (a.f > 64 ? 128 : 64) : (npad <= 64 ? 32 : 16);
-    const size_t lds = sizeof(float) * ((size_t)npad * ((a.jt * fc + 1) + (fc + 1)) + (size_t)a.jt * fc + 3 * fc);
-    if (lds > 96 * 1024) return 2;
     const int tiles = npad / 32;
-    const int nitems = tiles * tiles * a.jt;
-    int maxi = ceil_div(nitems, 4), gy = 1;
-    if (a.bs < 256 && nitems > 4) {
-        // few graphs (cfg1: 32): one item per wave and the items' passes spread over blocks, so the
-        // grid is not a handful of long blocks (17 -> a few us per launch)
+    // large batches: one block per (graph, slice); few graphs (cfg1: 32): the items' passes of a
+    // graph spread over blocks instead, so the grid is not a handful of long blocks
+    const bool js = jsplit_enabled() && a.bs >= 256;
+    const int J = js ? 1 : a.jt;
+    const size_t lds = sizeof(float) * ((size_t)npad * ((J * fc + 1) + (fc + 1)) + (size_t)J * fc + 3 * fc);
+    if (lds > 96 * 1024) return 2;
+    const int nitems = tiles * tiles * J;
+    int maxi = ceil_div(nitems, 4), gy = js ? a.jt : 1;
+    if (!js && a.bs < 256 && nitems > 4) {
         maxi = 1;
         gy = ceil_div(nitems, 4);
     }
-    if (fc == 128) launch_fc<128>(a, maxi, gy, lds, s);
-    else if (fc == 64) launch_fc<64>(a, maxi, gy, lds, s);
-    else if (fc == 32) launch_fc<32>(a, maxi, gy, lds, s);
-    else launch_fc<16>(a, maxi, gy, lds, s);
+#define HGNN_DW_FC(JS)                                         \
+    if (fc == 128) launch_fc<128, JS>(a, maxi, gy, lds, s);    \
+    else if (fc == 64) launch_fc<64, JS>(a, maxi, gy, lds, s); \
+    else if (fc == 32) launch_fc<32, JS>(a, maxi, gy, lds, s); \
+    else launch_fc<16, JS>(a, maxi, gy, lds, s);
+    if (js) {
+        HGNN_DW_FC(true)
+    } else {
+        HGNN_DW_FC(false)
+    }
+#undef HGNN_DW_FC
     HGNN_LAUNCH_CHECK();
     return 0;
 }

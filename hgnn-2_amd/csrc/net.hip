@@ -856,7 +856,10 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     }
 
     SideStream* side = nullptr;
-    if (P.v2) TRY(side_stream(s, &side));
+    // HGNN_SIDE=0: the weight-gradient work stays on the main stream, with no events at all (a
+    // cross-stream event record / wait costs the main stream ~6-7 us of idle GPU per fork)
+    static const bool use_side = env_flag("HGNN_SIDE", true);
+    if (P.v2 && use_side) TRY(side_stream(s, &side));
     // dY and the bias partials alternate between two buffers, so the side stream's
     // dW of half i may still read its pair while the main stream runs half i+1.
     bool pending[2] = {false, false};
@@ -869,13 +872,15 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     auto fork_dw = [&](const Half& h, int cap, const int* tot, float* dyb, float* dbp, bool ndw_side,
                        float* dab, bool da_side = false) -> int {
         const int kc = dw3_kchunk(cap, P.c2, h.k);
-        HGNN_HOST_CHECK(hipEventRecord(side->fork[parity], s));
-        HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, side->fork[parity], 0));
+        if (side) {
+            HGNN_HOST_CHECK(hipEventRecord(side->fork[parity], s));
+            HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, side->fork[parity], 0));
+        }
         hipStream_t main_s = s;
         // HGNN_SERIAL_BWD=1 (diagnostics): everything on the main stream, so a kernel trace shows
         // each kernel's standalone duration
         static const bool serial = env_flag("HGNN_SERIAL_BWD", false);
-        if (!serial) s = side->s;  // TL records its timer events on the stream the kernel runs on
+        if (side && !serial) s = side->s;  // TL records its timer events on the stream the kernel runs on
         int r = 0;
         do {
             // fused backward: dX needs no dA, only the dense operator gradient does -- its G
@@ -888,10 +893,10 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
                                                at<float>(ws, P.slabs), s));
             TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, kc, P.c2, h.k, P.d, grads[h.pw_lin],
                                                    grads[h.pw_relu], dbp, grads[h.pb_lin], grads[h.pb_relu], s));
-            r = hipEventRecord(side->join[parity], s) == hipSuccess ? 0 : HGNN_ERR_HIP;
+            if (side) r = hipEventRecord(side->join[parity], s) == hipSuccess ? 0 : HGNN_ERR_HIP;
         } while (0);
         s = main_s;
-        pending[parity] = true;
+        pending[parity] = side != nullptr;
         return r;
     };
     // per-layer completion events (hgnn_net_backward_ex): recorded once the first half (in program
