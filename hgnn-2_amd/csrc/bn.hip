@@ -8,6 +8,8 @@
 // packed row.  The GEMM epilogue already produced per-64-row-tile (count,
 // mean, M2); they are combined in fp64 (Chan) per channel, which keeps the
 // two-pass accuracy of the reference without a second pass over Y.
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace hgnn {
@@ -915,6 +917,140 @@ int launch_readout_bwd_da(const float* dout, const int* node_off, int bs, int ca
     (void)cap_rows;
     (void)total_rows;
     hipLaunchKernelGGL(k_readout_bwd_da, dim3(bs), dim3(256), 0, s, dout, node_off, fcw, dim_out, k, da);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// ---- Readout backward without the [rows][K] gradient buffer.  The readout sums fc(x1) over the
+// nodes of a graph (layers_mnb.py:385-386), so the gradient of x1 at every node n of graph b is
+// the same row R_b = dout[b] . fcw.  The transposed gathers of the last layer therefore reduce
+// to the row's coefficient sums times R_b:
+//   G rows (graph_oper(W, X)^T):  dX[r, c] (+)= sum_j (sum_e v_j(e)) R_b[j C + c]
+//   P rows (P_multi(Pm/Pd, XL)^T): dXL[r, c] (+)= (sum_e pm) R_b[Kg + c] + (sum_e pd) R_b[Kg + Cp + c]
+// (entries of a row only reference columns of the same graph), and the dense operator gradient
+// of the readout is dW[b, n, m, j] = sum_f R_b[j F + f] X[m, f] for every n < Nmax.  The
+// coefficient sums are exact for the reference's operators (small dyadic values), so only the
+// order of the final products differs from the gather form.
+__device__ __forceinline__ float readout_row(const float* __restrict__ dout, const float* __restrict__ fcw,
+                                             int dim_out, int k, int b, int col) {
+    float v = 0.f;
+    for (int o = 0; o < dim_out; ++o) v = fmaf(dout[b * dim_out + o], fcw[(long long)o * k + col], v);
+    return v;
+}
+
+// One block per (graph, kind): blockIdx.y = 0 -> the graph's node rows (G), 1 -> its edge rows (P).
+// A thread per row sums the row's coefficients (4 entries in flight), then the block writes the
+// rows coalesced over (row, channel).
+constexpr int RA_THREADS = 256;
+
+__global__ void __launch_bounds__(RA_THREADS) k_readout_agg_bwd(ReadoutAggArgs a) {
+    const int b = blockIdx.x;
+    const bool g = blockIdx.y == 0;
+    float* out = g ? a.g_out : a.p_out;
+    if (!out) return;
+    extern __shared__ float sh[];
+    const int ns = g ? a.jt : 2;
+    const int C = g ? a.cg : a.cp;
+    const int* off = g ? a.node_off : a.edge_off;
+    const int r0 = off[b], nr = off[b + 1] - r0;
+    float* R = sh;                // [ns C]: R_b over the gathered columns
+    float* CS = sh + ns * C;      // [rows][ns]
+    const int kb = g ? 0 : a.jt * a.cg;
+    for (int t = threadIdx.x; t < ns * C; t += RA_THREADS)
+        R[t] = readout_row(a.dout, a.fcw, a.dim_out, a.k, b, kb + t);
+    const StructView L = g ? a.g : a.p;
+    for (int i = threadIdx.x; i < nr; i += RA_THREADS) {
+        const RowInfo ri = L.rows[r0 + i];
+        float cs[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cs[j] = 0.f;
+        int e = 0;
+        for (; e + 4 <= ri.count; e += 4) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(L.entries + (long long)(ri.start + e + u) * L.stride);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                cs[0] += v[u].y;
+                cs[1] += v[u].z;
+                cs[2] += v[u].w;
+                for (int j = 3; j < ns; ++j) cs[j] += L.entries[(long long)(ri.start + e + u) * L.stride + 1 + j];
+            }
+        }
+        for (; e < ri.count; ++e) {
+            const float* en = L.entries + (long long)(ri.start + e) * L.stride;
+            for (int j = 0; j < ns; ++j) cs[j] += en[1 + j];
+        }
+        for (int j = 0; j < ns; ++j) CS[i * ns + j] = cs[j];
+    }
+    __syncthreads();
+    const int acc = g ? a.g_acc : a.p_acc;
+    for (int i = threadIdx.x; i < nr * C; i += RA_THREADS) {
+        const int r = i / C, c = i % C;
+        float v = acc ? out[(long long)(r0 + r) * C + c] : 0.f;
+        for (int j = 0; j < ns; ++j) v = fmaf(CS[r * ns + j], R[j * C + c], v);
+        out[(long long)(r0 + r) * C + c] = v;
+    }
+}
+
+int launch_readout_agg_bwd(const ReadoutAggArgs& a, hipStream_t s) {
+    if (a.jt > 8 || (!a.g_out && !a.p_out)) return a.jt > 8 ? HGNN_ERR_UNSUPPORTED : 0;
+    const int maxrows = a.p_out ? (a.p_cap + a.bs - 1) / a.bs : 0;  // rows per graph <= emax
+    const int grow = (a.g_cap + a.bs - 1) / a.bs;
+    const size_t lds = sizeof(float) * (size_t)std::max(a.jt * a.cg + grow * a.jt, 2 * a.cp + maxrows * 2);
+    if (lds > 64 * 1024) return HGNN_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(k_readout_agg_bwd, dim3(a.bs, a.p_out ? 2 : 1), dim3(RA_THREADS), lds, s, a);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// dW[b, n, m, j] (+)= u_b[m, j] = sum_f R_b[j F + f] X[m, f] for all n < Nmax: one block per graph,
+// u in LDS, then written to every row n.  X: BN of the producer applied on load, the BN of 0 at
+// padded m (as k_dw_dense); the dense layer input (xdense) as stored.
+__global__ void __launch_bounds__(256) k_dw_readout(DwDenseArgs a) {
+    extern __shared__ float sh[];
+    const int b = blockIdx.x;
+    const int nmax = a.nmax, J = a.jt, F = a.f, FP = F + 1;
+    float* R = sh;              // [J F]
+    float* X = sh + J * F;      // [nmax][F + 1]
+    float* U = X + nmax * FP;   // [nmax J]
+    const int off = a.node_off[b], nb = a.node_off[b + 1] - off;
+    const float wv = a.pw ? *a.pw : 0.f, bv = a.pb ? *a.pb : 0.f;
+    for (int t = threadIdx.x; t < J * F; t += 256)
+        R[t] = readout_row(a.dout, a.fcw, a.dim_out, a.kfc, b, t);
+    for (int t = threadIdx.x; t < nmax * F; t += 256) {  // coalesced over f
+        const int m = t / F, f = t % F;
+        float x;
+        if (a.xdense) {
+            x = a.xdense[((long long)b * F + f) * nmax + m];
+        } else if (m < nb) {
+            x = a.xp[(long long)(off + m) * F + f];
+            if (a.pmean) x = bn_z_s(x, a.pmean[f], bn_scale(wv, a.pstd[f]), bv);
+        } else {
+            x = a.pmean ? bn_z(0.f, a.pmean[f], a.pstd[f], wv, bv) : 0.f;
+        }
+        X[m * FP + f] = x;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < nmax * J; t += 256) {
+        const int m = t / J, j = t % J;
+        float u = 0.f;
+        for (int f = 0; f < F; ++f) u = fmaf(R[j * F + f], X[m * FP + f], u);
+        U[t] = u;
+    }
+    __syncthreads();
+    float* dWb = a.dW + (long long)b * nmax * nmax * J;
+    const int per = nmax * J;
+    for (long long i = threadIdx.x; i < (long long)nmax * per; i += 256) {
+        const float u = U[i % per];
+        dWb[i] = a.accumulate ? dWb[i] + u : u;
+    }
+}
+
+int launch_dw_readout(const DwDenseArgs& a, hipStream_t s) {
+    const size_t lds = sizeof(float) * ((size_t)a.jt * a.f + (size_t)a.nmax * (a.f + 1) + (size_t)a.nmax * a.jt);
+    if (lds > 64 * 1024 || !a.dout) return HGNN_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(k_dw_readout, dim3(a.bs), dim3(256), lds, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

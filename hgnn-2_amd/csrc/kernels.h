@@ -350,5 +350,28 @@ int launch_readout_bwd_da(const float* dout, const int* node_off, int bs, int ca
 int launch_readout_bwd_params(const float* dout, const float* colsum, int bs, int nmax,
                               int dim_out, int k, float* dfcw, float* dfcb, void* scratch, hipStream_t s);
 size_t readout_bwd_scratch_bytes(int dim_out, int k);
+// The last layer's transposed gathers straight from the readout gradient row R_b = dout[b] . fcw
+// (no [rows][K] gradient buffer): G rows -> g_out (node features), P rows -> p_out (edge features).
+struct ReadoutAggArgs {
+    const float* dout;
+    const float* fcw;
+    int dim_out, k;          // k = fc input width (jt * cg + 2 * cp)
+    int jt, cg, cp, bs;
+    const int* node_off;
+    const int* edge_off;
+    StructView g;            // S_WT (node rows)
+    const int* g_total;
+    int g_cap;
+    float* g_out;            // null: no G gather
+    int g_acc;
+    StructView p;            // S_PE (edge rows)
+    const int* p_total;
+    int p_cap;
+    float* p_out;            // null: no P gather
+    int p_acc;
+};
+int launch_readout_agg_bwd(const ReadoutAggArgs& a, hipStream_t s);
+// dW of the readout layer's graph_oper: dW[b, n, m, j] (+)= sum_f R_b[j F + f] X[m, f], every n
+int launch_dw_readout(const DwDenseArgs& a, hipStream_t s);
 
 }  // namespace hgnn

@@ -779,7 +779,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     const bool need_dw = c->need_dw != 0;
     if (need_dw && (!dW || !in || !in->d_X || csr)) return HGNN_ERR_ARG;
     // dense dW contribution of one graph_oper(W, X_l): G block of dA (node rows) x X_l
-    auto dw_dense = [&](int gin, const float* da, int lda, bool readout, int accumulate) -> int {
+    auto dw_args = [&](int gin, const float* da, int lda, bool readout, int accumulate) -> DwDenseArgs {
         DwDenseArgs a{};
         a.dA = da;
         a.lda = lda;
@@ -806,13 +806,47 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         a.nmax = c->nmax;
         a.dW = dW;
         a.accumulate = accumulate;
-        return launch_dw_dense(a, s);
+        return a;
+    };
+    auto dw_dense = [&](int gin, const float* da, int lda, bool readout, int accumulate) -> int {
+        return launch_dw_dense(dw_args(gin, da, lda, readout, accumulate), s);
     };
 
     // readout
     TL(HGNN_K_READOUT, launch_readout_bwd_params(dout, at<float>(ws, P.colsum), c->bs, c->nmax, c->dim_out, P.k_last,
                                   grads[P.p_fcw], grads[P.p_fcb], at<void>(ws, P.rb_scratch), s));
-    if (needs_grad(P.last_gin) || needs_grad(P.last_pin) || need_dw) {
+    // HGNN_READOUT_ROW=0: the readout gradient materialised as a [rows][K] buffer and gathered
+    static const bool ro_row = env_flag("HGNN_READOUT_ROW", true);
+    if (ro_row && P.jt <= 8 && (needs_grad(P.last_gin) || needs_grad(P.last_pin) || need_dw)) {
+        if (need_dw) TL(HGNN_K_DW_DENSE, launch_dw_readout(dw_args(P.last_gin, nullptr, 0, true, 0), s));
+        const bool lg = needs_grad(P.last_gin), lp = needs_grad(P.last_pin);
+        ReadoutAggArgs ra{};
+        ra.dout = dout;
+        ra.fcw = prm[P.p_fcw];
+        ra.dim_out = c->dim_out;
+        ra.k = P.k_last;
+        ra.jt = P.jt;
+        ra.cg = P.feats[P.last_gin].c;
+        ra.cp = P.last_pin >= 0 ? P.feats[P.last_pin].c : 0;
+        ra.bs = c->bs;
+        ra.node_off = m.node_off;
+        ra.edge_off = m.edge_off;
+        ra.g = src.v[S_WT];
+        ra.g_total = tot_n;
+        ra.g_cap = P.cap_n;
+        ra.g_out = lg ? at<float>(ws, P.feats[P.last_gin].grad) : nullptr;
+        ra.g_acc = init[P.last_gin];
+        if (lp) {
+            ra.p = src.v[S_PE];
+            ra.p_total = tot_e;
+            ra.p_cap = P.cap_e;
+            ra.p_out = at<float>(ws, P.feats[P.last_pin].grad);
+            ra.p_acc = init[P.last_pin];
+        }
+        if (lg || lp) TL(HGNN_K_AGG_BWD, launch_readout_agg_bwd(ra, s));
+        if (lg) init[P.last_gin] = 1;
+        if (lp) init[P.last_pin] = 1;
+    } else if (needs_grad(P.last_gin) || needs_grad(P.last_pin) || need_dw) {
         float* da = at<float>(ws, P.da);
         TL(HGNN_K_READOUT, launch_readout_bwd_da(dout, m.node_off, c->bs, P.cap_n, tot_n, prm[P.p_fcw], c->dim_out, P.k_last,
                                   da, s));
