@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round-end measurement set: profile_round.sh (kernel trace/stats, PMC traffic, SQ wave states,
+# CCN profiles, all configs), then the default bench line (CPU baseline + parity leg) reading the
+# fresh PMC traffic.  Results under gpurun_out/ (copied into profiles/ by the caller).
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+bash tools/profile_round.sh || exit $?
+cp gpurun_out/pmc_traffic.json profiles/pmc_traffic.json || exit $?
+timeout -k 10 600 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -5 gpurun_out/bench_default.err; exit 1; }
+tail -1 gpurun_out/bench_default.json | cut -c1-600
