@@ -49,6 +49,7 @@ struct G3 {
     float* dbpart;      // [tiles][k] column sums of dY
     float* dw_s;        // BN scalar grads
     float* db_s;
+    int xcd;            // E3_FWD: the column tiles of a row tile on one XCD (gridDim.x % 8 == 0)
 };
 
 template <int BM, int BN, int BK, int WGM, int WGN, int EPI>
@@ -64,7 +65,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv / WGN, wn = wv % WGN;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (EPI == E3_FWD && p.xcd) {
+        // blocks b and b + 8 share an XCD's L2 (MI355X_MICROARCH.md): the gridDim.y column tiles
+        // of one row tile get equal b % 8, so its A rows (the wide aggregate) come from HBM once
+        const int L = blockIdx.x + gridDim.x * blockIdx.y, j = L >> 3;
+        by = j % gridDim.y;
+        bx = (L & 7) + 8 * (j / gridDim.y);
+    }
+    const int m0 = bx * BM, n0 = by * BN;
     const int Mv = p.m_valid ? *p.m_valid : p.m_cap;
     if (m0 >= Mv && !(EPI == E3_DA_BN && blockIdx.x == 0 && blockIdx.y == 0)) return;
     const int K = p.k, N = p.n;
@@ -328,7 +337,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
                     const int col = wn * TN + j * 32 + l31;
                     const int gn = n0 + col;
                     if (gn < N) {
-                        float* pp = p.bn_part + ((long long)blockIdx.x * N + gn) * 3;
+                        float* pp = p.bn_part + ((long long)bx * N + gn) * 3;
                         pp[0] = (float)cnt[j];
                         pp[1] = mean[j];
                         pp[2] = red[col] + red[BN + col];
@@ -364,7 +373,8 @@ template <int BM, int BN, int BK, int WGM, int WGN>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __restrict__ A, int lda,
                                                              const float* __restrict__ B, int ldb,
                                                              float* __restrict__ slabs, int M, int N,
-                                                             const int* __restrict__ r_valid, int kchunk) {
+                                                             const int* __restrict__ r_valid, int kchunk,
+                                                             int xcd_remap) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 32, AN = TN / 32;
     constexpr int PA = BM + 4, PB = BN + 4;
@@ -375,9 +385,21 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
     __shared__ __attribute__((aligned(16))) float Bs[2][BK * PB];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv / WGN, wn = wv % WGN;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (xcd_remap) {
+        // the output tiles of one row chunk on one XCD (blocks b and b + 8 share an XCD's L2,
+        // MI355X_MICROARCH.md), so the chunk's dY rows are fetched from HBM once, not once per
+        // tile; gridDim.z is a multiple of 8 here
+        const int T = gridDim.x * gridDim.y;
+        const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int j = L >> 3, t = j % T;
+        bz = (L & 7) + 8 * (j / T);
+        bx = t % gridDim.x;
+        by = t / gridDim.x;
+    }
+    const int m0 = bx * BM, n0 = by * BN;
     const int R = *r_valid;
-    const int kbeg = blockIdx.z * kchunk, kend = min(R, kbeg + kchunk);
+    const int kbeg = bz * kchunk, kend = min(R, kbeg + kchunk);
     if (kbeg >= kend) return;  // the reduce only sums the chunks that hold rows
     float4 ra[AF4], rb[BF4];
     auto load = [&](int k0) {
@@ -453,7 +475,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
         }
         __syncthreads();
     }
-    float* out = slabs + (long long)blockIdx.z * M * N;
+    float* out = slabs + (long long)bz * M * N;
 #pragma unroll
     for (int i = 0; i < AM; ++i)
 #pragma unroll
@@ -517,7 +539,7 @@ template <int BM, int BN, int WGM, int WGN>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm5(const float* __restrict__ A, int lda,
                                                           const float* __restrict__ B, int ldb,
                                                           const int* __restrict__ m_valid, int m_cap, int N, int K,
-                                                          float* __restrict__ C, int ldc) {
+                                                          float* __restrict__ C, int ldc, int xcd) {
     constexpr int BK = 32, NW = WGM * WGN, ST = 2;
     constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 16, AN = TN / 16;
     constexpr int AI = BM * BK * 4 / 1024, BI = BN * BK * 4 / 1024;  // 1-KB wave instructions per stage
@@ -529,7 +551,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm5(const float* __restric
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wv / WGN, wn = wv % WGN;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (xcd) {  // the column tiles of a row tile on one XCD (see k_gemm3); gridDim.x % 8 == 0
+        const int L = blockIdx.x + gridDim.x * blockIdx.y, j = L >> 3;
+        by = j % gridDim.y;
+        bx = (L & 7) + 8 * (j / gridDim.y);
+    }
+    const int m0 = bx * BM, n0 = by * BN;
     if (m0 >= M) return;
     constexpr unsigned OOB = 0x7ffffff0u;
     const i32x4 ra = rsrc4(A, M * lda * 4), rb = rsrc4(B, N * ldb * 4);
@@ -680,9 +708,14 @@ int launch_gemm3_da_bn(const BnBwdArgs& bn, const int* m_valid, int m_cap, int o
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
                     int kchunk, float* slabs, hipStream_t s) {
     if (r_cap <= 0) return 0;
+    static const bool xcd = [] {
+        const char* e = getenv("HGNN_DW_XCD");
+        return !e || e[0] != '0';
+    }();
     const int z = ceil_div(r_cap, kchunk);
-    hipLaunchKernelGGL((k_gemm3_tn<128, 128, 32, 4, 2>), dim3(ceil_div(o, 128), ceil_div(k, 128), z), dim3(512), 0, s,
-                       dy, lddy, a, lda, slabs, o, k, r_valid, kchunk);
+    const int zg = xcd ? ceil_div(z, 8) * 8 : z;  // padded chunks exit at once (no rows)
+    hipLaunchKernelGGL((k_gemm3_tn<128, 128, 32, 4, 2>), dim3(ceil_div(o, 128), ceil_div(k, 128), zg), dim3(512), 0, s,
+                       dy, lddy, a, lda, slabs, o, k, r_valid, kchunk, xcd ? 1 : 0);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -712,14 +745,19 @@ int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int
     p.bias = bias;
     p.relu_from = relu_from;
     p.bn_part = bn_part;
+    static const bool xcd = [] {
+        const char* e = getenv("HGNN_FWD_XCD");
+        return !e || e[0] != '0';
+    }();
+    const int bn = n <= 128 ? 64 : 128;
+    p.xcd = xcd && ceil_div(n, bn) > 1;
+    const int gx = p.xcd ? ceil_div(ceil_div(m_cap, 64), 8) * 8 : ceil_div(m_cap, 64);  // padded tiles exit
     if (n <= 128) {
         // 64-column tiles up to 2d = 128: twice the blocks of 64 x 128 tiles, measured (round-1 GEMM lab)
         // edge forward 47.7 -> 40.7 us, node forward 34 -> 28 us
-        hipLaunchKernelGGL((k_gemm3<64, 64, 32, 2, 2, E3_FWD>), dim3(ceil_div(m_cap, 64), ceil_div(n, 64)), dim3(256),
-                           0, s, p);
+        hipLaunchKernelGGL((k_gemm3<64, 64, 32, 2, 2, E3_FWD>), dim3(gx, ceil_div(n, 64)), dim3(256), 0, s, p);
     } else {
-        hipLaunchKernelGGL((k_gemm3<64, 128, 32, 2, 2, E3_FWD>), dim3(ceil_div(m_cap, 64), ceil_div(n, 128)),
-                           dim3(256), 0, s, p);
+        hipLaunchKernelGGL((k_gemm3<64, 128, 32, 2, 2, E3_FWD>), dim3(gx, ceil_div(n, 128)), dim3(256), 0, s, p);
     }
     HGNN_LAUNCH_CHECK();
     return 0;
@@ -737,8 +775,13 @@ int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, in
     }();
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
     if (dma && lddy % 4 == 0 && ldw % 4 == 0 && al(dy) && al(wt)) {
-        hipLaunchKernelGGL((k_gemm5<64, 64, 2, 2>), dim3(ceil_div(m_cap, 64), ceil_div(kout, 64)), dim3(256), 0, s,
-                           dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda);
+        static const bool xcd = [] {
+            const char* e = getenv("HGNN_DA_XCD");
+            return !e || e[0] != '0';
+        }();
+        const int gx = xcd ? ceil_div(ceil_div(m_cap, 64), 8) * 8 : ceil_div(m_cap, 64);
+        hipLaunchKernelGGL((k_gemm5<64, 64, 2, 2>), dim3(gx, ceil_div(kout, 64)), dim3(256), 0, s,
+                           dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda, xcd ? 1 : 0);
         HGNN_LAUNCH_CHECK();
         return 0;
     }
