@@ -788,6 +788,155 @@ __global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_apply2(BnBwdArgs a) {
     }
 }
 
+// ---- The same two-launch BN backward for narrow channel counts (c = 4L, L in {1, 2, 4}: the
+// GNN_simple layers of config 1).  256 rows per block, one row per lane group (256 L threads),
+// and the row-group sums as wave shuffles + a sum over the block's waves instead of a serial walk
+// over 256 row groups.  Replaces the single-block k_bn_bwd_small (18.6 us per launch at config 1:
+// one CU does all the work).
+template <int L>
+__device__ __forceinline__ float4 wave_rows_sum4(float4 v) {
+    // sum over the lanes of a wave holding the same channel group (lanes t, t + L, t + 2L, ...)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int o = 32; o >= L; o >>= 1) f4c(v, k) += __shfl_xor(f4c(v, k), o, 64);
+    return v;
+}
+
+template <int L>
+__global__ void __launch_bounds__(256 * L) k_bn_bwd_part2s(BnBwdArgs a) {
+    constexpr int NT = 256 * L, C = 4 * L, NW = NT / 64;
+    const int total = *a.total_rows;
+    const int r0 = blockIdx.x * BN2_ROWS;
+    if (r0 >= total) return;
+    const float wv = *a.w;
+    const int lane = threadIdx.x % L, r = r0 + threadIdx.x / L;
+    float4 st[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[j] = f4_zero();
+    if (r < total) {
+        float4 dz = ld4(a.dz + (long long)r * C + 4 * lane), yv = ld4(a.y + (long long)r * C + 4 * lane);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float mu = a.mean[4 * lane + k], isd = 1.0f / a.std[4 * lane + k];
+            const float h = (f4c(yv, k) - mu) * isd;
+            const float d = f4c(dz, k);
+            const float g = wv * d;
+            f4c(st[0], k) = g;
+            f4c(st[1], k) = g * h;
+            f4c(st[2], k) = d * h;
+            f4c(st[3], k) = d;
+        }
+    }
+    __shared__ float4 wp[4][NW][L];
+    const int w = threadIdx.x >> 6, wl = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float4 t = wave_rows_sum4<L>(st[j]);
+        if (wl < L) wp[j][w][wl] = t;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < C) {
+        const int ch = threadIdx.x;
+        float out[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float t = 0.f;
+            for (int q = 0; q < NW; ++q) t += f4c(wp[j][q][ch >> 2], ch & 3);
+            out[j] = t;
+        }
+        *reinterpret_cast<float4*>(a.part + ((long long)blockIdx.x * C + ch) * 4) =
+            make_float4(out[0], out[1], out[2], out[3]);
+    }
+}
+
+template <int L>
+__global__ void __launch_bounds__(256 * L) k_bn_bwd_apply2s(BnBwdArgs a) {
+    constexpr int NT = 256 * L, C = 4 * L, NW = NT / 64, SUB = NT / C;
+    const int total = *a.total_rows;
+    const int r0 = blockIdx.x * BN2_ROWS;
+    const bool first = blockIdx.x == 0;
+    if (r0 >= total && !first) return;
+    const int tiles = ceil_div(total, BN2_ROWS);
+    __shared__ double2 pr[NT];
+    __shared__ double2 pt[NT];
+    __shared__ float sm1[C], sm2[C];
+    {
+        const int ch = threadIdx.x % C, sub = threadIdx.x / C;
+        double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+        for (int t = sub; t < tiles; t += SUB) {
+            const float4 q = ld4(a.part + ((long long)t * C + ch) * 4);
+            v0 += (double)q.x;
+            v1 += (double)q.y;
+            v2 += (double)q.z;
+            v3 += (double)q.w;
+        }
+        pr[threadIdx.x] = make_double2(v0, v1);
+        pt[threadIdx.x] = make_double2(v2, v3);
+    }
+    __syncthreads();
+    const float inv_n = total > 0 ? 1.0f / (float)total : 0.f;
+    if ((int)threadIdx.x < C) {
+        double s1 = 0.0, s2 = 0.0, t1 = 0.0, t2 = 0.0;
+        for (int q = 0; q < SUB; ++q) {
+            s1 += pr[q * C + threadIdx.x].x;
+            s2 += pr[q * C + threadIdx.x].y;
+            t1 += pt[q * C + threadIdx.x].x;
+            t2 += pt[q * C + threadIdx.x].y;
+        }
+        sm1[threadIdx.x] = (float)s1 * inv_n;
+        sm2[threadIdx.x] = (float)s2 * inv_n;
+        if (first) pt[threadIdx.x] = make_double2((double)(float)t1, (double)(float)t2);
+    }
+    __syncthreads();
+    if (first && threadIdx.x == 0) {
+        double T1 = 0.0, T2 = 0.0;
+        for (int c = 0; c < C; ++c) {
+            T1 += pt[c].x;
+            T2 += pt[c].y;
+        }
+        *a.dw = (float)T1;
+        *a.db = (float)T2;
+    }
+    if (r0 >= total) return;
+    const float wv = *a.w;
+    const int lane = threadIdx.x % L, r = r0 + threadIdx.x / L;
+    float4 d = f4_zero();
+    if (r < total) {
+        float4 dz = ld4(a.dz + (long long)r * C + 4 * lane), yv = ld4(a.y + (long long)r * C + 4 * lane);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int ch = 4 * lane + k;
+            f4c(d, k) = bn_bwd_dy_inv(f4c(yv, k), f4c(dz, k), a.mean[ch], 1.0f / a.std[ch], wv, sm1[ch], sm2[ch],
+                                      a.training != 0, ch >= a.relu_from);
+        }
+        *reinterpret_cast<float4*>(a.dy + (long long)r * C + 4 * lane) = d;
+    }
+    if (!a.dbpart) return;
+    // per-64-row-tile column sums of dY: a tile is L consecutive waves
+    __shared__ float4 wd[NW][L];
+    const int w = threadIdx.x >> 6, wl = threadIdx.x & 63;
+    const float4 t = wave_rows_sum4<L>(d);
+    if (wl < L) wd[w][wl] = t;
+    __syncthreads();
+    const int t64 = ceil_div(total, 64);
+    if ((int)threadIdx.x < 4 * C) {
+        const int q = threadIdx.x / C, ch = threadIdx.x % C, tq = blockIdx.x * 4 + q;
+        if (tq < t64) {
+            float acc = 0.f;
+            for (int u = 0; u < L; ++u) acc += f4c(wd[q * L + u][ch >> 2], ch & 3);
+            a.dbpart[(long long)tq * C + ch] = acc;
+        }
+    }
+}
+
+template <int L>
+static void bn2s_launch(const BnBwdArgs& a, hipStream_t s) {
+    const int t2 = ceil_div(a.cap_rows, BN2_ROWS);
+    hipLaunchKernelGGL(k_bn_bwd_part2s<L>, dim3(t2), dim3(256 * L), 0, s, a);
+    hipLaunchKernelGGL(k_bn_bwd_apply2s<L>, dim3(t2), dim3(256 * L), 0, s, a);
+}
+
 static bool bn2_enabled() {
     static const bool on = [] {
         const char* e = getenv("HGNN_BN_BWD2");
@@ -807,6 +956,18 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     const int tiles = bn_bwd_tiles(a.cap_rows);
     const bool v4 = bn_vec4(a);
     // (c / 4 a power of two: the per-wave shuffle reduction pairs the lanes of one channel group)
+    // HGNN_BN_SMALL=1: the single-block k_bn_bwd_small instead of the two-launch narrow form
+    static const bool one_block = [] {
+        const char* e = getenv("HGNN_BN_SMALL");
+        return e && e[0] == '1';
+    }();
+    if (apply && v4 && !one_block && bn2_enabled() && tiles > 0 && (a.c == 4 || a.c == 8 || a.c == 16)) {
+        if (a.c == 4) bn2s_launch<1>(a, s);
+        else if (a.c == 8) bn2s_launch<2>(a, s);
+        else bn2s_launch<4>(a, s);
+        HGNN_LAUNCH_CHECK();
+        return 0;
+    }
     if (apply && v4 && (a.c == 4 || a.c == 8 || a.c == 16) && tiles <= BN_SMALL_TILES) {
         hipLaunchKernelGGL(k_bn_bwd_small, dim3(1), dim3(BN_SMALL_THREADS), 0, s, a);
         HGNN_LAUNCH_CHECK();

@@ -254,7 +254,61 @@ static bool jsplit_enabled() {
     return on;
 }
 
+// Narrow inputs (F <= 16: layer 0's node features, the GNN_simple layers of config 1): the outer
+// products are a handful of FMAs per output, so one block per graph computes them straight from
+// LDS copies of G and X -- no 32-wide MFMA tiles padded from F = 4 or 5 to 32 channels.  Same
+// padded-position values as k_dw_dense (dG = 0 at padded n outside the readout, the BN of 0 at
+// padded m); f summed in order.
+__global__ void __launch_bounds__(256) k_dw_dense_narrow(DwDenseArgs a) {
+    extern __shared__ float sm[];
+    const int b = blockIdx.x;
+    const int nmax = a.nmax, J = a.jt, F = a.f, JF = J * F;
+    float* G = sm;               // [nmax][J F]
+    float* X = sm + nmax * JF;   // [nmax][F]
+    const int off = a.node_off[b], nb = a.node_off[b + 1] - off;
+    const float pw = a.pmean ? *a.pw : 0.f, pb = a.pmean ? *a.pb : 0.f;
+    for (int i = threadIdx.x; i < nmax * JF; i += 256) {
+        const int n = i / JF, q = i - n * JF;
+        G[i] = n < nb ? a.dA[(long long)(off + n) * a.lda + q] : 0.f;
+    }
+    for (int i = threadIdx.x; i < nmax * F; i += 256) {
+        const int m = i / F, f = i - m * F;
+        float x;
+        if (a.xdense) x = a.xdense[((long long)b * F + f) * nmax + m];
+        else if (m < nb) {
+            x = a.xp[(long long)(off + m) * F + f];
+            if (a.pmean) x = bn_z_s(x, a.pmean[f], bn_scale(pw, a.pstd[f]), pb);
+        } else {
+            x = a.pmean ? bn_z(0.f, a.pmean[f], a.pstd[f], pw, pb) : 0.f;
+        }
+        X[i] = x;
+    }
+    __syncthreads();
+    float* dWb = a.dW + (long long)b * nmax * nmax * J;
+    const int tot = nmax * nmax * J;
+    for (int i = threadIdx.x; i < tot; i += 256) {
+        const int n = i / (nmax * J), m = (i / J) % nmax, j = i % J;
+        const float* g = G + n * JF + j * F;
+        const float* x = X + m * F;
+        float v = 0.f;
+        for (int f = 0; f < F; ++f) v = fmaf(g[f], x[f], v);
+        dWb[i] = a.accumulate ? dWb[i] + v : v;
+    }
+}
+
 int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
+    static const bool narrow_ok = [] {
+        const char* e = getenv("HGNN_DW_NARROW");
+        return !e || e[0] != '0';
+    }();
+    if (narrow_ok && a.f <= 16 && !a.dout) {
+        const size_t lds = sizeof(float) * (size_t)a.nmax * (a.jt * a.f + a.f);
+        if (lds <= 64 * 1024) {
+            hipLaunchKernelGGL(k_dw_dense_narrow, dim3(a.bs), dim3(256), lds, s, a);
+            HGNN_LAUNCH_CHECK();
+            return 0;
+        }
+    }
     const int npad = (a.nmax + 31) / 32 * 32;
     // one F chunk when it fits (F = 2d = 128 at config 2): 19.1 -> 18.3 us per launch
     const int fc = npad <= 32 ? (a.f > 64 ? 128 : 64) : (npad <= 64 ? 32 : 16);
