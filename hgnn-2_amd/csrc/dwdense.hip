@@ -14,6 +14,7 @@
 // done with v_mfma_f32_32x32x2_f32 on 32x32 tiles of (n, m): one workgroup per
 // graph stages the graph's G and X rows in LDS (F in chunks), each wave owns a
 // few (n-tile, m-tile, j) items.
+#include <algorithm>
 #include <type_traits>
 
 #include "kernels.h"
@@ -286,7 +287,8 @@ __global__ void __launch_bounds__(256) k_dw_dense_narrow(DwDenseArgs a) {
     __syncthreads();
     float* dWb = a.dW + (long long)b * nmax * nmax * J;
     const int tot = nmax * nmax * J;
-    for (int i = threadIdx.x; i < tot; i += 256) {
+    // gridDim.y blocks of a graph split its outputs (few graphs: cfg1's 32 would be 32 blocks)
+    for (int i = blockIdx.y * 256 + threadIdx.x; i < tot; i += 256 * gridDim.y) {
         const int n = i / (nmax * J), m = (i / J) % nmax, j = i % J;
         const float* g = G + n * JF + j * F;
         const float* x = X + m * F;
@@ -304,7 +306,8 @@ int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
     if (narrow_ok && a.f <= 16 && !a.dout) {
         const size_t lds = sizeof(float) * (size_t)a.nmax * (a.jt * a.f + a.f);
         if (lds <= 64 * 1024) {
-            hipLaunchKernelGGL(k_dw_dense_narrow, dim3(a.bs), dim3(256), lds, s, a);
+            const int gy = std::max(1, std::min(16, 512 / std::max(1, a.bs)));
+            hipLaunchKernelGGL(k_dw_dense_narrow, dim3(a.bs, gy), dim3(256), lds, s, a);
             HGNN_LAUNCH_CHECK();
             return 0;
         }

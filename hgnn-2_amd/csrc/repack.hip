@@ -44,12 +44,17 @@ int launch_repack(const RepackTable& t, hipStream_t s) {
     return 0;
 }
 
+// Slab sums: SG groups of slabs per output, each summed by one thread (4 accumulators), the SG
+// partials combined in order through LDS -- many slabs (the narrow-K layer-0 halves cut their rows
+// into ~374 chunks) no longer mean one long serial chain per output.  Trailing blocks: the bias
+// gradient of output channel o from the BN-backward tile sums (k_db_reduce's work, same order).
+template <int SG>
 __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ slabs, const int* r_valid,
                                                     int kchunk, int M, int N, int split, float* dw0, float* dw1,
                                                     const float* __restrict__ dbpart, float* db0, float* db1) {
-    const int nwb = (M * N + 255) / 256;
+    constexpr int OUT = 256 / SG;
+    const int nwb = (M * N + OUT - 1) / OUT;
     if ((int)blockIdx.x >= nwb) {
-        // trailing blocks: the bias gradient of output channel o (k_db_reduce's work, same order)
         __shared__ double red[4];
         const int o = blockIdx.x - nwb;
         const int tv = ceil_div(*r_valid, 64);
@@ -65,21 +70,29 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
         }
         return;
     }
-    const int idx = blockIdx.x * 256 + threadIdx.x;
+    __shared__ float part[SG][OUT];
+    const int ol = threadIdx.x % OUT, g = threadIdx.x / OUT;
+    const int idx = blockIdx.x * OUT + ol;
     const int rows = *r_valid;
+    const int zv = ceil_div(rows, kchunk);
+    const long long st = (long long)M * N;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (idx < M * N) {
-        const int zv = ceil_div(rows, kchunk);
-        const long long st = (long long)M * N;
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        int z = 0;
-        for (; z + 4 <= zv; z += 4) {
+        int z = g;
+        for (; z + 3 * SG < zv; z += 4 * SG) {
             s0 += slabs[z * st + idx];
-            s1 += slabs[(z + 1) * st + idx];
-            s2 += slabs[(z + 2) * st + idx];
-            s3 += slabs[(z + 3) * st + idx];
+            s1 += slabs[(z + SG) * st + idx];
+            s2 += slabs[(z + 2 * SG) * st + idx];
+            s3 += slabs[(z + 3 * SG) * st + idx];
         }
-        for (; z < zv; ++z) s0 += slabs[z * st + idx];
-        const float s = (s0 + s1) + (s2 + s3);
+        for (; z < zv; z += SG) s0 += slabs[z * st + idx];
+    }
+    part[g][ol] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (g == 0 && idx < M * N) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < SG; ++q) s += part[q][ol];
         const int o = idx / N, c = idx % N;
         if (o < split) dw0[(long long)o * N + c] = s;
         else dw1[(long long)(o - split) * N + c] = s;
@@ -89,9 +102,16 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
 int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int k, int split, float* dw0,
                       float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s) {
     const int total = o * k;
-    // one launch: ceil(o k / 256) blocks of slab sums, then o blocks of bias sums
-    hipLaunchKernelGGL(k_dw_reduce2, dim3(ceil_div(total, 256) + (dbpart ? o : 0)), dim3(256), 0, s, slabs, r_valid,
-                       kchunk, o, k, split, dw0, dw1, dbpart, db0, db1);
+    // slab groups by the slab count (upper bound from the capacity is not known here: the host
+    // passes the chunk size; more groups when the chunks are short, i.e. many slabs per output)
+    const int nb = dbpart ? o : 0;
+    if (kchunk <= 128) {
+        hipLaunchKernelGGL(k_dw_reduce2<16>, dim3(ceil_div(total, 16) + nb), dim3(256), 0, s, slabs, r_valid, kchunk,
+                           o, k, split, dw0, dw1, dbpart, db0, db1);
+    } else {
+        hipLaunchKernelGGL(k_dw_reduce2<4>, dim3(ceil_div(total, 64) + nb), dim3(256), 0, s, slabs, r_valid, kchunk,
+                           o, k, split, dw0, dw1, dbpart, db0, db1);
+    }
     HGNN_LAUNCH_CHECK();
     return 0;
 }
