@@ -142,10 +142,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # HGNN_BENCH_BACKEND=gloo: rehearsal of the N > 1 path on a box with fewer GPUs than ranks (the
+    # ranks share devices round-robin; gloo reduces device tensors through the host) -- timings of
+    # such a run are not the RCCL numbers
+    backend = os.environ.get("HGNN_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     from hgnn_amd import roofline as RF
@@ -344,6 +353,7 @@ def main():
             "graphs_per_gpu": args.bs,
             "global_batch": args.bs * world,
             "parallelism": f"dp{world}",
+            "collective": ("rccl" if backend == "nccl" else backend) if world > 1 else None,
         },
         "roofline": roof,
         "roofline_hbm": roof_hbm,
