@@ -147,6 +147,47 @@ def test_gnn_lg_vs_oracle_fp64_bs128(order):
     assert err <= 1e-4 * max(1.0, ref_dx.abs().max().item())
 
 
+@pytest.mark.parametrize("d", [2, 4, 8])
+def test_gnn_simple_narrow_widths_vs_oracle_fp64(d):
+    """GNN_simple at 2d = 4 / 8 / 16 channels on 24 SBM-50 graphs (1 200 node rows: several 256-row
+    BN tiles), X and W requiring grad: the narrow-channel BN backward (k_bn_bwd_part2s /
+    apply2s, c = 4L), the direct dense dW for F <= 16 (k_dw_dense_narrow) and the readout
+    backward from R_b (k_readout_agg_bwd, k_dw_readout) against the fp64 oracle
+    (model_mnb.py:58-66); outputs on the two-leg policy, every gradient incl. W.grad."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_simple
+    L = 4
+    b = _batch(dg.sbm_dataset(24, n=50, seed=7 + d))
+    model = GNN_simple(0, d, L, 5, 1, 1).cuda()
+    fu.det_init(model, 300 + d)
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = [t.cpu() for t in b]
+
+    def oracle(dtype, grads):
+        p = {k: v.detach().cpu().to(dtype).requires_grad_(grads) for k, v in model.state_dict().items()}
+        Xo = X.to(dtype).requires_grad_(grads)
+        Wo = W.to(dtype).requires_grad_(grads)
+        out = R.gnn_simple(p, [Xo, Wo], Nb, mask.to(dtype), L, R.bn_states(L, 2 * d, "simple", dtype), True)
+        if grads:
+            torch.nn.MSELoss()(out, T.to(dtype)).backward()
+        return out.detach(), p, Xo, Wo
+
+    ref64, p64, X64, W64 = oracle(torch.float64, True)
+    with torch.no_grad():
+        ref32 = oracle(torch.float32, False)[0]
+    Xg, Wg, Tg, maskg, Nbg = X.cuda().requires_grad_(True), W.cuda().requires_grad_(True), T.cuda(), mask.cuda(), Nb.cuda()
+    out = model([Xg, Wg], Nbg, maskg)
+    torch.nn.MSELoss()(out, Tg).backward()
+    o = PP.outputs_two_leg(out, ref32, ref64)
+    assert o["pass"], o
+    gmax = max(v.grad.abs().max().item() for v in p64.values())
+    for k, prm in model.named_parameters():
+        err = (prm.grad.cpu().double() - p64[k].grad).abs()
+        assert torch.all(err <= 1e-4 * gmax + 1e-5 * p64[k].grad.abs()), (k, err.max().item(), gmax)
+    for g, r in ((Xg.grad, X64.grad), (Wg.grad, W64.grad)):
+        err = (g.cpu().double() - r).abs().max().item()
+        assert err <= 1e-4 * max(1.0, r.abs().max().item()), err
+
+
 def test_config2_batch_permutation_equivariance():
     """bs=512 QM9-shape (the benchmark batch): permuting the graphs permutes the outputs."""
     import hgnn_amd.datagen as dg
