@@ -48,6 +48,13 @@ struct ExtractArgs {
     int validate;
     int dual;             // 0: GNN_simple (only S_W / S_WT)
     int kind0;            // first block slot of the launch (blockIdx.y + kind0, struct.hip)
+    // optional: pack the inputs in the same launch (X (bs, f, nmax) -> xo [nodes][f];
+    // XL (bs, 1, emax) -> xlo [edges])
+    const float* X;
+    const float* XL;
+    int f;
+    float* xo;
+    float* xlo;
 };
 int launch_extract(const ExtractArgs& a, hipStream_t s);
 

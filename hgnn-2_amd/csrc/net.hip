@@ -481,7 +481,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
     const bool lg = c->kind == 1;
     const Src src = make_src(P, ws, csr);
     BatchMeta m = src.m;
-    HGNN_HOST_CHECK(hipMemsetAsync(m.err, 0, sizeof(uint32_t), s));
+    if (csr) HGNN_HOST_CHECK(hipMemsetAsync(m.err, 0, sizeof(uint32_t), s));  // dense inputs: k_plan zeroes it
     if (!csr) {
     TL(HGNN_K_STRUCT, launch_plan(in->d_N_batch, lg ? in->d_E_batch : nullptr, c->bs, c->nmax, lg ? c->emax : 0, m, s));
 
@@ -504,9 +504,14 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
     ex.entry_stride_w = P.entry_stride_w;
     ex.validate = 1;
     ex.dual = lg ? 1 : 0;
+    ex.X = in->d_X;
+    ex.f = c->f_in;
+    ex.xo = at<float>(ws, P.feats[0].z);
+    if (lg) {
+        ex.XL = in->d_XL;
+        ex.xlo = at<float>(ws, P.feats[1].z);
+    }
     TL(HGNN_K_STRUCT, launch_extract(ex, s));
-    TL(HGNN_K_STRUCT, launch_pack_nodes(in->d_X, c->bs, c->f_in, c->nmax, m, at<float>(ws, P.feats[0].z), s));
-    if (lg) TL(HGNN_K_STRUCT, launch_pack_edges(in->d_XL, c->bs, c->emax, m, at<float>(ws, P.feats[1].z), s));
     }
 
     const int* tot_n = m.totals;

@@ -28,6 +28,7 @@ __global__ void __launch_bounds__(256) k_plan(const int64_t* __restrict__ nb,
     if (t == 0) {
         carry[0] = 0;
         carry[1] = 0;
+        *m.err = 0u;  // the call's validation word (this kernel is the first of the forward)
     }
     __syncthreads();
     for (int base = 0; base < bs; base += 256) {
@@ -431,8 +432,15 @@ __global__ void __launch_bounds__(XL_THREADS) k_extract_lds(ExtractArgs a) {
             lds_validate(S, emax, emax, JT, eb, eb, a.meta.err);
             validate_mask(a.mask_lg + (long long)b * emax * emax, emax, eb, a.meta.err);
         }
+        if (a.xlo)  // the packed edge input (k_pack_edges' work)
+            for (int i = threadIdx.x; i < eb; i += XL_THREADS) a.xlo[e0 + i] = a.XL[(long long)b * emax + i];
         return;
     }
+    if (a.xo)  // the packed node input (k_pack_nodes' work): [nodes][f] from (bs, f, nmax)
+        for (int i = threadIdx.x; i < nb * a.f; i += XL_THREADS) {
+            const int n = i / a.f, c = i - n * a.f;
+            a.xo[(long long)(n0 + n) * a.f + c] = a.X[((long long)b * a.f + c) * nmax + n];
+        }
     const int nw_ = nmax * nmax * JT, np = nmax * emax;
     float* SW = S;
     float* SM = S + nw_;
@@ -508,6 +516,15 @@ int launch_extract(const ExtractArgs& a, hipStream_t s) {
         }
         HGNN_LAUNCH_CHECK();
         return 0;
+    }
+    // the general kernel leaves the input packing to its own launches
+    if (a.xo) {
+        const int r = launch_pack_nodes(a.X, a.bs, a.f, a.nmax, a.meta, a.xo, s);
+        if (r) return r;
+    }
+    if (a.xlo) {
+        const int r = launch_pack_edges(a.XL, a.bs, a.emax, a.meta, a.xlo, s);
+        if (r) return r;
     }
     const int kinds = a.dual ? X_SLOTS : 2;
     // HGNN_EXTRACT_SPLIT=1 (diagnostics): one launch per block slot, so a kernel trace times
