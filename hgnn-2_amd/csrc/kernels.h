@@ -30,8 +30,10 @@ struct BatchMeta {
     uint32_t* err;   // validation bits (ERR_*)
 };
 
+struct RepackTable;
+// rt (optional): a weight repack table done by extra blocks of the same launch
 int launch_plan(const int64_t* nb, const int64_t* eb, int bs, int nmax, int emax, BatchMeta m,
-                hipStream_t s);
+                hipStream_t s, const RepackTable* rt = nullptr);
 
 struct ExtractArgs {
     const float* W;
@@ -197,6 +199,32 @@ struct RepackTable {
     int n, d;
 };
 int launch_repack(const RepackTable& t, hipStream_t s);
+constexpr int REPACK_Y = 96;  // blocks per repack item
+// one repack item's share of block yb of REPACK_Y (256 threads):
+// WT[k][n] = Wcat[n][k] (dA B), WC[n][k < kp] = Wcat[n][k] zero-padded to kp (forward B),
+// bc = cat(b_lin, b_relu)
+__device__ __forceinline__ void repack_part(const RepackTable& t, int item, int yb) {
+    const RepackItem& it = t.it[item];
+    const int d = t.d, c2 = 2 * d, K = it.k, kp = it.kp;
+    const long long nt = (long long)K * c2, nc = (long long)c2 * kp;
+    for (long long e = (long long)yb * 256 + threadIdx.x; e < nt + nc + c2; e += (long long)REPACK_Y * 256) {
+        if (e < nt) {
+            // coalesced reads along k, scattered 4-byte writes (the L2 merges them)
+            const int n = (int)(e / K), k = (int)(e % K);
+            it.wt[(long long)k * c2 + n] = n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k];
+        } else if (e < nt + nc) {
+            const long long f = e - nt;
+            const int n = (int)(f / kp), k = (int)(f % kp);
+            float v = 0.f;
+            if (k < K) v = n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k];
+            it.wc[f] = v;
+        } else {
+            const int n = (int)(e - nt - nc);
+            it.bc[n] = n < d ? it.bl[n] : it.br[n - d];
+        }
+    }
+}
+
 // GEMM v3 (gemm3.hip): both operands k-contiguous ("NT"), used for the forward and dA.
 bool gemm3_ok(int lda, int ldb, int ldc, const void* a, const void* b);
 int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const float* wc, int ldw, int n,

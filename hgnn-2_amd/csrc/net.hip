@@ -481,9 +481,34 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
     const bool lg = c->kind == 1;
     const Src src = make_src(P, ws, csr);
     BatchMeta m = src.m;
+    std::vector<RepackTable> tables;
+    if (P.v2) {
+        RepackTable rt{};
+        rt.d = P.d;
+        for (size_t hi = 0; hi < P.halves.size(); ++hi) {
+            const Half& h = P.halves[hi];
+            RepackItem& it = rt.it[rt.n++];
+            it.wl = prm[h.pw_lin];
+            it.wr = prm[h.pw_relu];
+            it.bl = prm[h.pb_lin];
+            it.br = prm[h.pb_relu];
+            it.wt = at<float>(ws, h.wt);
+            it.wc = at<float>(ws, h.wc);
+            it.bc = at<float>(ws, h.bc);
+            it.k = h.k;
+            it.kp = h.kp;
+            if (rt.n == REPACK_MAX || hi + 1 == P.halves.size()) {
+                tables.push_back(rt);
+                rt.n = 0;
+            }
+        }
+    }
+    size_t plan_tables = 0;
     if (csr) HGNN_HOST_CHECK(hipMemsetAsync(m.err, 0, sizeof(uint32_t), s));  // dense inputs: k_plan zeroes it
     if (!csr) {
-    TL(HGNN_K_STRUCT, launch_plan(in->d_N_batch, lg ? in->d_E_batch : nullptr, c->bs, c->nmax, lg ? c->emax : 0, m, s));
+    plan_tables = tables.empty() ? 0 : 1;
+    TL(HGNN_K_STRUCT, launch_plan(in->d_N_batch, lg ? in->d_E_batch : nullptr, c->bs, c->nmax, lg ? c->emax : 0, m, s,
+                                  tables.empty() ? nullptr : &tables[0]));
 
     ExtractArgs ex{};
     ex.W = in->d_W;
@@ -516,28 +541,10 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
 
     const int* tot_n = m.totals;
     const int* tot_e = m.totals + 1;
-    if (P.v2) {
-        // repack the Conv1d pairs of every half: Wcat^T (forward B) and padded Wcat (dA B)
-        RepackTable rt{};
-        rt.d = P.d;
-        for (size_t hi = 0; hi < P.halves.size(); ++hi) {
-            const Half& h = P.halves[hi];
-            RepackItem& it = rt.it[rt.n++];
-            it.wl = prm[h.pw_lin];
-            it.wr = prm[h.pw_relu];
-            it.bl = prm[h.pb_lin];
-            it.br = prm[h.pb_relu];
-            it.wt = at<float>(ws, h.wt);
-            it.wc = at<float>(ws, h.wc);
-            it.bc = at<float>(ws, h.bc);
-            it.k = h.k;
-            it.kp = h.kp;
-            if (rt.n == REPACK_MAX || hi + 1 == P.halves.size()) {
-                TL(HGNN_K_STRUCT, launch_repack(rt, s));
-                rt.n = 0;
-            }
-        }
-    }
+    // the repack tables of the Conv1d pairs of every half: Wcat^T (forward B) and padded Wcat (dA B);
+    // the first rides in k_plan's launch (dense inputs), the rest (> REPACK_MAX halves, or a CSR
+    // batch) are launches of their own
+    for (size_t t = plan_tables; t < tables.size(); ++t) TL(HGNN_K_STRUCT, launch_repack(tables[t], s));
     // Line graph: a half's aggregation is two independent parts -- G (its own kind's features of
     // the previous layer, final one half earlier) and P (the other kind's features, produced by
     // the half just before).  The G part runs on the side stream as soon as its input is final,

@@ -14,32 +14,11 @@ namespace hgnn {
 
 // WT[k][n] = Wcat[n][k] (forward B, N-major), WC[n][k < kp]
 // = Wcat[n][k] zero-padded to kp columns (dA B), bc = cat(b_lin, b_relu).
-__global__ void __launch_bounds__(256) k_repack(RepackTable t) {
-    const RepackItem& it = t.it[blockIdx.x];
-    const int d = t.d, c2 = 2 * d, K = it.k, kp = it.kp;
-    const long long nt = (long long)K * c2, nc = (long long)c2 * kp;
-    for (long long e = (long long)blockIdx.y * blockDim.x + threadIdx.x; e < nt + nc + c2;
-         e += (long long)gridDim.y * blockDim.x) {
-        if (e < nt) {
-            // coalesced reads along k, scattered 4-byte writes (the L2 merges them)
-            const int n = (int)(e / K), k = (int)(e % K);
-            it.wt[(long long)k * c2 + n] = n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k];
-        } else if (e < nt + nc) {
-            const long long f = e - nt;
-            const int n = (int)(f / kp), k = (int)(f % kp);
-            float v = 0.f;
-            if (k < K) v = n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k];
-            it.wc[f] = v;
-        } else {
-            const int n = (int)(e - nt - nc);
-            it.bc[n] = n < d ? it.bl[n] : it.br[n - d];
-        }
-    }
-}
+__global__ void __launch_bounds__(256) k_repack(RepackTable t) { repack_part(t, blockIdx.x, blockIdx.y); }
 
 int launch_repack(const RepackTable& t, hipStream_t s) {
     if (t.n <= 0) return 0;
-    hipLaunchKernelGGL(k_repack, dim3(t.n, 96), dim3(256), 0, s, t);
+    hipLaunchKernelGGL(k_repack, dim3(t.n, REPACK_Y), dim3(256), 0, s, t);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -18,9 +18,15 @@
 
 namespace hgnn {
 
+// Block 0: the batch plan.  Blocks 1..: the weight repack (repack_part), folded into this launch.
 __global__ void __launch_bounds__(256) k_plan(const int64_t* __restrict__ nb,
                                               const int64_t* __restrict__ eb, int bs,
-                                              int nmax, int emax, BatchMeta m) {
+                                              int nmax, int emax, BatchMeta m, RepackTable rt) {
+    if (blockIdx.x > 0) {
+        const int b = blockIdx.x - 1;
+        repack_part(rt, b / REPACK_Y, b % REPACK_Y);
+        return;
+    }
     __shared__ int sn[256];
     __shared__ int se[256];
     __shared__ int carry[2];
@@ -77,8 +83,10 @@ __global__ void __launch_bounds__(256) k_plan(const int64_t* __restrict__ nb,
 }
 
 int launch_plan(const int64_t* nb, const int64_t* eb, int bs, int nmax, int emax, BatchMeta m,
-                hipStream_t s) {
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(256), 0, s, nb, eb, bs, nmax, emax, m);
+                hipStream_t s, const RepackTable* rt) {
+    RepackTable t{};
+    if (rt) t = *rt;
+    hipLaunchKernelGGL(k_plan, dim3(1 + t.n * REPACK_Y), dim3(256), 0, s, nb, eb, bs, nmax, emax, m, t);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
