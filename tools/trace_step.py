@@ -17,7 +17,7 @@ t_end = k[-1][1]
 anchors = [s for s, e, n, q in k if "k_plan" in n or "k_repack" in n]
 t0 = anchors[-min(len(anchors), max(1, steps // 2))]
 win = [x for x in k if x[0] >= t0]
-nstep = sum(1 for x in win if "k_repack" in x[2]) or 1
+nstep = sum(1 for x in win if "k_plan" in x[2]) or 1
 tot = defaultdict(float)
 cnt = defaultdict(int)
 for s, e, n, q in win:
