@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--d", type=int, default=64)
     ap.add_argument("--layers", type=int, default=5)
     ap.add_argument("--order", type=int, default=2)
+    ap.add_argument("--settle-s", type=float, default=1.0,
+                    help="untimed steps for this many seconds before the warmup steps (clock ramp)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-bs", type=int, default=512)
     ap.add_argument("--cpu-steps", type=int, default=1)
@@ -191,6 +193,27 @@ def main():
         allreduce()  # no-op at N = 1
         return loss
 
+    # settle: untimed steps for --settle-s seconds before the W warmup steps, so a fresh box's
+    # clocks have ramped before anything is timed (the first run on a box was up to 30 % slow
+    # in A/B runs with only the W steps ahead of it)
+    settle_steps = 0
+    if args.settle_s > 0:
+        # a step count, not a deadline: every rank must run the same number of steps (their
+        # all-reduces pair up), so the count from 10 timed steps is maxed over the ranks
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize()
+        n = int(args.settle_s / max((time.perf_counter() - t0) / 10, 1e-5))
+        if world > 1:
+            t = torch.tensor([n], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            n = int(t.item())
+        for _ in range(n):
+            step()
+        settle_steps = 10 + n
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -340,6 +363,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle_steps": settle_steps,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
