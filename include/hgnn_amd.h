@@ -27,6 +27,15 @@
  *    block, mask/N_batch disagreement) ORs HGNN_DEVERR_* bits into a uint32
  *    word inside the workspace; hgnn_*_error_word() gives its device address.
  *  - no global mutable state: calls are re-entrant, one stream per call.
+ *
+ * Size limits (a call outside them returns HGNN_ERR_UNSUPPORTED or HGNN_ERR_ARG before anything
+ * is enqueued, or -- for data-dependent bounds -- sets a device error bit; the reference has no
+ * such limits, the Python layer raises RuntimeError):
+ *  - networks: J + 2 in [3, 5]; 2d <= 512; the GEMMs address each operand through a 32-bit
+ *    buffer resource, so every per-call operand must stay under 2 GB -- about 12 K QM9-shape
+ *    graphs per call at d = 64 (the 640-wide edge aggregate is the largest; split larger batches);
+ *  - CCN: receptive-field degree <= 1024 (CCN-1D) / 64 (CCN-2D), f_in and hidden <= 16
+ *    (HGNN_DEVERR_CCN_DEGREE for the degree, an error status for the channel counts).
  */
 #ifndef HGNN_AMD_H
 #define HGNN_AMD_H
