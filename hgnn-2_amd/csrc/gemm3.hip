@@ -535,11 +535,17 @@ __device__ __forceinline__ void stage_barrier() {
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int WGM, int WGN>
+// FWD: the forward GEMM's epilogue (k_gemm3 E3_FWD: bias, ReLU from column relu_from, BN partials
+// (count, mean, M2) per 64-row tile); used with 32 x 16 wave tiles for the node halves, whose
+// 32 x 32-wave k_gemm3 grid (1 216 waves on 1 024 SIMDs) left most SIMDs with one wave and some
+// with two.
+template <int BM, int BN, int WGM, int WGN, bool FWD = false>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm5(const float* __restrict__ A, int lda,
                                                           const float* __restrict__ B, int ldb,
                                                           const int* __restrict__ m_valid, int m_cap, int N, int K,
-                                                          float* __restrict__ C, int ldc, int xcd) {
+                                                          float* __restrict__ C, int ldc, int xcd,
+                                                          const float* __restrict__ bias = nullptr,
+                                                          int relu_from = 0, float* __restrict__ bn_part = nullptr) {
     constexpr int BK = 32, NW = WGM * WGN, ST = 2;
     constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 16, AN = TN / 16;
     constexpr int AI = BM * BK * 4 / 1024, BI = BN * BK * 4 / 1024;  // 1-KB wave instructions per stage
@@ -630,6 +636,66 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm5(const float* __restric
         stage_barrier<0>();  // tile t + 1 landed; every wave is done with tile t's buffer
     }
     // C layout of the 16x16 MFMA: col = lane & 15, row = 4 (lane >> 4) + r
+    if constexpr (FWD) {
+        static_assert(BM == 64 && WGM == 2 && AN == 1, "BN partials per 64-row tile, one column per lane");
+        float* red = lds;  // the stage buffers are free: the main loop ended with a barrier
+        const int col = wn * TN + l15, gn = n0 + col;
+        const float bv = gn < N ? bias[gn] : 0.f;
+        const bool relu = gn >= relu_from;
+        float sm = 0.f;
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gm = m0 + wm * TM + i * 16 + 4 * g + r;
+                float v = acc[i][0][r] + bv;
+                if (relu) v = v < 0.f ? 0.f : v;
+                acc[i][0][r] = v;
+                if (gm < M) {
+                    if (gn < N) C[(long long)gm * ldc + gn] = v;
+                    sm += v;
+                    ++cnt;
+                }
+            }
+        if (bn_part) {
+            sm += __shfl_xor(sm, 16, 64);
+            sm += __shfl_xor(sm, 32, 64);
+            cnt += __shfl_xor(cnt, 16, 64);
+            cnt += __shfl_xor(cnt, 32, 64);
+            if (lane < 16) {
+                red[wm * BN + col] = sm;
+                red[2 * BN + wm * BN + col] = (float)cnt;
+            }
+            __syncthreads();
+            const float S = red[col] + red[BN + col];
+            const float Cn = red[2 * BN + col] + red[3 * BN + col];
+            const float mean = Cn > 0.f ? S / Cn : 0.f;
+            __syncthreads();
+            float q = 0.f;
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int gm = m0 + wm * TM + i * 16 + 4 * g + r;
+                    if (gm < M) {
+                        const float dl = acc[i][0][r] - mean;
+                        q = fmaf(dl, dl, q);
+                    }
+                }
+            q += __shfl_xor(q, 16, 64);
+            q += __shfl_xor(q, 32, 64);
+            if (lane < 16) red[wm * BN + col] = q;
+            __syncthreads();
+            if (wm == 0 && lane < 16 && gn < N) {
+                float* pp = bn_part + ((long long)bx * N + gn) * 3;
+                pp[0] = Cn;
+                pp[1] = mean;
+                pp[2] = red[col] + red[BN + col];
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < AM; ++i)
 #pragma unroll
@@ -727,10 +793,25 @@ bool gemm3_ok(int lda, int ldb, int ldc, const void* a, const void* b) {
 
 // Y[r, n] = A[r, :k] . Wc[n, :k] + bias[n]; ReLU on n >= relu_from; BN partials per 64-row tile.
 int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const float* wc, int ldw, int n,
-                     const float* bias, int relu_from, float* y, int ldy, float* bn_part, hipStream_t s) {
+                     const float* bias, int relu_from, float* y, int ldy, float* bn_part, hipStream_t s,
+                     int mfma16) {
     if (m_cap <= 0) return 0;
     if (k % 4 != 0) return HGNN_ERR_UNSUPPORTED;  // pass the padded width (zero padding in both operands)
     if ((long long)m_cap * lda * 4 >= (1ll << 31) || (long long)n * ldw * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    // 32 x 16 wave tiles (v_mfma_f32_16x16x4_f32, LDS-DMA staging) when the 32 x 32-wave grid would
+    // leave the SIMDs unevenly loaded (under 2 waves per SIMD); HGNN_FWD_G5=0 never, 2 always
+    static const int g5 = [] {
+        const char* e = getenv("HGNN_FWD_G5");
+        return e ? atoi(e) : 1;
+    }();
+    const long long waves32 = (long long)ceil_div(m_cap, 64) * ceil_div(n, 64) * 4;
+    if (mfma16 && g5 > 0 && n % 64 == 0 && n <= 512 && (g5 == 2 || waves32 < 2 * 1024)) {
+        const int gx = ceil_div(ceil_div(m_cap, 64), 8) * 8;
+        hipLaunchKernelGGL((k_gemm5<64, 64, 2, 4, true>), dim3(gx, n / 64), dim3(512), 0, s, a, lda, wc, ldw,
+                           m_valid, m_cap, n, k, y, ldy, 1, bias, relu_from, bn_part);
+        HGNN_LAUNCH_CHECK();
+        return 0;
+    }
     G3 p{};
     p.a = a;
     p.lda = lda;

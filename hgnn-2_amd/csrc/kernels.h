@@ -227,8 +227,11 @@ __device__ __forceinline__ void repack_part(const RepackTable& t, int item, int 
 
 // GEMM v3 (gemm3.hip): both operands k-contiguous ("NT"), used for the forward and dA.
 bool gemm3_ok(int lda, int ldb, int ldc, const void* a, const void* b);
+// mfma16: the 16x16x4-MFMA kernel may take the imbalanced (small-grid) shapes; its k-order differs
+// from the 32x32x2 kernel's by rounding (line-graph networks; GNN_simple keeps the 32x32 order)
 int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const float* wc, int ldw, int n,
-                     const float* bias, int relu_from, float* y, int ldy, float* bn_part, hipStream_t s);
+                     const float* bias, int relu_from, float* y, int ldy, float* bn_part, hipStream_t s,
+                     int mfma16 = 0);
 int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, int o, const float* wt, int ldw,
                     int kout, float* da, int ldda, hipStream_t s);
 int dw3_kchunk(int r_cap, int o, int k);

@@ -626,7 +626,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
             TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<float>(ws, h.wc), h.kp,
                                                  P.c2, at<float>(ws, h.bc), h.relu_from,
                                                  at<float>(ws, P.feats[h.out].y), P.c2,
-                                                 c->training ? at<float>(ws, h.part) : nullptr, s));
+                                                 c->training ? at<float>(ws, h.part) : nullptr, s, lg ? 1 : 0));
         } else if (fused_fwd_half(P, h)) {
             // aggregation gathered into LDS tiles of the Conv1d-pair GEMM; the aggregate is still
             // written once (h.a) for the weight-gradient GEMM of the backward
@@ -693,7 +693,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
             TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<float>(ws, h.wc), h.kp,
                                                  P.c2, at<float>(ws, h.bc), h.relu_from,
                                                  at<float>(ws, P.feats[h.out].y), P.c2,
-                                                 c->training ? at<float>(ws, h.part) : nullptr, s));
+                                                 c->training ? at<float>(ws, h.part) : nullptr, s, lg ? 1 : 0));
         } else {
         GemmFwdArgs gf{};
         gf.a = at<float>(ws, h.a);
