@@ -84,6 +84,11 @@ static bool vec_ok(int cpl, int c, const void* base, std::initializer_list<long 
 // and broadcast with readlane, and U feature rows are loaded before any is used,
 // so a row of n entries costs ~n/U dependent memory round trips instead of 2n.
 constexpr int AGG_U = 4;
+// rows (waves) per block of the aggregation kernels; AGG_BLOCK_WAVES at build time (A/B)
+#ifndef AGG_BLOCK_WAVES
+#define AGG_BLOCK_WAVES 4
+#endif
+constexpr int AGG_WV = AGG_BLOCK_WAVES, AGG_NT = 64 * AGG_WV;
 
 __device__ __forceinline__ float4 lane_entry(const float* __restrict__ entries, int stride, int start, int n, int lane) {
     // W / WL entries: (col, v_0..v_{J-1}) padded to `stride` floats; P entries: (col, pm, pd, -)
@@ -134,8 +139,8 @@ struct LaneBn {
 };
 
 template <int JT, int CG, int CP, bool V>
-__global__ void __launch_bounds__(256) k_agg_fwd(AggFwdArgs a) {
-    const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+__global__ void __launch_bounds__(AGG_NT) k_agg_fwd(AggFwdArgs a) {
+    const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * AGG_WV + (threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     if (r >= *a.total_rows) return;
     float* o = a.out + (long long)r * a.ldo;
@@ -262,8 +267,8 @@ static void agg_fwd_v(const AggFwdArgs& a, dim3 g, hipStream_t s) {
     const bool v = (CG == 0 || vec_ok(CG, a.cg, a.xg, {})) && (CP == 0 || vec_ok(CP, a.cp, a.xp, {})) &&
                    (CG == 0 || vec_ok(CG, a.cg, a.out, {a.ldo, (long long)kk})) &&
                    (CP == 0 || vec_ok(CP, a.cp, a.out, {a.ldo, (long long)JT * a.cg, (long long)a.cp}));
-    if (v) hipLaunchKernelGGL((k_agg_fwd<JT, CG, CP, true>), g, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_agg_fwd<JT, CG, CP, false>), g, dim3(256), 0, s, a);
+    if (v) hipLaunchKernelGGL((k_agg_fwd<JT, CG, CP, true>), g, dim3(AGG_NT), 0, s, a);
+    else hipLaunchKernelGGL((k_agg_fwd<JT, CG, CP, false>), g, dim3(AGG_NT), 0, s, a);
 }
 
 template <int JT, int CG>
@@ -296,7 +301,7 @@ static int agg_fwd_cg(const AggFwdArgs& a, dim3 g, hipStream_t s) {
 
 int launch_agg_fwd(const AggFwdArgs& a, hipStream_t s) {
     if (a.cap_rows <= 0) return 0;
-    const dim3 g(ceil_div(a.cap_rows, 4));
+    const dim3 g(ceil_div(a.cap_rows, AGG_WV));
     switch (a.jtot) {
         case 3: return agg_fwd_cg<3>(a, g, s);
         case 4: return agg_fwd_cg<4>(a, g, s);
@@ -420,18 +425,18 @@ __device__ __forceinline__ void agg_bwd_p(const AggBwdArgs& a, int r, int lane) 
 
 // MODE 1: G only (ga); 2: P only (pa); 3: blocks [0, gb) G on ga, the rest P on pa.
 template <int JT, int CG, int CP, bool V, int MODE>
-__global__ void __launch_bounds__(256) k_agg_bwd(AggBwdArgs ga, AggBwdArgs pa, int gb) {
+__global__ void __launch_bounds__(AGG_NT) k_agg_bwd(AggBwdArgs ga, AggBwdArgs pa, int gb) {
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     if (MODE == 1 || (MODE == 3 && (int)blockIdx.x < gb)) {
         if constexpr (MODE != 2) {
-            const int r = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wv);
+            const int r = __builtin_amdgcn_readfirstlane((int)blockIdx.x * AGG_WV + wv);
             if (r >= *ga.total_rows) return;
             agg_bwd_g<JT, CG, V>(ga, r, lane);
         }
     } else {
         if constexpr (MODE != 1) {
-            const int r = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - (MODE == 3 ? gb : 0)) * 4 + wv);
+            const int r = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - (MODE == 3 ? gb : 0)) * AGG_WV + wv);
             if (r >= *pa.total_rows) return;
             agg_bwd_p<CP, V>(pa, r, lane);
         }
@@ -447,13 +452,13 @@ static bool bwd_vec_p(int cpl, const AggBwdArgs& a) {
 
 template <int JT, int C>
 static int agg_bwd_single(const AggBwdArgs& a, hipStream_t s) {
-    const dim3 g(ceil_div(a.cap_rows, 4));
+    const dim3 g(ceil_div(a.cap_rows, AGG_WV));
     if (a.ing) {
-        if (bwd_vec_g(C, a)) hipLaunchKernelGGL((k_agg_bwd<JT, C, C, true, 1>), g, dim3(256), 0, s, a, a, 0);
-        else hipLaunchKernelGGL((k_agg_bwd<JT, C, C, false, 1>), g, dim3(256), 0, s, a, a, 0);
+        if (bwd_vec_g(C, a)) hipLaunchKernelGGL((k_agg_bwd<JT, C, C, true, 1>), g, dim3(AGG_NT), 0, s, a, a, 0);
+        else hipLaunchKernelGGL((k_agg_bwd<JT, C, C, false, 1>), g, dim3(AGG_NT), 0, s, a, a, 0);
     } else {
-        if (bwd_vec_p(C, a)) hipLaunchKernelGGL((k_agg_bwd<3, C, C, true, 2>), g, dim3(256), 0, s, a, a, 0);
-        else hipLaunchKernelGGL((k_agg_bwd<3, C, C, false, 2>), g, dim3(256), 0, s, a, a, 0);
+        if (bwd_vec_p(C, a)) hipLaunchKernelGGL((k_agg_bwd<3, C, C, true, 2>), g, dim3(AGG_NT), 0, s, a, a, 0);
+        else hipLaunchKernelGGL((k_agg_bwd<3, C, C, false, 2>), g, dim3(AGG_NT), 0, s, a, a, 0);
     }
     HGNN_LAUNCH_CHECK();
     return 0;
@@ -483,8 +488,8 @@ int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s) {
 
 template <int JT, int C>
 static int agg_bwd_pair_c(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t s) {
-    const int gb = ceil_div(ga.cap_rows, 4), pb = ceil_div(pa.cap_rows, 4);
-    hipLaunchKernelGGL((k_agg_bwd<JT, C, C, true, 3>), dim3(gb + pb), dim3(256), 0, s, ga, pa, gb);
+    const int gb = ceil_div(ga.cap_rows, AGG_WV), pb = ceil_div(pa.cap_rows, AGG_WV);
+    hipLaunchKernelGGL((k_agg_bwd<JT, C, C, true, 3>), dim3(gb + pb), dim3(AGG_NT), 0, s, ga, pa, gb);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
