@@ -197,29 +197,50 @@ constexpr int REPACK_MAX = 24;
 struct RepackTable {
     RepackItem it[REPACK_MAX];
     int n, d;
+    int y;  // blocks per item (repack_y)
 };
 int launch_repack(const RepackTable& t, hipStream_t s);
-constexpr int REPACK_Y = 96;  // blocks per repack item
-// one repack item's share of block yb of REPACK_Y (256 threads):
+// blocks per repack item: ~4 elements per thread of the largest item, 8..256 blocks (d = 64: 80
+// transpose tiles; d = 128: 320 -- 96 blocks left 44 us of sequential tiles at d = 128)
+inline int repack_y(const RepackTable& t) {
+    long long mx = 1;
+    for (int i = 0; i < t.n; ++i) mx = mx > (long long)t.it[i].k * 2 * t.d ? mx : (long long)t.it[i].k * 2 * t.d;
+    const long long y = (mx + 1023) / 1024;
+    return (int)(y < 8 ? 8 : (y > 256 ? 256 : y));
+}
+// one repack item's share of block yb of t.y (256 threads):
 // WT[k][n] = Wcat[n][k] (dA B), WC[n][k < kp] = Wcat[n][k] zero-padded to kp (forward B),
 // bc = cat(b_lin, b_relu)
 __device__ __forceinline__ void repack_part(const RepackTable& t, int item, int yb) {
     const RepackItem& it = t.it[item];
     const int d = t.d, c2 = 2 * d, K = it.k, kp = it.kp;
-    const long long nt = (long long)K * c2, nc = (long long)c2 * kp;
-    for (long long e = (long long)yb * 256 + threadIdx.x; e < nt + nc + c2; e += (long long)REPACK_Y * 256) {
-        if (e < nt) {
-            // coalesced reads along k, scattered 4-byte writes (the L2 merges them)
-            const int n = (int)(e / K), k = (int)(e % K);
-            it.wt[(long long)k * c2 + n] = n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k];
-        } else if (e < nt + nc) {
-            const long long f = e - nt;
-            const int n = (int)(f / kp), k = (int)(f % kp);
-            float v = 0.f;
-            if (k < K) v = n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k];
-            it.wc[f] = v;
+    auto W = [&](int n, int k) { return n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k]; };
+    // WT through 32 x 33 LDS tiles: reads along k and writes along n both coalesced (the direct
+    // transpose wrote 4-byte scattered stores: 8 us at d = 64, 44 us at d = 128)
+    __shared__ float tile[32][33];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 row groups
+    const int nkt = (K + 31) / 32, ntiles = ((c2 + 31) / 32) * nkt;
+    for (int tl = yb; tl < ntiles; tl += t.y) {
+        const int n0 = (tl / nkt) * 32, k0 = (tl % nkt) * 32;
+        for (int rr = ty; rr < 32; rr += 8) {
+            const int n = n0 + rr, k = k0 + tx;
+            tile[rr][tx] = (n < c2 && k < K) ? W(n, k) : 0.f;
+        }
+        __syncthreads();
+        for (int rr = ty; rr < 32; rr += 8) {
+            const int k = k0 + rr, n = n0 + tx;
+            if (k < K && n < c2) it.wt[(long long)k * c2 + n] = tile[tx][rr];
+        }
+        __syncthreads();
+    }
+    // WC (zero-padded to kp) and bc: coalesced along k
+    const long long nc = (long long)c2 * kp;
+    for (long long e = (long long)yb * 256 + threadIdx.x; e < nc + c2; e += (long long)t.y * 256) {
+        if (e < nc) {
+            const int n = (int)(e / kp), k = (int)(e % kp);
+            it.wc[e] = k < K ? W(n, k) : 0.f;
         } else {
-            const int n = (int)(e - nt - nc);
+            const int n = (int)(e - nc);
             it.bc[n] = n < d ? it.bl[n] : it.br[n - d];
         }
     }

@@ -18,7 +18,9 @@ __global__ void __launch_bounds__(256) k_repack(RepackTable t) { repack_part(t, 
 
 int launch_repack(const RepackTable& t, hipStream_t s) {
     if (t.n <= 0) return 0;
-    hipLaunchKernelGGL(k_repack, dim3(t.n, REPACK_Y), dim3(256), 0, s, t);
+    RepackTable u = t;
+    u.y = repack_y(t);
+    hipLaunchKernelGGL(k_repack, dim3(u.n, u.y), dim3(256), 0, s, u);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

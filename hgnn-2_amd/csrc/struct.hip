@@ -24,7 +24,7 @@ __global__ void __launch_bounds__(256) k_plan(const int64_t* __restrict__ nb,
                                               int nmax, int emax, BatchMeta m, RepackTable rt) {
     if (blockIdx.x > 0) {
         const int b = blockIdx.x - 1;
-        repack_part(rt, b / REPACK_Y, b % REPACK_Y);
+        repack_part(rt, b / rt.y, b % rt.y);
         return;
     }
     __shared__ int sn[256];
@@ -86,7 +86,8 @@ int launch_plan(const int64_t* nb, const int64_t* eb, int bs, int nmax, int emax
                 hipStream_t s, const RepackTable* rt) {
     RepackTable t{};
     if (rt) t = *rt;
-    hipLaunchKernelGGL(k_plan, dim3(1 + t.n * REPACK_Y), dim3(256), 0, s, nb, eb, bs, nmax, emax, m, t);
+    t.y = repack_y(t);
+    hipLaunchKernelGGL(k_plan, dim3(1 + t.n * t.y), dim3(256), 0, s, nb, eb, bs, nmax, emax, m, t);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
