@@ -422,6 +422,11 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
     const int r0 = blockIdx.x * 64;
     if (r0 >= total) return;
     const int r1 = min(total, r0 + 64);
+    // dY rows of stride ldy > c (an odd 2d padded for the dA GEMM's float4 k): the padding columns
+    // are zeroed here, so the GEMM's zero weight columns never meet uninitialised workspace
+    const int ldy = a.ldy > 0 ? a.ldy : a.c;
+    for (int e = threadIdx.x; e < (r1 - r0) * (ldy - a.c); e += blockDim.x)
+        a.dy[(long long)(r0 + e / (ldy - a.c)) * ldy + a.c + e % (ldy - a.c)] = 0.f;
     const int cw = a.c < 256 ? a.c : 256;
     const int rgn = 256 / cw;
     const int tch = threadIdx.x % cw, rg = threadIdx.x / cw;
@@ -448,14 +453,14 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const float d = one(yv[u], dzv[u]);
-                    a.dy[(long long)(r + u * rgn) * a.c + ch] = d;
+                    a.dy[(long long)(r + u * rgn) * ldy + ch] = d;
                     cs += d;
                 }
             }
             for (; r < r1; r += rgn) {
                 const long long i = (long long)r * a.c + ch;
                 const float d = one(a.y[i], a.dz[i]);
-                a.dy[i] = d;
+                a.dy[(long long)r * ldy + ch] = d;
                 cs += d;
             }
         }
@@ -954,7 +959,9 @@ static void bn2_launch(const BnBwdArgs& a, hipStream_t s) {
 
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     const int tiles = bn_bwd_tiles(a.cap_rows);
-    const bool v4 = bn_vec4(a);
+    if (a.ldy != 0 && a.ldy < a.c) return HGNN_ERR_ARG;
+    // a padded dY stride is written by the scalar apply only
+    const bool v4 = bn_vec4(a) && (a.ldy == 0 || a.ldy == a.c);
     // (c / 4 a power of two: the per-wave shuffle reduction pairs the lanes of one channel group)
     // HGNN_BN_SMALL=1: the single-block k_bn_bwd_small instead of the two-launch narrow form
     static const bool one_block = [] {

@@ -162,7 +162,7 @@ int hgnn_conv1x1_backward(const float* d_x, const float* d_w, const float* d_dy,
     const int kc = dw3_kchunk((int)rows, cout, cin);
     int r = launch_gemm3_dw(yt, coutp, xt, cinp, cnt, (int)rows, cout, cin, kc, slabs, s);
     if (r) return r;
-    r = launch_dw_reduce2(slabs, cnt, kc, cout, cin, cout, d_dw, d_dw, nullptr, nullptr, nullptr, s);
+    r = launch_dw_reduce2(slabs, cnt, kc, cout, cout, cin, cout, d_dw, d_dw, nullptr, nullptr, nullptr, s);
     if (r) return r;
     hipLaunchKernelGGL(k_bias_grad, dim3(cout), dim3(256), 0, s, d_dy, bs, cout, n, d_db);
     HGNN_LAUNCH_CHECK();

@@ -786,6 +786,8 @@ int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const in
     return 0;
 }
 
+int gemm_fwd_tiles_m(int m_cap) { return ceil_div(m_cap, 64); }
+
 bool gemm3_ok(int lda, int ldb, int ldc, const void* a, const void* b) {
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
     return lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 && al(a) && al(b);

@@ -130,68 +130,16 @@ int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s);  // exactly one of ing /
 // share the lane layout, else two launches
 int launch_agg_bwd_pair(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t s);
 
-// ---------------------------------------------------------------- GEMM (fp32 MFMA)
-// Y = A . W^T + bias, relu on cols >= relu_from, BN partials over valid rows.
-struct GemmFwdArgs {
-    const float* a;
-    int lda;
-    const int* m_valid;  // device row count
-    int m_cap, k;
-    const float* w0;     // weights for output cols [0, split): row-major [split][k]
-    const float* w1;     // weights for output cols [split, n): row-major [n - split][k]
-    const float* b0;
-    const float* b1;
-    int n, split, relu_from;
-    float* y;
-    int ldy;
-    float* bn_part;      // [tiles_m][n][3] (count, mean, M2) or nullptr
-};
-int launch_gemm_fwd(const GemmFwdArgs& g, hipStream_t s);
-int gemm_fwd_tiles_m(int m_cap);
-
-// dA = dY . Wcat :  dA[m, k] = sum_o dY[m, o] * Wcat[o, k], Wcat rows split at `split`.
-struct GemmDaArgs {
-    const float* dy;
-    int lddy;
-    const int* m_valid;
-    int m_cap, o;       // o = 2d rows of Wcat
-    const float* w0;
-    const float* w1;
-    int split, k;       // k = output columns
-    float* da;
-    int ldda;
-};
-int launch_gemm_da(const GemmDaArgs& g, hipStream_t s);
-
-// dWcat[o, k] = sum_r dY[r, o] * A[r, k]; column k == kdim of the result is the bias
-// gradient (sum_r dY[r, o]).  Split over row chunks into slabs, then reduced.
-struct GemmDwArgs {
-    const float* dy;
-    int lddy;
-    const float* a;
-    int lda;
-    const int* r_valid;
-    int r_cap, o, k;
-    int split;
-    float* slabs;       // scratch
-    float* dw0;         // (split, k)
-    float* dw1;         // (o - split, k)
-    float* db0;         // (split,)
-    float* db1;         // (o - split,)
-};
-int launch_gemm_dw(const GemmDwArgs& g, hipStream_t s);
-size_t gemm_dw_slab_floats(int r_cap, int o, int k);
-
 // ---------------------------------------------------------------- GEMM (gemm3.hip, repack.hip)
 struct RepackItem {
     const float* wl;   // linear conv weight (d, K)
     const float* wr;   // ReLU conv weight (d, K)
     const float* bl;
     const float* br;
-    float* wt;         // out: [K][2d]
+    float* wt;         // out: [K][ldt], columns [2d, ldt) zero
     float* wc;         // out: [2d][kp]
     float* bc;         // out: [2d]
-    int k, kp;
+    int k, kp, ldt;
 };
 constexpr int REPACK_MAX = 24;
 struct RepackTable {
@@ -204,7 +152,7 @@ int launch_repack(const RepackTable& t, hipStream_t s);
 // transpose tiles; d = 128: 320 -- 96 blocks left 44 us of sequential tiles at d = 128)
 inline int repack_y(const RepackTable& t) {
     long long mx = 1;
-    for (int i = 0; i < t.n; ++i) mx = mx > (long long)t.it[i].k * 2 * t.d ? mx : (long long)t.it[i].k * 2 * t.d;
+    for (int i = 0; i < t.n; ++i) mx = mx > (long long)t.it[i].k * t.it[i].ldt ? mx : (long long)t.it[i].k * t.it[i].ldt;
     const long long y = (mx + 1023) / 1024;
     return (int)(y < 8 ? 8 : (y > 256 ? 256 : y));
 }
@@ -213,13 +161,14 @@ inline int repack_y(const RepackTable& t) {
 // bc = cat(b_lin, b_relu)
 __device__ __forceinline__ void repack_part(const RepackTable& t, int item, int yb) {
     const RepackItem& it = t.it[item];
-    const int d = t.d, c2 = 2 * d, K = it.k, kp = it.kp;
+    const int d = t.d, c2 = 2 * d, K = it.k, kp = it.kp, ldt = it.ldt;
     auto W = [&](int n, int k) { return n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k]; };
     // WT through 32 x 33 LDS tiles: reads along k and writes along n both coalesced (the direct
-    // transpose wrote 4-byte scattered stores: 8 us at d = 64, 44 us at d = 128)
+    // transpose wrote 4-byte scattered stores: 8 us at d = 64, 44 us at d = 128); the columns
+    // [2d, ldt) -- the zero padding of an odd 2d to the dA GEMM's float4 k -- are written as zeros
     __shared__ float tile[32][33];
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 row groups
-    const int nkt = (K + 31) / 32, ntiles = ((c2 + 31) / 32) * nkt;
+    const int nkt = (K + 31) / 32, ntiles = ((ldt + 31) / 32) * nkt;
     for (int tl = yb; tl < ntiles; tl += t.y) {
         const int n0 = (tl / nkt) * 32, k0 = (tl % nkt) * 32;
         for (int rr = ty; rr < 32; rr += 8) {
@@ -229,7 +178,7 @@ __device__ __forceinline__ void repack_part(const RepackTable& t, int item, int 
         __syncthreads();
         for (int rr = ty; rr < 32; rr += 8) {
             const int k = k0 + rr, n = n0 + tx;
-            if (k < K && n < c2) it.wt[(long long)k * c2 + n] = tile[tx][rr];
+            if (k < K && n < ldt) it.wt[(long long)k * ldt + n] = tile[tx][rr];
         }
         __syncthreads();
     }
@@ -247,6 +196,7 @@ __device__ __forceinline__ void repack_part(const RepackTable& t, int item, int 
 }
 
 // GEMM v3 (gemm3.hip): both operands k-contiguous ("NT"), used for the forward and dA.
+int gemm_fwd_tiles_m(int m_cap);  // 64-row tiles of the forward GEMM's BN partials
 bool gemm3_ok(int lda, int ldb, int ldc, const void* a, const void* b);
 // mfma16: the 16x16x4-MFMA kernel may take the imbalanced (small-grid) shapes; its k-order differs
 // from the 32x32x2 kernel's by rounding (line-graph networks; GNN_simple keeps the 32x32 order)
@@ -259,9 +209,11 @@ int dw3_kchunk(int r_cap, int o, int k);
 size_t dw3_slab_floats(int r_cap, int o, int k);
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
                     int kchunk, float* slabs, hipStream_t s);
-// slabs -> dW (split rows) ; bias grads from the BN-backward per-tile column sums of dY
-int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int k, int split, float* dw0,
-                      float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s);
+// slabs [z][o][k] -> dW (rows [0, split) -> dw0, [split, o_real) -> dw1; rows >= o_real are the
+// zero padding of an odd 2d); bias grads from the BN-backward per-tile column sums of dY
+// (dbpart [tiles][o_real])
+int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int o_real, int k, int split,
+                      float* dw0, float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s);
 
 // ---------------------------------------------------------------- fused aggregation + GEMM (fused.hip)
 // One K segment of the virtual aggregate: ns coefficient slices of a cs-channel feature matrix
@@ -331,7 +283,8 @@ struct BnBwdArgs {
     int training;
     float* part;           // scratch [tiles][c][2]
     float* sums;           // scratch [c][2] + [2]
-    float* dy;             // out [rows][c]
+    float* dy;             // out [rows][ldy] (ldy = 0: c; ldy > c only on the scalar path, c % 4 != 0)
+    int ldy;
     float* dw;             // scalar out
     float* db;             // scalar out
     float* dbpart;         // optional out: per-64-row-tile column sums of dy [tiles][c]

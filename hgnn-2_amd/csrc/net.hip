@@ -37,13 +37,14 @@ struct Half {
     int out, bn;
     int pw_lin, pb_lin, pw_relu, pb_relu, pbn_w, pbn_b;
     int relu_from;
-    int kp;  // row stride of the aggregate / dA buffers (k rounded up to 4 for GEMM v2)
+    int kp;  // row stride of the aggregate / dA buffers (k rounded up to 4: the GEMMs' float4 k)
     size_t a = 0, part = 0, mean = 0, stdv = 0;
-    size_t wt = 0, wc = 0, bc = 0;  // GEMM v2 repacked weights
+    size_t wt = 0, wc = 0, bc = 0;  // repacked Conv1d-pair weights (repack.hip)
 };
 
 struct Program {
     int cap_n = 0, cap_e = 0, jt = 0, d = 0, c2 = 0;
+    int c2p = 0;  // 2d rounded up to 4: row stride of dY and of the repacked WT (dA GEMM's float4 k)
     int n_params = 0, n_bn = 0;
     std::vector<Feat> feats;
     std::vector<Half> halves;
@@ -53,7 +54,6 @@ struct Program {
     size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
     int entry_stride_w = 4;
     size_t dy = 0, dy2 = 0, da = 0, da2 = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0, dbpart2 = 0;
-    bool v2 = false;  // GEMM v2 path (2d % 4 == 0); gemm.hip otherwise
     bool fused = false;      // fused aggregation + GEMM forward (fused.hip): 2d % 16 == 0, 2d <= 256
     bool fused_bwd = false;  // fused backward dX (HGNN_FUSED_BWD=1; see DESIGN.md §8 for why it is off)
     size_t bytes = 0;
@@ -112,6 +112,7 @@ Program build_program(const hgnn_net_config* c) {
     P.jt = c->j_tot;
     P.d = c->d;
     P.c2 = 2 * c->d;
+    P.c2p = (P.c2 + 3) / 4 * 4;
     P.entry_stride_w = c->j_tot <= 3 ? 4 : 8;
     const int L = c->n_layers;
     P.n_params = (lg ? 12 : 6) * (L - 1) + 2;
@@ -242,23 +243,20 @@ Program build_program(const hgnn_net_config* c) {
     }
     size_t max_da = 0, max_slab = 0;
     int max_cap = 0;
-    P.v2 = (P.c2 % 4) == 0;
-    P.fused = P.v2 && P.c2 % 16 == 0 && P.c2 <= 256 && fused_enabled();
+    P.fused = P.c2 % 16 == 0 && P.c2 <= 256 && fused_enabled();
     P.fused_bwd = P.fused && env_flag("HGNN_FUSED_BWD", false);
     for (auto& h : P.halves) {
         const int cap = h.edge ? P.cap_e : P.cap_n;
-        h.kp = P.v2 ? (h.k + 3) / 4 * 4 : h.k;
+        h.kp = (h.k + 3) / 4 * 4;
         h.a = B.take((size_t)cap * h.kp * sizeof(float));
         h.part = B.take((size_t)gemm_fwd_tiles_m(cap) * P.c2 * 3 * sizeof(float));
         h.mean = B.take(P.c2 * sizeof(float));
         h.stdv = B.take(P.c2 * sizeof(float));
-        if (P.v2) {
-            h.wt = B.take((size_t)h.k * P.c2 * sizeof(float));
-            h.wc = B.take((size_t)P.c2 * h.kp * sizeof(float));
-            h.bc = B.take((size_t)P.c2 * sizeof(float));
-        }
+        h.wt = B.take((size_t)h.k * P.c2p * sizeof(float));
+        h.wc = B.take((size_t)P.c2 * h.kp * sizeof(float));
+        h.bc = B.take((size_t)P.c2 * sizeof(float));
         max_da = std::max(max_da, (size_t)cap * h.kp);
-        max_slab = std::max(max_slab, P.v2 ? dw3_slab_floats(cap, P.c2, h.k) : gemm_dw_slab_floats(cap, P.c2, h.k));
+        max_slab = std::max(max_slab, dw3_slab_floats(cap, P.c2, h.k));
         max_cap = std::max(max_cap, cap);
     }
     P.dbpart = B.take((size_t)bn_bwd_tiles(max_cap > 0 ? max_cap : 1) * P.c2 * sizeof(float));
@@ -266,10 +264,10 @@ Program build_program(const hgnn_net_config* c) {
     P.a_last = B.take((size_t)P.cap_n * P.k_last * sizeof(float));
     P.colsum = B.take((size_t)c->bs * P.k_last * sizeof(float));
     max_da = std::max(max_da, (size_t)P.cap_n * P.k_last);
-    P.dy = B.take((size_t)max_cap * P.c2 * sizeof(float));
-    P.dy2 = B.take((size_t)max_cap * P.c2 * sizeof(float));
+    P.dy = B.take((size_t)max_cap * P.c2p * sizeof(float));
+    P.dy2 = B.take((size_t)max_cap * P.c2p * sizeof(float));
     P.da = B.take(max_da * sizeof(float));
-    if (P.v2) P.da2 = B.take(max_da * sizeof(float));  // dA alternates like dY: the side stream's dense dW reads it
+    P.da2 = B.take(max_da * sizeof(float));  // dA alternates like dY: the side stream's dense dW reads it
     P.slabs = B.take(max_slab * sizeof(float));
     P.bnb_part = B.take((size_t)bn_bwd_tiles(max_cap) * P.c2 * 4 * sizeof(float));
     P.bnb_sums = B.take((size_t)P.c2 * 4 * sizeof(float));
@@ -303,7 +301,7 @@ bool fits_32bit(const Program& P) {
     const long long lim = (1ll << 31) - 1;
     for (const Half& h : P.halves) {
         const long long cap = h.edge ? P.cap_e : P.cap_n;
-        if (cap * h.kp * 4 > lim || cap * P.c2 * 4 > lim || (long long)P.c2 * h.kp * 4 > lim) return false;
+        if (cap * h.kp * 4 > lim || cap * P.c2p * 4 > lim || (long long)P.c2p * h.kp * 4 > lim) return false;
     }
     return (long long)P.cap_n * P.k_last * 4 <= lim;
 }
@@ -482,7 +480,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
     const Src src = make_src(P, ws, csr);
     BatchMeta m = src.m;
     std::vector<RepackTable> tables;
-    if (P.v2) {
+    {
         RepackTable rt{};
         rt.d = P.d;
         for (size_t hi = 0; hi < P.halves.size(); ++hi) {
@@ -497,6 +495,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
             it.bc = at<float>(ws, h.bc);
             it.k = h.k;
             it.kp = h.kp;
+            it.ldt = P.c2p;
             if (rt.n == REPACK_MAX || hi + 1 == P.halves.size()) {
                 tables.push_back(rt);
                 rt.n = 0;
@@ -552,7 +551,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
     // beside an MFMA-bound GEMM.  Events: pool[hi] = half hi's BN statistics final (main),
     // pool[H + hi] = half hi's G part written (side), pool[2H] = inputs packed (main).
     const int H = (int)P.halves.size();
-    const bool split = lg && P.v2 && !P.fused && split_agg_enabled();
+    const bool split = lg && !P.fused && split_agg_enabled();
     SideStream* side = nullptr;
     if (split) {
         TRY(side_stream(s, &side));
@@ -689,30 +688,10 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
         ag.ldo = h.kp;
         TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
 
-        if (P.v2) {
-            TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<float>(ws, h.wc), h.kp,
-                                                 P.c2, at<float>(ws, h.bc), h.relu_from,
-                                                 at<float>(ws, P.feats[h.out].y), P.c2,
-                                                 c->training ? at<float>(ws, h.part) : nullptr, s, lg ? 1 : 0));
-        } else {
-        GemmFwdArgs gf{};
-        gf.a = at<float>(ws, h.a);
-        gf.lda = h.k;
-        gf.m_valid = tot;
-        gf.m_cap = cap;
-        gf.k = h.k;
-        gf.w0 = prm[h.pw_lin];
-        gf.w1 = prm[h.pw_relu];
-        gf.b0 = prm[h.pb_lin];
-        gf.b1 = prm[h.pb_relu];
-        gf.n = P.c2;
-        gf.split = P.d;
-        gf.relu_from = h.relu_from;
-        gf.y = at<float>(ws, P.feats[h.out].y);
-        gf.ldy = P.c2;
-        gf.bn_part = c->training ? at<float>(ws, h.part) : nullptr;
-        TL(HGNN_K_GEMM_FWD, launch_gemm_fwd(gf, s));
-        }
+        TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<float>(ws, h.wc), h.kp,
+                                             P.c2, at<float>(ws, h.bc), h.relu_from,
+                                             at<float>(ws, P.feats[h.out].y), P.c2,
+                                             c->training ? at<float>(ws, h.part) : nullptr, s, lg ? 1 : 0));
         }
 
         BnFwdArgs bf{};
@@ -905,7 +884,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     // HGNN_SIDE=0: the weight-gradient work stays on the main stream, with no events at all (a
     // cross-stream event record / wait costs the main stream ~6-7 us of idle GPU per fork)
     static const bool use_side = env_flag("HGNN_SIDE", true);
-    if (P.v2 && use_side) TRY(side_stream(s, &side));
+    if (use_side) TRY(side_stream(s, &side));
     // dY and the bias partials alternate between two buffers, so the side stream's
     // dW of half i may still read its pair while the main stream runs half i+1.
     bool pending[2] = {false, false};
@@ -932,13 +911,16 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             // fused backward: dX needs no dA, only the dense operator gradient does -- its G
             // columns (dY . Wcat_G) are made here, beside the main stream
             if (ndw_side && da_side)
-                TL(HGNN_K_DW_DENSE, launch_gemm3_da(dyb, P.c2, tot, cap, P.c2, at<float>(ws, h.wt), P.c2, P.jt * h.cg,
-                                                    dab, h.kp, s));
+                TL(HGNN_K_DW_DENSE, launch_gemm3_da(dyb, P.c2p, tot, cap, P.c2p, at<float>(ws, h.wt), P.c2p,
+                                                    P.jt * h.cg, dab, h.kp, s));
             if (ndw_side) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, dab, h.kp, false, 1));
-            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(dyb, P.c2, at<float>(ws, h.a), h.kp, tot, cap, P.c2, h.k, kc,
+            // dY rows have stride c2p; the dW GEMM's float4 loads along the 2d outputs read the zero
+            // padding of an odd 2d and store only the 2d real rows of each slab
+            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(dyb, P.c2p, at<float>(ws, h.a), h.kp, tot, cap, P.c2, h.k, kc,
                                                at<float>(ws, P.slabs), s));
-            TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, kc, P.c2, h.k, P.d, grads[h.pw_lin],
-                                                   grads[h.pw_relu], dbp, grads[h.pb_lin], grads[h.pb_relu], s));
+            TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, kc, P.c2, P.c2, h.k, P.d,
+                                                   grads[h.pw_lin], grads[h.pw_relu], dbp, grads[h.pb_lin],
+                                                   grads[h.pb_relu], s));
             if (side) r = hipEventRecord(side->join[parity], s) == hipSuccess ? 0 : HGNN_ERR_HIP;
         } while (0);
         s = main_s;
@@ -984,11 +966,12 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         bb.dy = dyb;
         bb.dw = grads[h.pbn_w];
         bb.db = grads[h.pbn_b];
-        bb.dbpart = P.v2 ? dbp : nullptr;
+        bb.dbpart = dbp;
+        bb.ldy = P.c2p;
         const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
         const bool ndw = need_dw && !h.edge;
         // with a dA GEMM the BN backward's apply pass is fused into its operand staging
-        const bool fused_da = !P.fused_bwd && P.v2 && (ng || np || ndw) && fused_da_enabled();
+        const bool fused_da = !P.fused_bwd && P.c2 % 4 == 0 && (ng || np || ndw) && fused_da_enabled();
         TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s, fused_da ? 0 : 1));
 
         if (P.fused_bwd) {
@@ -1049,56 +1032,22 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             return 0;
         }
 
-        if (!P.v2) {
-            GemmDwArgs gw{};
-            gw.dy = dyb;
-            gw.lddy = P.c2;
-            gw.a = at<float>(ws, h.a);
-            gw.lda = h.k;
-            gw.r_valid = tot;
-            gw.r_cap = cap;
-            gw.o = P.c2;
-            gw.k = h.k;
-            gw.split = P.d;
-            gw.slabs = at<float>(ws, P.slabs);
-            gw.dw0 = grads[h.pw_lin];
-            gw.dw1 = grads[h.pw_relu];
-            gw.db0 = grads[h.pb_lin];
-            gw.db1 = grads[h.pb_relu];
-            TL(HGNN_K_GEMM_DW, launch_gemm_dw(gw, s));
-        }
-
         if (!ng && !np && !ndw) {
-            if (P.v2) TRY(fork_dw(h, cap, tot, dyb, dbp, false, nullptr));
+            TRY(fork_dw(h, cap, tot, dyb, dbp, false, nullptr));
             return 0;
         }
-        float* da = at<float>(ws, (P.v2 && parity) ? P.da2 : P.da);
-        if (P.v2) {
+        float* da = at<float>(ws, parity ? P.da2 : P.da);
+        {
             if (fused_da)
                 TL(HGNN_K_GEMM_DA,
                    launch_gemm3_da_bn(bb, tot, cap, P.c2, at<float>(ws, h.wt), P.c2, h.k, da, h.kp, s));
             else
-                TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2, tot, cap, P.c2, at<float>(ws, h.wt), P.c2, h.k, da,
-                                                   h.kp, s));
+                TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2p, tot, cap, P.c2p, at<float>(ws, h.wt), P.c2p, h.k,
+                                                   da, h.kp, s));
             // dW starts once dA is done: two MFMA GEMMs side by side only slow each other,
             // dW beside the latency-bound dense-dW / aggregation-backward kernels does not
             TRY(fork_dw(h, cap, tot, dyb, dbp, ndw, da));
-        } else {
-            GemmDaArgs gd{};
-            gd.dy = dyb;
-            gd.lddy = P.c2;
-            gd.m_valid = tot;
-            gd.m_cap = cap;
-            gd.o = P.c2;
-            gd.w0 = prm[h.pw_lin];
-            gd.w1 = prm[h.pw_relu];
-            gd.split = P.d;
-            gd.k = h.k;
-            gd.da = da;
-            gd.ldda = h.k;
-            TL(HGNN_K_GEMM_DA, launch_gemm_da(gd, s));
         }
-        if (ndw && !P.v2) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, da, h.kp, false, 1));
         AggBwdArgs gab{}, pab{};
         if (ng) {
             gab.total_rows = tot;

@@ -31,16 +31,17 @@ int launch_repack(const RepackTable& t, hipStream_t s) {
 // gradient of output channel o from the BN-backward tile sums (k_db_reduce's work, same order).
 template <int SG>
 __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ slabs, const int* r_valid,
-                                                    int kchunk, int M, int N, int split, float* dw0, float* dw1,
-                                                    const float* __restrict__ dbpart, float* db0, float* db1) {
+                                                    int kchunk, int M, int MR, int N, int split, float* dw0,
+                                                    float* dw1, const float* __restrict__ dbpart, float* db0,
+                                                    float* db1) {
     constexpr int OUT = 256 / SG;
-    const int nwb = (M * N + OUT - 1) / OUT;
+    const int nwb = (MR * N + OUT - 1) / OUT;
     if ((int)blockIdx.x >= nwb) {
         __shared__ double red[4];
         const int o = blockIdx.x - nwb;
         const int tv = ceil_div(*r_valid, 64);
         double s = 0.0;
-        for (int t = threadIdx.x; t < tv; t += 256) s += (double)dbpart[(long long)t * M + o];
+        for (int t = threadIdx.x; t < tv; t += 256) s += (double)dbpart[(long long)t * MR + o];
         s = wave_sum_d(s);
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
         __syncthreads();
@@ -58,7 +59,7 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
     const int zv = ceil_div(rows, kchunk);
     const long long st = (long long)M * N;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    if (idx < M * N) {
+    if (idx < MR * N) {
         int z = g;
         for (; z + 3 * SG < zv; z += 4 * SG) {
             s0 += slabs[z * st + idx];
@@ -70,7 +71,7 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
     }
     part[g][ol] = (s0 + s1) + (s2 + s3);
     __syncthreads();
-    if (g == 0 && idx < M * N) {
+    if (g == 0 && idx < MR * N) {
         float s = 0.f;
 #pragma unroll
         for (int q = 0; q < SG; ++q) s += part[q][ol];
@@ -80,18 +81,19 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
     }
 }
 
-int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int k, int split, float* dw0,
-                      float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s) {
-    const int total = o * k;
+int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int o_real, int k, int split,
+                      float* dw0, float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s) {
+    if (o_real <= 0 || o_real > o) return HGNN_ERR_ARG;
+    const int total = o_real * k;
     // slab groups by the slab count (upper bound from the capacity is not known here: the host
     // passes the chunk size; more groups when the chunks are short, i.e. many slabs per output)
-    const int nb = dbpart ? o : 0;
+    const int nb = dbpart ? o_real : 0;
     if (kchunk <= 128) {
         hipLaunchKernelGGL(k_dw_reduce2<16>, dim3(ceil_div(total, 16) + nb), dim3(256), 0, s, slabs, r_valid, kchunk,
-                           o, k, split, dw0, dw1, dbpart, db0, db1);
+                           o, o_real, k, split, dw0, dw1, dbpart, db0, db1);
     } else {
         hipLaunchKernelGGL(k_dw_reduce2<4>, dim3(ceil_div(total, 64) + nb), dim3(256), 0, s, slabs, r_valid, kchunk,
-                           o, k, split, dw0, dw1, dbpart, db0, db1);
+                           o, o_real, k, split, dw0, dw1, dbpart, db0, db1);
     }
     HGNN_LAUNCH_CHECK();
     return 0;

@@ -127,3 +127,30 @@ def test_gnn_simple_j2_vs_oracle():
     # reference fp32's own 5.2e-4 (3.2e-6 vs 1.3e-6 relative), inside the first leg (1e-5 relative) but
     # 2.6x the reference's error, so the fp64 leg is held at 3x here
     _check(model, b, 6, 0, kind="simple", factor=3.0)
+
+
+@pytest.mark.parametrize("d", [1, 3])
+@pytest.mark.parametrize("order", [1, 2, 3])
+def test_gnn_lg_odd_widths_vs_oracle(d, order):
+    """2d = 2 / 6 output channels (n_features = 1 is the reference driver's default,
+    scripts/main_gnn_qm9.py:78, and scripts/exp_lggnn_qm9.sh's h=1): the padded-stride path of
+    the Conv1d-pair GEMMs (dY and the repacked WT at a row stride of 2d rounded up to 4, the
+    scalar BN-backward apply zeroing the padding) against the oracle -- outputs on the two-leg
+    bound, loss, every parameter grad, dX and the dense W.grad (model_mnb.py:69-129)."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_lg
+    b = _batch(dg.qm9_shape_dataset(64, seed=500 + 10 * d + order))
+    model = GNN_lg(0, d, 5, 5, 1, 1, order).cuda()
+    fu.det_init(model, 510 + 10 * d + order)
+    _check(model, b, 5, order)
+
+
+@pytest.mark.parametrize("d", [1, 3])
+def test_gnn_simple_odd_widths_vs_oracle(d):
+    """GNN_simple at 2d = 2 / 6 (scripts/main_gnn.py with --h 1 / 3) on 24 SBM-50 graphs."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_simple
+    b = _batch(dg.sbm_dataset(24, n=50, seed=520 + d))
+    model = GNN_simple(0, d, 5, 5, 1, 1).cuda()
+    fu.det_init(model, 530 + d)
+    _check(model, b, 5, 0, kind="simple")

@@ -318,3 +318,56 @@ def test_gnn_lg_d128_config4_model_vs_oracle_fp64():
     _, _, _, dx32 = _oracle_lg(model, b, 4, 2, dtype=torch.float32)
     ref32_err = (dx32.double() - ref_dx).abs().max().item()
     assert err <= max(1e-4 * max(1.0, ref_dx.abs().max().item()), 2.0 * ref32_err), (err, ref32_err)
+
+
+@pytest.mark.parametrize("name", LG_CASES + ["gnn_simple"])
+def test_csr_path_matches_reference_fixture(golden, name):
+    """The CSR executor path (native batcher -> hgnn_net_forward_csr / hgnn_net_backward_csr, no
+    dense operators) on the reference's fixture graphs against the reference's own recorded
+    outputs, loss, parameter grads, dX, running statistics and eval outputs
+    (functions/batching.py:77-185 semantics, models/gnns/model_mnb.py:58-66, 124-129)."""
+    from hgnn_amd.csr import CsrBatch
+    from models.gnns.model_mnb import GNN_lg, GNN_simple
+    z = golden(name)
+    graphs = fu.unpack_graphs(z)
+    lg = name != "gnn_simple"
+    if lg:
+        d, L, order, bs, wseed = [int(v) for v in z["cfg"]]
+        model = GNN_lg(0, d, L, 5, 1, 1, order).cuda()
+        out_key, out64_key, gpref, dx_key = "out", "out64", "grad.", "dX"
+    else:
+        L, wseed = 20, 201
+        model = GNN_simple(0, 2, L, 5, 1, 1).cuda()
+        out_key, out64_key, gpref, dx_key = "out32", "out64", "grad32.", "dX32"
+    fu.det_init(model, wseed)
+    model.train()
+    b = CsrBatch([(x, a) for x, a, _ in graphs], dual=lg, targets=torch.stack([t[0] for _, _, t in graphs]))
+    b.x.requires_grad_(True)
+    out = model.forward_csr(b)
+    loss = torch.nn.MSELoss()(out, b.T)
+    loss.backward()
+    torch.cuda.synchronize()
+    o = out.detach().cpu().numpy()
+    ref, ref64 = z[out_key], z[out64_key]
+    assert np.max(np.abs(o - ref)) <= 1e-5 * max(1.0, np.abs(ref).max())
+    assert np.max(np.abs(o - ref64)) <= 2 * np.max(np.abs(ref - ref64)) + 1e-6
+    lref = float(z["loss" if lg else "loss32"])
+    assert abs(loss.item() - lref) <= 1e-5 * max(1.0, abs(lref))
+    _check_grads({k: p.grad for k, p in model.named_parameters()}, z, prefix=gpref)
+    # dX: the fixture's dense (bs, f, Nmax) gradient, packed like the CSR batch's rows
+    dxr = z[dx_key]
+    packed = np.concatenate([dxr[g, :, :x.shape[0]].T for g, (x, _, _) in enumerate(graphs)])
+    dx = b.x.grad.cpu().numpy()
+    assert dx.shape == packed.shape
+    assert np.max(np.abs(dx - packed)) <= 1e-4 * max(1.0, np.abs(packed).max()) + 1e-6
+    if lg:
+        for l in range(L - 1):
+            layer = model.layer0 if l == 0 else getattr(model, f"layer{l}")
+            for nm in ("bn1", "bn2"):
+                bn = getattr(layer, nm)
+                np.testing.assert_allclose(bn.running_mean.cpu().numpy(), z[f"rmean.layer{l}.{nm}"], rtol=1e-5, atol=1e-5)
+                np.testing.assert_allclose(bn.running_std.cpu().numpy(), z[f"rstd.layer{l}.{nm}"], rtol=1e-5, atol=1e-5)
+    model.eval()
+    with torch.no_grad():
+        oe = model.forward_csr(b).cpu().numpy()
+    assert np.max(np.abs(oe - z["out_eval"])) <= 1e-5 * max(1.0, np.abs(z["out_eval"]).max())
