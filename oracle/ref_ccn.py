@@ -113,36 +113,40 @@ def ccn2_forward_closed(p, X, adj, layers):
     which the reference itself cannot (5.65 GB per node).  Pinned against ccn_forward on small
     graphs by tests/test_oracle.py; vectorised per node, any dtype (fp64 for parity)."""
     n_nodes = X.shape[0]
-    nbrs = receptive_fields(adj)
-    F = [X[i].view(1, 1, -1).expand(len(nbrs[i]), len(nbrs[i]), -1) for i in range(n_nodes)]
+    nbrs = [torch.nonzero(adj[i] > 0).view(-1) for i in range(n_nodes)]
+    deg = [len(v) for v in nbrs]
+    idx = torch.full((n_nodes, n_nodes), -1, dtype=torch.long)  # idx[j, v] = position of v in nbr_j
+    for j in range(n_nodes):
+        idx[j, nbrs[j]] = torch.arange(deg[j])
+    F = [X[i].view(1, 1, -1).expand(deg[i], deg[i], -1) for i in range(n_nodes)]
     levels = [F]
+    dmax = max(deg) if deg else 0
     for l in range(layers):
         new = []
+        # (nodes, dmax, dmax, C) zero-padded, autograd through it
+        Fp = torch.stack([Fn.pad(f, (0, 0, 0, dmax - f.shape[1], 0, dmax - f.shape[0])) for f in F], 0)
         for i in range(n_nodes):
-            n = len(nbrs[i])
-            rows = []
-            for j in nbrs[i]:
-                pj = torch.tensor(positions(nbrs, i, j))
-                valid = pj >= 0
-                q = pj.clamp(min=0)
-                sub = F[j][q][:, q]                       # (n, n, C) = F_j[p(x)][p(y)]
-                m = (valid.view(-1, 1) & valid.view(1, -1)).to(sub.dtype).unsqueeze(-1)
-                rows.append(sub * m)
-            T = torch.stack(rows, 0)                      # [a][b][c][ch]
+            n = deg[i]
+            J = nbrs[i]
+            P = idx[J][:, J]                              # P[a][x] = position of nbr_i[x] in nbr_{j_a}
+            q = P.clamp(min=0)
+            valid = (P >= 0).to(X.dtype)
+            # T[a][b][c] = F_{j_a}[p_a(b)][p_a(c)], 0 where either position is absent
+            T = Fp[J.view(-1, 1, 1), q.unsqueeze(2), q.unsqueeze(1)] * (valid.unsqueeze(2) * valid.unsqueeze(1)).unsqueeze(-1)
             Sc = T.sum(2)                                 # [a][b]
             Sa = T.sum(0)                                 # [b][c]
             q1 = Sc.sum(1)                                # [a]
             q3 = Sa.sum(1)                                # [b]
             tot = Sc.sum((0, 1))
-            idx = torch.arange(n)
-            d3 = T[idx, idx, idx].sum(0)
+            ar = torch.arange(n)
+            d3 = T[ar, ar, ar].sum(0)
             eye = torch.eye(n, dtype=T.dtype).unsqueeze(-1)
             nf = float(n)
             blocks = [nf * Sc, q1.view(n, 1, -1).expand(n, n, -1), nf * Sa, q3.view(n, 1, -1).expand(n, n, -1),
                       eye * tot, Sc]
             blocks += [nf * Sc] * 9
-            blocks += [T[:, idx, idx],                    # q15[x][y] = T[x][y][y]
-                       T[idx, :, idx].transpose(0, 1),    # q16[x][y] = T[y][x][y]
+            blocks += [T[:, ar, ar],                      # q15[x][y] = T[x][y][y]
+                       T[ar, :, ar].transpose(0, 1),      # q16[x][y] = T[y][x][y]
                        eye * d3]
             coll = torch.cat(blocks, 2)                   # (n, n, 18 C), channel q * C + ch
             new.append(Fn.relu(_linear(p, "w{}".format(l + 1), coll)))

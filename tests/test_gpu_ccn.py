@@ -245,3 +245,85 @@ def test_ccn2_wide_channels_vs_closed_form_oracle(hidden):
         _grad_close(Xr.grad[b, :x.shape[0]], xr.grad, f"hidden {hidden} dX graph {b}")
     for n, p in net.named_parameters():
         _grad_close(p.grad, p64[n].grad, f"hidden {hidden} grad {n}")
+
+
+def test_ccn1_config3_full_batch_256_vs_oracle():
+    """Config 3 at its size: CCN_1D(5, 1, 2, 2) (scripts/main_ccn_qm9.py:69-74 defaults) on 256
+    QM9-shape graphs in one forward_batch call, loss = sum of the per-graph MSE (the reference's
+    per-graph train_ccn step, scripts/train_ccn.py:52-60, summed), against the fp64 oracle per graph
+    (oracle/ref_ccn.py ccn1_forward_vec, pinned to the literal restatement): every output, every
+    graph's dX and the parameter gradients."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_1D
+    from oracle import ref_ccn as RC
+    graphs = [(X, A + torch.eye(A.shape[0]), t) for X, A, t in dg.qm9_shape_dataset(256, seed=303)]
+    net = CCN_1D(5, 1, 2, 2)
+    fu.det_init(net, 303)
+    p64 = {n: v.detach().double().clone().requires_grad_(True) for n, v in net.named_parameters()}
+    net = net.cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    T = torch.stack([t[0] for _, _, t in graphs]).view(-1, 1)
+    Xr = X.clone().requires_grad_(True)
+    out = net.forward_batch(Xr, A, nb)
+    ((out - T.cuda()) ** 2).sum().backward()
+    loss64 = 0.0
+    for b, (x, a, _) in enumerate(graphs):
+        xr = x.double().requires_grad_(True)
+        ref = RC.ccn1_forward_vec(p64, xr, a.double(), 2)
+        _close(out[b], ref, f"cfg3 graph {b}")
+        lb = ((ref - T[b].double()) ** 2).sum()
+        lb.backward()
+        loss64 += lb.item()
+        _grad_close(Xr.grad[b, :x.shape[0]], xr.grad, f"cfg3 dX graph {b}")
+    for n, p in net.named_parameters():
+        _grad_close(p.grad, p64[n].grad, f"cfg3 grad {n}")
+
+
+def test_ccn2_config5_full_batch_64_sbm200():
+    """Config 5 at its size: CCN_2D(5, 1, 2, 2) on 64 SBM-200 graphs (degrees up to ~57).
+    (1) Full-size property: one forward_batch call equals the drop-in per-graph forward(X, adj)
+    that scripts/train_ccn.py:52 calls, on all 64 graphs -- outputs, each graph's dX and the
+    parameter gradients (the per-graph backward passes summed).  (2) The reference cannot run
+    SBM-200 (d^5 intermediates): 8 of the 64 graphs against the fp64 closed-form
+    oracle (oracle/ref_ccn.py ccn2_forward_closed, pinned to the literal restatement) -- outputs,
+    dX, and the parameter gradients of those 8 graphs' terms."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_2D
+    from oracle import ref_ccn as RC
+    graphs = [(X, A + torch.eye(A.shape[0]), t) for X, A, t in dg.sbm_dataset(64, n=200, seed=505)]
+    net = CCN_2D(5, 1, 2, 2)
+    fu.det_init(net, 505)
+    p64 = {n: v.detach().double().clone().requires_grad_(True) for n, v in net.named_parameters()}
+    net = net.cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    w = torch.randn(64, 1, generator=torch.Generator().manual_seed(506))
+    Xr = X.clone().requires_grad_(True)
+    out = net.forward_batch(Xr, A, nb)
+    params = [p for _, p in net.named_parameters()]
+    gb = torch.autograd.grad((out * w.cuda()).sum(), [Xr] + params, retain_graph=True)
+    # (1) per-graph drop-in path on all 64 graphs
+    gsum = [torch.zeros_like(p) for p in params]
+    for b, (x, a, _) in enumerate(graphs):
+        xr = x.cuda().requires_grad_(True)
+        o = net(xr, a.cuda())
+        _close(o, out[b].detach().cpu(), f"cfg5 per-graph out {b}", rel=1e-6)
+        gs = torch.autograd.grad((o * w[b].cuda()).sum(), [xr] + params)
+        _close(gs[0], gb[0][b, :x.shape[0]].cpu(), f"cfg5 per-graph dX {b}", rel=1e-5)
+        for acc, g in zip(gsum, gs[1:]):
+            acc += g
+    for (n, _), g1, g2 in zip(net.named_parameters(), gb[1:], gsum):
+        _grad_close(g1, g2.cpu(), f"cfg5 per-graph sum grad {n}")
+    # (2) the closed-form fp64 oracle on 8 of the graphs
+    sel = list(range(0, 64, 8))
+    wsel = torch.zeros(64, 1)
+    wsel[sel] = w[sel]
+    g8 = torch.autograd.grad((out * wsel.cuda()).sum(), params)
+    for b in sel:
+        x, a, _ = graphs[b]
+        xr = x.double().requires_grad_(True)
+        ref = RC.ccn2_forward_closed(p64, xr, a.double(), 2)
+        _close(out[b], ref, f"cfg5 graph {b}")
+        (ref * w[b].double()).sum().backward()
+        _grad_close(gb[0][b, :x.shape[0]], xr.grad, f"cfg5 dX graph {b}")
+    for (n, _), g in zip(net.named_parameters(), g8):
+        _grad_close(g, p64[n].grad, f"cfg5 grad {n}")
