@@ -968,7 +968,11 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
         const char* e = getenv("HGNN_BN_SMALL");
         return e && e[0] == '1';
     }();
-    if (apply && v4 && !one_block && bn2_enabled() && tiles > 0 && (a.c == 4 || a.c == 8 || a.c == 16)) {
+    // the two-launch forms sum every statistics partial in each apply block's prologue (O(tiles^2 C)
+    // L2 reads): only up to 192 row tiles of capacity (49 K rows; config 2's edge half is 140 with 91
+    // live); larger inputs take part4 + fin + apply4
+    const bool few = ceil_div(a.cap_rows, BN2_ROWS) <= 192;
+    if (apply && v4 && !one_block && bn2_enabled() && few && tiles > 0 && (a.c == 4 || a.c == 8 || a.c == 16)) {
         if (a.c == 4) bn2s_launch<1>(a, s);
         else if (a.c == 8) bn2s_launch<2>(a, s);
         else bn2s_launch<4>(a, s);
@@ -980,7 +984,7 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
         HGNN_LAUNCH_CHECK();
         return 0;
     }
-    if (apply && v4 && tiles > 0 && bn2_enabled() && (a.c == 64 || a.c == 128 || a.c == 256)) {
+    if (apply && v4 && tiles > 0 && bn2_enabled() && few && (a.c == 64 || a.c == 128 || a.c == 256)) {
         if (a.c == 64) bn2_launch<16>(a, s);
         else if (a.c == 128) bn2_launch<32>(a, s);
         else bn2_launch<64>(a, s);
@@ -1161,12 +1165,37 @@ __global__ void __launch_bounds__(RA_THREADS) k_readout_agg_bwd(ReadoutAggArgs a
     }
 }
 
-int launch_readout_agg_bwd(const ReadoutAggArgs& a, hipStream_t s) {
-    if (a.jt > 8 || (!a.g_out && !a.p_out)) return a.jt > 8 ? HGNN_ERR_UNSUPPORTED : 0;
+// dynamic LDS of the two readout-row kernels (beyond 64 KB allowed per kernel, up to the CU's 160 KB)
+constexpr size_t RO_LDS_CAP = 160 * 1024;
+
+static size_t readout_agg_bwd_lds(const ReadoutAggArgs& a) {
     const int maxrows = a.p_out ? (a.p_cap + a.bs - 1) / a.bs : 0;  // rows per graph <= emax
     const int grow = (a.g_cap + a.bs - 1) / a.bs;
-    const size_t lds = sizeof(float) * (size_t)std::max(a.jt * a.cg + grow * a.jt, 2 * a.cp + maxrows * 2);
-    if (lds > 64 * 1024) return HGNN_ERR_UNSUPPORTED;
+    return sizeof(float) * (size_t)std::max(a.jt * a.cg + grow * a.jt, 2 * a.cp + maxrows * 2);
+}
+
+static size_t dw_readout_lds(const DwDenseArgs& a) {
+    return sizeof(float) * ((size_t)a.jt * a.f + (size_t)a.nmax * (a.f + 1) + (size_t)a.nmax * a.jt);
+}
+
+template <typename K>
+static void allow_ro_lds(K* kernel, size_t lds) {
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)RO_LDS_CAP);
+}
+
+bool readout_row_fits(const ReadoutAggArgs& ra, const DwDenseArgs* dw) {
+    if (ra.jt > 8) return false;
+    if ((ra.g_out || ra.p_out) && readout_agg_bwd_lds(ra) > RO_LDS_CAP) return false;
+    return !dw || dw_readout_lds(*dw) <= RO_LDS_CAP;
+}
+
+int launch_readout_agg_bwd(const ReadoutAggArgs& a, hipStream_t s) {
+    if (a.jt > 8 || (!a.g_out && !a.p_out)) return a.jt > 8 ? HGNN_ERR_UNSUPPORTED : 0;
+    const size_t lds = readout_agg_bwd_lds(a);
+    if (lds > RO_LDS_CAP) return HGNN_ERR_UNSUPPORTED;
+    allow_ro_lds(k_readout_agg_bwd, lds);
     hipLaunchKernelGGL(k_readout_agg_bwd, dim3(a.bs, a.p_out ? 2 : 1), dim3(RA_THREADS), lds, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;
@@ -1216,8 +1245,9 @@ __global__ void __launch_bounds__(256) k_dw_readout(DwDenseArgs a) {
 }
 
 int launch_dw_readout(const DwDenseArgs& a, hipStream_t s) {
-    const size_t lds = sizeof(float) * ((size_t)a.jt * a.f + (size_t)a.nmax * (a.f + 1) + (size_t)a.nmax * a.jt);
-    if (lds > 64 * 1024 || !a.dout) return HGNN_ERR_UNSUPPORTED;
+    const size_t lds = dw_readout_lds(a);
+    if (lds > RO_LDS_CAP || !a.dout) return HGNN_ERR_UNSUPPORTED;
+    allow_ro_lds(k_dw_readout, lds);
     hipLaunchKernelGGL(k_dw_readout, dim3(a.bs), dim3(256), lds, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;

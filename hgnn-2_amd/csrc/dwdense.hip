@@ -226,10 +226,11 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
 template <int FC, int MAXI, bool JS>
 static void allow_lds(size_t lds) {
     // dynamic LDS beyond 64 KB must be allowed per kernel (gfx950: 160 KB per CU)
+    // (the whole 160 KB once: a first call with a smaller size must not cap a later, larger one)
     static bool done = false;
     if (!done && lds > 64 * 1024) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_dense<FC, MAXI, JS>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         done = true;
     }
 }
@@ -314,14 +315,20 @@ int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
     }
     const int npad = (a.nmax + 31) / 32 * 32;
     // one F chunk when it fits (F = 2d = 128 at config 2): 19.1 -> 18.3 us per launch
-    const int fc = npad <= 32 ? (a.f > 64 ? 128 : 64) : (npad <= 64 ? 32 : 16);
+    int fc = npad <= 32 ? (a.f > 64 ? 128 : 64) : (npad <= 64 ? 32 : 16);
     const int tiles = npad / 32;
     // large batches: one block per (graph, slice); few graphs (cfg1: 32): the items' passes of a
     // graph spread over blocks instead, so the grid is not a handful of long blocks
     const bool js = jsplit_enabled() && a.bs >= 256;
     const int J = js ? 1 : a.jt;
-    const size_t lds = sizeof(float) * ((size_t)npad * ((J * fc + 1) + (fc + 1)) + (size_t)J * fc + 3 * fc);
-    if (lds > 96 * 1024) return 2;
+    auto lds_of = [&](int c) {
+        return sizeof(float) * ((size_t)npad * ((J * c + 1) + (c + 1)) + (size_t)J * c + 3 * c);
+    };
+    // the graph's G and X rows stay in LDS (up to the CU's 160 KB): SBM graphs of several hundred
+    // nodes take 8-channel chunks (Nmax <= ~1200 at J + 2 = 3 slices)
+    if (lds_of(fc) > 160 * 1024) fc = 8;
+    const size_t lds = lds_of(fc);
+    if (lds > 160 * 1024) return HGNN_ERR_UNSUPPORTED;
     const int nitems = tiles * tiles * J;
     int maxi = ceil_div(nitems, 4), gy = js ? a.jt : 1;
     if (!js && a.bs < 256 && nitems > 4) {
@@ -332,7 +339,8 @@ int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
     if (fc == 128) launch_fc<128, JS>(a, maxi, gy, lds, s);    \
     else if (fc == 64) launch_fc<64, JS>(a, maxi, gy, lds, s); \
     else if (fc == 32) launch_fc<32, JS>(a, maxi, gy, lds, s); \
-    else launch_fc<16, JS>(a, maxi, gy, lds, s);
+    else if (fc == 16) launch_fc<16, JS>(a, maxi, gy, lds, s); \
+    else launch_fc<8, JS>(a, maxi, gy, lds, s);
     if (js) {
         HGNN_DW_FC(true)
     } else {

@@ -383,6 +383,10 @@ struct ReadoutAggArgs {
     int p_acc;
 };
 int launch_readout_agg_bwd(const ReadoutAggArgs& a, hipStream_t s);
+// whether the readout-row backward (launch_readout_agg_bwd and, with dw, launch_dw_readout) fits its
+// LDS; the executor falls back to the materialised [rows][K] readout gradient otherwise
+struct DwDenseArgs;
+bool readout_row_fits(const ReadoutAggArgs& ra, const DwDenseArgs* dw);
 // dW of the readout layer's graph_oper: dW[b, n, m, j] (+)= sum_f R_b[j F + f] X[m, f], every n
 int launch_dw_readout(const DwDenseArgs& a, hipStream_t s);
 

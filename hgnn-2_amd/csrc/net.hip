@@ -806,37 +806,40 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     // readout
     TL(HGNN_K_READOUT, launch_readout_bwd_params(dout, at<float>(ws, P.colsum), c->bs, c->nmax, c->dim_out, P.k_last,
                                   grads[P.p_fcw], grads[P.p_fcb], at<void>(ws, P.rb_scratch), s));
-    // HGNN_READOUT_ROW=0: the readout gradient materialised as a [rows][K] buffer and gathered
+    // HGNN_READOUT_ROW=0: the readout gradient materialised as a [rows][K] buffer and gathered.  The
+    // readout-row kernels hold a graph's rows in LDS: configurations beyond it (wide 2d with a large
+    // Nmax / Emax) take the materialised form as well.
     static const bool ro_row = env_flag("HGNN_READOUT_ROW", true);
-    if (ro_row && P.jt <= 8 && (needs_grad(P.last_gin) || needs_grad(P.last_pin) || need_dw)) {
-        if (need_dw) TL(HGNN_K_DW_DENSE, launch_dw_readout(dw_args(P.last_gin, nullptr, 0, true, 0), s));
-        const bool lg = needs_grad(P.last_gin), lp = needs_grad(P.last_pin);
-        ReadoutAggArgs ra{};
-        ra.dout = dout;
-        ra.fcw = prm[P.p_fcw];
-        ra.dim_out = c->dim_out;
-        ra.k = P.k_last;
-        ra.jt = P.jt;
-        ra.cg = P.feats[P.last_gin].c;
-        ra.cp = P.last_pin >= 0 ? P.feats[P.last_pin].c : 0;
-        ra.bs = c->bs;
-        ra.node_off = m.node_off;
-        ra.edge_off = m.edge_off;
-        ra.g = src.v[S_WT];
-        ra.g_total = tot_n;
-        ra.g_cap = P.cap_n;
-        ra.g_out = lg ? at<float>(ws, P.feats[P.last_gin].grad) : nullptr;
-        ra.g_acc = init[P.last_gin];
-        if (lp) {
-            ra.p = src.v[S_PE];
-            ra.p_total = tot_e;
-            ra.p_cap = P.cap_e;
-            ra.p_out = at<float>(ws, P.feats[P.last_pin].grad);
-            ra.p_acc = init[P.last_pin];
-        }
-        if (lg || lp) TL(HGNN_K_AGG_BWD, launch_readout_agg_bwd(ra, s));
-        if (lg) init[P.last_gin] = 1;
-        if (lp) init[P.last_pin] = 1;
+    const bool lgr = needs_grad(P.last_gin), lpr = needs_grad(P.last_pin);
+    ReadoutAggArgs ra{};
+    ra.dout = dout;
+    ra.fcw = prm[P.p_fcw];
+    ra.dim_out = c->dim_out;
+    ra.k = P.k_last;
+    ra.jt = P.jt;
+    ra.cg = P.feats[P.last_gin].c;
+    ra.cp = P.last_pin >= 0 ? P.feats[P.last_pin].c : 0;
+    ra.bs = c->bs;
+    ra.node_off = m.node_off;
+    ra.edge_off = m.edge_off;
+    ra.g = src.v[S_WT];
+    ra.g_total = tot_n;
+    ra.g_cap = P.cap_n;
+    ra.g_out = lgr ? at<float>(ws, P.feats[P.last_gin].grad) : nullptr;
+    ra.g_acc = init[P.last_gin];
+    if (lpr) {
+        ra.p = src.v[S_PE];
+        ra.p_total = tot_e;
+        ra.p_cap = P.cap_e;
+        ra.p_out = at<float>(ws, P.feats[P.last_pin].grad);
+        ra.p_acc = init[P.last_pin];
+    }
+    const DwDenseArgs dwr = need_dw ? dw_args(P.last_gin, nullptr, 0, true, 0) : DwDenseArgs{};
+    if (ro_row && (lgr || lpr || need_dw) && readout_row_fits(ra, need_dw ? &dwr : nullptr)) {
+        if (need_dw) TL(HGNN_K_DW_DENSE, launch_dw_readout(dwr, s));
+        if (lgr || lpr) TL(HGNN_K_AGG_BWD, launch_readout_agg_bwd(ra, s));
+        if (lgr) init[P.last_gin] = 1;
+        if (lpr) init[P.last_pin] = 1;
     } else if (needs_grad(P.last_gin) || needs_grad(P.last_pin) || need_dw) {
         float* da = at<float>(ws, P.da);
         TL(HGNN_K_READOUT, launch_readout_bwd_da(dout, m.node_off, c->bs, P.cap_n, tot_n, prm[P.p_fcw], c->dim_out, P.k_last,

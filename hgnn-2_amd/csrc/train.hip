@@ -69,7 +69,10 @@ __global__ void __launch_bounds__(256) k_xent_loss(const float* __restrict__ out
         const float* x = out + (long long)i * c;
         const int ti = (int)t[i];  // LongTensor cast truncates toward zero
         if (ti < 0 || ti >= c || (float)ti != t[i]) {
+            // a rejected row contributes nothing: its dout row is zero, never uninitialised memory
             atomicOr(err, 1u);
+            if (dout)
+                for (int k = 0; k < c; ++k) dout[(long long)i * c + k] = 0.f;
             continue;
         }
         float m = x[0];

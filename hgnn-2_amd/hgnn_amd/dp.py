@@ -129,6 +129,12 @@ class LayerBucketAllReduce:
     it enqueues, last layer first, a wait on the layer's events and the all-reduce of its
     bucket on a communication stream, then joins that stream and divides by the world size.
     sync_running=True also averages the BN running statistics.
+
+    Gradient accumulation: the overlapped path needs every p.grad to be None at backward time
+    (optimizer.zero_grad(), whose default is set_to_none=True).  When a p.grad is present
+    (zero_grad(set_to_none=False), or several backwards per step) the executor writes fresh
+    gradient tensors that autograd adds to p.grad as usual; the call then copies the accumulated
+    gradients into the flat buffer and all-reduces it in one collective after the backward.
     """
 
     def __init__(self, model, group=None, sync_running=True):
@@ -165,24 +171,51 @@ class LayerBucketAllReduce:
                 self.events.append(ev)
             self.comm = torch.cuda.Stream(dev)
         self.event_handles = [int(e.cuda_event) for e in self.events]
+        # set by the executor's backward (net._grad_targets): True when the gradients went to fresh
+        # tensors (some p.grad present), i.e. no per-layer events were recorded this step
+        self.fresh = False
         _ATTACHED[model] = self
+
+    def grad_targets(self):
+        """(views, use_events): the flat buffer's views and True when every p.grad is None, else
+        (None, False) -- the executor then writes fresh tensors for autograd to accumulate."""
+        self.fresh = any(p.grad is not None for p in self.params)
+        return (None, False) if self.fresh else (self.views, True)
 
     def __call__(self):
         world = _world(self.group)
-        # the executor wrote into self.views; autograd may have copied instead of stealing them
+        fresh = self.fresh
+        # the executor wrote into self.views (autograd may have copied instead of stealing them), or,
+        # with accumulation, autograd summed fresh gradients into p.grad: gather those into the views
         for p, v in zip(self.params, self.views):
-            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
-                p.grad = v
+            if p.grad is None:
+                if fresh:
+                    v.zero_()  # a parameter without a gradient this step
+            elif p.grad.data_ptr() != v.data_ptr():
+                if fresh:
+                    v.copy_(p.grad)
+            p.grad = v
+        self.fresh = False
         if world == 1:
             return
-        cur = torch.cuda.current_stream(self.device)
-        for l in reversed(range(len(self.buckets))):
-            self.comm.wait_event(self.events[2 * l])
-            self.comm.wait_event(self.events[2 * l + 1])
-            off, n = self.buckets[l]
-            with torch.cuda.stream(self.comm):
-                dist.all_reduce(self.flat[off:off + n], group=self.group)
-        cur.wait_stream(self.comm)
+        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        if fresh or cur is None:
+            # no per-layer events this step: one collective over the whole buffer after the backward
+            if cur is not None:
+                self.comm.wait_stream(cur)
+                with torch.cuda.stream(self.comm):
+                    dist.all_reduce(self.flat, group=self.group)
+                cur.wait_stream(self.comm)
+            else:
+                dist.all_reduce(self.flat, group=self.group)
+        else:
+            for l in reversed(range(len(self.buckets))):
+                self.comm.wait_event(self.events[2 * l])
+                self.comm.wait_event(self.events[2 * l + 1])
+                off, n = self.buckets[l]
+                with torch.cuda.stream(self.comm):
+                    dist.all_reduce(self.flat[off:off + n], group=self.group)
+            cur.wait_stream(self.comm)
         self.flat.div_(world)
         if self.sync_running:
             average_running_stats(self.model, self.group)

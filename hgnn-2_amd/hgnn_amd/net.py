@@ -287,8 +287,11 @@ def _grad_targets(spec, params):
     dp = spec.dp
     if dp is not None and len(dp.views) == len(params) and all(
             v.shape == p.shape and v.device == p.device for v, p in zip(dp.views, params)):
-        evs = (ctypes.c_void_p * max(1, len(dp.event_handles)))(*dp.event_handles)
-        return list(dp.views), evs, len(dp.event_handles)
+        views, use_events = dp.grad_targets()
+        if use_events:
+            evs = (ctypes.c_void_p * max(1, len(dp.event_handles)))(*dp.event_handles)
+            return list(views), evs, len(dp.event_handles)
+        # some p.grad present: fresh tensors, accumulated by autograd (dp.py, gradient accumulation)
     # one allocation for all of them (50 empty_like calls were ~0.1 ms of host time per step)
     sizes = [p.numel() for p in params]
     flat = torch.empty(sum(sizes), dtype=torch.float32, device=params[0].device)

@@ -20,6 +20,7 @@ hgnn_xent_loss instead; the MAE meters stay untouched as in the reference.
 """
 
 import ctypes
+import os
 
 import torch
 
@@ -34,11 +35,15 @@ class TrainStep:
     [loss, mae, running loss, running mae] (read it when you log, not per step).
     """
 
-    def __init__(self, model, lr=3e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, t_mean=0.0, t_std=1.0,
+    def __init__(self, model, lr=3e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, t_mean=None, t_std=1.0,
                  grad_allreduce=None, classification=None):
         self.model = model
-        # the reference's rule: mean == 0 marks generated (classification) data
-        self.classification = (float(t_mean) == 0.0) if classification is None else bool(classification)
+        # the reference's rule (train_mnb.py:50-51): mean == 0 marks generated (classification) data --
+        # inferred only from an explicitly passed t_mean; TrainStep(model) is the regression step
+        if classification is None:
+            classification = t_mean is not None and float(t_mean) == 0.0
+        self.classification = bool(classification)
+        t_mean = 0.0 if t_mean is None else t_mean
         self.params = [p for p in model.parameters()]
         self.lr = float(lr)
         self.betas = (float(betas[0]), float(betas[1]))
@@ -55,6 +60,10 @@ class TrainStep:
                 raise RuntimeError("hgnn_amd: TrainStep needs contiguous float32 parameters")
         self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
         self._err = torch.zeros(1, dtype=torch.int32, device=dev)
+        # the class-target error word, copied to pinned memory behind an event and checked at the
+        # next step without synchronising the stream (HGNN_STRICT=1: checked at once)
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._err_ev = None
         self._numel = (ctypes.c_int64 * len(self.params))(*[p.numel() for p in self.params])
         self.reset_optimizer()
 
@@ -82,8 +91,24 @@ class TrainStep:
             out = m([X, W], Nb, mask)
         return out, T
 
+    def _poll_targets(self, block):
+        ev = self._err_ev
+        if ev is None:
+            return
+        if block:
+            ev.synchronize()
+        elif not ev.query():
+            return
+        self._err_ev = None
+        if int(self._err_host[0]):
+            self._err.zero_()
+            self._err_host.zero_()
+            raise RuntimeError("hgnn_amd: class target outside [0, dim_output) or not an integer "
+                               "(the rows were left out of the loss and gradients)")
+
     def __call__(self, batch):
         lib = L.lib()
+        self._poll_targets(block=False)
         self.model.train()
         for p in self.params:
             p.grad = None
@@ -92,10 +117,22 @@ class TrainStep:
         stream = L.stream_handle(out.device)
         dout = torch.empty_like(out)
         if self.classification:
+            if out.shape[1] < 2:
+                raise RuntimeError("hgnn_amd: classification needs dim_output >= 2 (cross-entropy over one "
+                                   "class is identically 0); pass t_mean != 0 or classification=False")
             if T.numel() != out.shape[0]:
                 raise RuntimeError(f"hgnn_amd: class targets {tuple(T.shape)} do not match {out.shape[0]} rows")
             L.check(lib.hgnn_xent_loss(L.ptr(out.detach()), L.ptr(T), out.shape[0], out.shape[1], L.ptr(self.stats),
                                        L.ptr(dout), L.ptr(self._err), stream), "cross-entropy loss")
+            if os.environ.get("HGNN_STRICT", "0") == "1":
+                self._err_ev = None
+                if int(self._err.item()):
+                    self._err.zero_()
+                    raise RuntimeError("hgnn_amd: class target outside [0, dim_output) or not an integer")
+            elif not torch.cuda.is_current_stream_capturing():
+                self._err_host.copy_(self._err, non_blocking=True)
+                self._err_ev = torch.cuda.Event()
+                self._err_ev.record()
         else:
             if T.numel() != out.numel():
                 raise RuntimeError(f"hgnn_amd: targets {tuple(T.shape)} do not match the output {tuple(out.shape)}")
@@ -116,5 +153,7 @@ class TrainStep:
 
     def check_targets(self):
         """Raise if a classification step saw a target outside [0, dim_output) (host sync)."""
+        self._poll_targets(block=True)
         if int(self._err.item()):
+            self._err.zero_()
             raise RuntimeError("hgnn_amd: class target outside [0, dim_output) or not an integer")

@@ -52,7 +52,7 @@ def _batch(graphs):
     return list(prepare_batch(data, 0, 1))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="none"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ.setdefault("HGNN_STRICT", "1")
@@ -71,8 +71,12 @@ def _worker(rank, world, port, q):
         fu.det_init(model, WSEED)
         dp = LayerBucketAllReduce(model)
         for step in range(2):  # twice: the flat buffer and the events are reused across steps
-            for p in model.parameters():
-                p.grad = None
+            if mode == "none":
+                model.zero_grad(set_to_none=True)
+            elif mode == "zero":
+                model.zero_grad(set_to_none=False)  # p.grad kept (the flat buffer's views), zeroed
+            elif step == 0:  # "accum": the second backward adds to the first step's averaged grads
+                model.zero_grad(set_to_none=True)
             out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
             torch.nn.MSELoss()(out, T).backward()
             dp()
@@ -108,12 +112,16 @@ def _oracle_shard(graphs, idx):
     return runs[-1], st
 
 
-def test_world2_bucketed_allreduce_matches_shard_average():
+@pytest.mark.parametrize("mode", ["none", "zero", "accum"])
+def test_world2_bucketed_allreduce_matches_shard_average(mode):
+    """mode: p.grad None before each backward (the overlapped per-layer buckets), zeroed but kept
+    (zero_grad(set_to_none=False)) and accumulated over two backwards (expected: twice the
+    average) -- the last two take the fresh-gradient path, one collective after the backward."""
     import multiprocessing as mp
     ctx = mp.get_context("forkserver")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for pr in procs:
         pr.start()
     got = dict(q.get(timeout=240) for _ in range(2))
@@ -124,7 +132,7 @@ def test_world2_bucketed_allreduce_matches_shard_average():
     # balanced shards: every graph in exactly one, loads within one graph's cost
     assert sorted(shards[0] + shards[1]) == list(range(NG))
     (g0, s0), (g1, s1) = _oracle_shard(graphs, shards[0]), _oracle_shard(graphs, shards[1])
-    ref = {k: (g0[k] + g1[k]) / 2 for k in g0}
+    ref = {k: (g0[k] + g1[k]) / 2 * (2 if mode == "accum" else 1) for k in g0}
     gmax = max(v.abs().max().item() for v in ref.values())
     for r in (0, 1):
         res = got[r]

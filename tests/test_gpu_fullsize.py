@@ -154,3 +154,27 @@ def test_gnn_simple_odd_widths_vs_oracle(d):
     model = GNN_simple(0, d, 5, 5, 1, 1).cuda()
     fu.det_init(model, 530 + d)
     _check(model, b, 5, 0, kind="simple")
+
+
+def test_gnn_lg_d256_readout_row_beyond_64kb_lds():
+    """2d = 512 (d = 256, the widest valid_config width) with W.requires_grad: the readout-row dense
+    dW kernel needs ~66 KB of LDS at QM9 Nmax = 29 (allowed per kernel up to the CU's 160 KB)."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_lg
+    b = _batch(dg.qm9_shape_dataset(16, seed=256))
+    model = GNN_lg(0, 256, 3, 5, 1, 1, 2).cuda()
+    fu.det_init(model, 256, scale=0.05)
+    _check(model, b, 3, 2, dx_relax=True)
+
+
+def test_gnn_simple_large_nmax_readout_fallback():
+    """Nmax = 400 (SBM-400) at 2d = 128: the readout-row kernels' LDS (rows of the graph) exceeds
+    160 KB, so the executor takes the materialised [rows][K] readout gradient instead -- still every
+    gradient incl. W.grad against the oracle."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_simple
+    b = _batch(dg.sbm_dataset(3, n=400, seed=400))
+    assert b[0].shape[2] == 400
+    model = GNN_simple(0, 64, 3, 5, 1, 1).cuda()
+    fu.det_init(model, 400, scale=0.05)
+    _check(model, b, 3, 0, kind="simple")

@@ -15,6 +15,7 @@ is below the noise floor (1e-4 max|g|) only |d| <= 2 lr holds.
 """
 
 import copy
+import os
 
 import pytest
 import torch
@@ -200,6 +201,30 @@ def test_train_step_classification_matches_cross_entropy_adamax():
                 step.exp_inf[k].copy_(st["exp_inf"])
     bad = _batch(dg.qm9_shape_dataset(4, seed=9))
     bad[2] = torch.tensor([[0.0], [5.0], [1.0], [2.0]]).cuda()
-    step(bad)
+    # HGNN_STRICT=1 (conftest): the step raises at once
     with pytest.raises(RuntimeError, match="class target"):
-        step.check_targets()
+        step(bad)
+    # asynchronous check: the rejected row's dout is zero (finite parameters), the next check raises
+    os.environ["HGNN_STRICT"] = "0"
+    try:
+        step(bad)
+        torch.cuda.synchronize()
+        assert all(torch.isfinite(p).all() for p in model.parameters())
+        with pytest.raises(RuntimeError, match="class target"):
+            step.check_targets()
+        step.check_targets()  # the error word was consumed
+    finally:
+        os.environ["HGNN_STRICT"] = "1"
+
+
+def test_train_step_defaults_to_regression():
+    """TrainStep(model) with no t_mean is the MSE step; classification over one class is refused."""
+    from hgnn_amd.train import TrainStep
+    from models.gnns.model_mnb import GNN_lg
+    model = GNN_lg(0, 8, 3, 5, 1, 1, 2).cuda()
+    assert not TrainStep(model).classification
+    assert TrainStep(model, t_mean=0.0).classification
+    import hgnn_amd.datagen as dg
+    b = _batch(dg.qm9_shape_dataset(4, seed=19))
+    with pytest.raises(RuntimeError, match="dim_output >= 2"):
+        TrainStep(model, t_mean=0.0)(b)
