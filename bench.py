@@ -53,8 +53,8 @@ def parse():
     ap.add_argument("--roofline", type=int, default=1)
     ap.add_argument("--fwd-line", type=int, default=1, help="also time the forward alone (cfg2f)")
     ap.add_argument("--graph", type=int, default=0,
-                    help="capture the step (forward + backward) in a HIP graph and replay it; measured on the box: "
-                         "293.6 K vs 293.7 K graphs/s eager -- the step is GPU-bound, so off by default")
+                    help="capture the step (forward + backward) in a HIP graph and replay it (off by default: "
+                         "the eager step is GPU-bound, DESIGN.md §8)")
     return ap.parse_args()
 
 
@@ -185,8 +185,12 @@ def main():
         out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
         loss = crit(out, T)
         loss.backward()
-        last_out[0] = out
-        return loss
+        # values only: keeping `out` itself would keep this step's autograd nodes alive, among them the
+        # parameters' AccumulateGrad nodes with the stream they were created on -- a HIP-graph capture
+        # on another stream then meets a cross-stream sync with that stream and capture_end fails
+        # (tools/graph_diag.py)
+        last_out[0] = out.detach()
+        return loss.detach()
 
     def step():
         loss = compute()
@@ -274,10 +278,29 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    rank_ms = None
+    comm = None
     if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        # every rank's own time (a slow rank shows here), then the max over ranks for `value`
+        e = torch.zeros(world, device=dev, dtype=torch.float64)
+        e[rank] = elapsed
+        dist.all_reduce(e)
+        rank_ms = [round(float(v) * 1e3 / args.steps, 4) for v in e.cpu()]
+        elapsed = float(e.max().item())
+        if isinstance(allreduce, LayerBucketAllReduce):
+            # the per-step gradient all-reduce (HIP events on the communication stream) over a
+            # separate region of the same steps, so `value` carries no event records
+            allreduce.timing = True
+            for _ in range(args.steps):
+                step()
+            allreduce.timing = False
+            comm = allreduce.timing_summary()
+            if comm is not None:
+                c = torch.tensor([comm["allreduce_span_ms"], comm["allreduce_exposed_ms"]], device=dev,
+                                 dtype=torch.float64)
+                dist.all_reduce(c, op=dist.ReduceOp.MAX)
+                comm["allreduce_span_ms_max_rank"] = round(float(c[0]), 4)
+                comm["allreduce_exposed_ms_max_rank"] = round(float(c[1]), 4)
 
     if timer is not None:
         # The dominant kernel class is timed with HIP events around each of its launches over a
@@ -379,6 +402,8 @@ def main():
             "parallelism": f"dp{world}",
             "collective": ("rccl" if backend == "nccl" else backend) if world > 1 else None,
         },
+        "rank_ms_per_step": rank_ms,
+        "comm": comm,
         "roofline": roof,
         "roofline_hbm": roof_hbm,
         "roofline_fused": roof_fused,
@@ -393,13 +418,35 @@ def main():
                    "grads": {k: p.grad.detach().cpu() for k, p in model.named_parameters()},
                    "dX": X.grad.detach().cpu(), "dW": W.grad.detach().cpu()}
         res["cpu_baseline"], res["parity"] = cpu_baseline(args, batch_cpu, model, gpu_res)
+    # every rank's last step must have produced a finite loss; any rank failing fails the run
+    ok = 1 if bool(torch.isfinite(last_out[0].detach()).all()) else 0
+    if world > 1:
+        f = torch.tensor([ok], device=dev, dtype=torch.int32)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        ok = int(f.item())
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not ok:
+        sys.exit("bench: a rank produced non-finite outputs")
     if res.get("parity") is not None and not res["parity"]["pass"]:
         sys.exit("bench: GPU step breaches the SURVEY.md §8 c parity policy (see the 'parity' object)")
 
 
+def _main_checked():
+    """A rank that raises exits non-zero (torch.distributed.run then stops the others and fails)."""
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001
+        import traceback
+        traceback.print_exc()
+        sys.stderr.write(f"bench: rank {os.environ.get('RANK', '0')} failed: {e!r}\n")
+        sys.stderr.flush()
+        os._exit(1)
+
+
 if __name__ == "__main__":
-    main()
+    _main_checked()

@@ -19,6 +19,40 @@ namespace hgnn {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// ---- Diagnostic build only (make EXTRA=-DHGNN_CLOCK_DIAG into its own BUILD / OUT, tools/clock_diag.py):
+// wave 0 of every block stamps the shader clock (s_memtime, shader cycles) and the constant 100 MHz
+// clock (s_memrealtime) around the GEMM main loop, so clock = d(memtime) / d(memrealtime) x 100 MHz
+// (MI355X_MICROARCH.md, DVFS give-back item 6).  In the normal build no stamp exists.
+#ifdef HGNN_CLOCK_DIAG
+constexpr unsigned CLOCK_SLOTS = 1u << 16;
+struct ClockStamp {
+    unsigned long long dt, dr;
+    unsigned kid, pad;
+};
+__device__ ClockStamp g_clock[CLOCK_SLOTS];
+__device__ unsigned g_clock_n;
+#define CLK_BEGIN()                                  \
+    unsigned long long _clk_t0 = 0, _clk_r0 = 0;     \
+    if (threadIdx.x == 0) {                          \
+        _clk_t0 = __builtin_amdgcn_s_memtime();      \
+        _clk_r0 = __builtin_amdgcn_s_memrealtime();  \
+    }
+#define CLK_END(KID_)                                                       \
+    if (threadIdx.x == 0) {                                                 \
+        const unsigned long long _t1 = __builtin_amdgcn_s_memtime();        \
+        const unsigned long long _r1 = __builtin_amdgcn_s_memrealtime();    \
+        const unsigned _i = atomicAdd(&g_clock_n, 1u);                      \
+        if (_i < CLOCK_SLOTS) {                                             \
+            g_clock[_i].dt = _t1 - _clk_t0;                                 \
+            g_clock[_i].dr = _r1 - _clk_r0;                                 \
+            g_clock[_i].kid = (KID_);                                       \
+        }                                                                   \
+    }
+#else
+#define CLK_BEGIN()
+#define CLK_END(KID_)
+#endif
+
 namespace {
 
 enum { E3_FWD = 0, E3_STORE = 1, E3_DA_BN = 2 };
@@ -222,6 +256,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
 
     const int nt = ceil_div(K, BK);
     const int h = lane >> 5, l31 = lane & 31;
+    CLK_BEGIN()
     load(0);
     store(0, 0);
     __syncthreads();
@@ -263,6 +298,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
         }
         __syncthreads();
     }
+    CLK_END(EPI == E3_FWD ? 0u : 1u)
 
     // C/D layout of the 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
     if constexpr (EPI == E3_FWD) {
@@ -441,6 +477,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     const int nt = ceil_div(kend - kbeg, BK);
     const int h = lane >> 5, l31 = lane & 31;
+    CLK_BEGIN()
     load(kbeg);
     store(0);
     __syncthreads();
@@ -475,6 +512,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
         }
         __syncthreads();
     }
+    CLK_END(2u)
     float* out = slabs + (long long)bz * M * N;
 #pragma unroll
     for (int i = 0; i < AM; ++i)
@@ -594,6 +632,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm5(const float* __restric
             for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
     const int nt = (K + BK - 1) / BK;
     const int g = lane >> 4, l15 = lane & 15;
+    CLK_BEGIN()
     issue(0, 0);
     stage_barrier<0>();
     for (int t = 0; t < nt; ++t) {
@@ -635,6 +674,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm5(const float* __restric
             for (int j = 0; j < AN; ++j) acc[i][j] += tacc[i][j];
         stage_barrier<0>();  // tile t + 1 landed; every wave is done with tile t's buffer
     }
+    CLK_END(FWD ? 3u : 4u)
     // C layout of the 16x16 MFMA: col = lane & 15, row = 4 (lane >> 4) + r
     if constexpr (FWD) {
         static_assert(BM == 64 && WGM == 2 && AN == 1, "BN partials per 64-row tile, one column per lane");
@@ -886,3 +926,20 @@ int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, in
 }
 
 }  // namespace hgnn
+
+#ifdef HGNN_CLOCK_DIAG
+// Diagnostic build: copy out (and with reset != 0 clear) the clock stamps; returns the count.
+extern "C" int hgnn_diag_clock_read(void* out, int max_n, int reset) {
+    unsigned n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(hgnn::g_clock_n), sizeof(n)) != hipSuccess) return -1;
+    if (n > hgnn::CLOCK_SLOTS) n = hgnn::CLOCK_SLOTS;
+    const unsigned k = n < (unsigned)max_n ? n : (unsigned)max_n;
+    if (k && hipMemcpyFromSymbol(out, HIP_SYMBOL(hgnn::g_clock), k * sizeof(hgnn::ClockStamp)) != hipSuccess)
+        return -1;
+    if (reset) {
+        const unsigned z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hgnn::g_clock_n), &z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return (int)k;
+}
+#endif

@@ -174,6 +174,11 @@ class LayerBucketAllReduce:
         # set by the executor's backward (net._grad_targets): True when the gradients went to fresh
         # tensors (some p.grad present), i.e. no per-layer events were recorded this step
         self.fresh = False
+        # optional timing (bench.py, N > 1): per call, HIP events on the main stream when the call is
+        # made (backward enqueued), on the communication stream when the first bucket's collective
+        # starts (the last layer's gradients final) and when the last one ends
+        self.timing = False
+        self.marks = []
         _ATTACHED[model] = self
 
     def grad_targets(self):
@@ -209,16 +214,41 @@ class LayerBucketAllReduce:
             else:
                 dist.all_reduce(self.flat, group=self.group)
         else:
+            mk = None
+            if self.timing:
+                mk = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                mk[0].record(cur)
             for l in reversed(range(len(self.buckets))):
                 self.comm.wait_event(self.events[2 * l])
                 self.comm.wait_event(self.events[2 * l + 1])
+                if mk is not None and l == len(self.buckets) - 1:
+                    mk[1].record(self.comm)
                 off, n = self.buckets[l]
                 with torch.cuda.stream(self.comm):
                     dist.all_reduce(self.flat[off:off + n], group=self.group)
+            if mk is not None:
+                mk[2].record(self.comm)
             cur.wait_stream(self.comm)
+            if mk is not None:
+                mk[3].record(cur)
+                self.marks.append(mk)
         self.flat.div_(world)
         if self.sync_running:
             average_running_stats(self.model, self.group)
+
+    def timing_summary(self):
+        """Mean over the timed calls (ms): 'span' from the first bucket's collective start to the
+        last one's end on the communication stream, 'exposed' from the backward's end on the main
+        stream to the main stream's join (the all-reduce time not hidden behind the backward)."""
+        if not self.marks:
+            return None
+        torch.cuda.synchronize(self.device)
+        span = sum(m[1].elapsed_time(m[2]) for m in self.marks) / len(self.marks)
+        exposed = sum(max(0.0, m[0].elapsed_time(m[3])) for m in self.marks) / len(self.marks)
+        n = len(self.marks)
+        self.marks = []
+        return {"allreduce_span_ms": round(span, 4), "allreduce_exposed_ms": round(exposed, 4), "calls": n,
+                "buckets": len(self.buckets), "bytes": int(self.flat.numel() * 4)}
 
     def detach(self):
         if _ATTACHED.get(self.model) is self:

@@ -15,12 +15,12 @@ import fixture_util as fu
 pytestmark = pytest.mark.gpu
 
 
-def _capture(step, keep=None):
-    """keep: the dict the step stores its output in; emptied before the capture so that no eagerly
-    allocated autograd graph (executor workspace included) is freed while capturing -- that was
-    seen to crash the graph instantiation (capture_end) on the box."""
-    if keep is not None:
-        keep.clear()
+def _capture(step):
+    """Warm-up on a side stream, then capture.  The steps keep their outputs as values only
+    (out.detach()): an output kept with its grad_fn keeps the eager step's autograd nodes alive,
+    among them the parameters' AccumulateGrad nodes with the stream they were created on, and the
+    capture then meets a cross-stream sync with that (default) stream -- capture_end crashed on
+    the box that way (tools/graph_diag.py with DIAG_KEEP=1)."""
     torch.cuda.synchronize()
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
@@ -28,9 +28,6 @@ def _capture(step, keep=None):
         for _ in range(2):
             step()
     torch.cuda.current_stream().wait_stream(side)
-    torch.cuda.synchronize()
-    if keep is not None:
-        keep.clear()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
@@ -65,14 +62,14 @@ def test_graph_replay_equals_eager_step(kind):
         X.grad = None
         out = model([X, W], Nb, mask) if kind == "simple" else model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
         torch.nn.MSELoss()(out, T).backward()
-        out_buf["out"] = out
+        out_buf["out"] = out.detach()
 
     step()
     torch.cuda.synchronize()
     ref_out = out_buf["out"].detach().clone()
     ref = {k: p.grad.clone() for k, p in model.named_parameters()}
     ref_dx = X.grad.clone()
-    g = _capture(step, out_buf)
+    g = _capture(step)
     for _ in range(3):
         g.replay()
     torch.cuda.synchronize()
@@ -107,7 +104,7 @@ def test_ccn1_graph_replay_with_plan_equals_eager():
         X.grad = None
         out = net.forward_batch(X, A, nb, plan)
         ((out - T) ** 2).sum().backward()
-        buf["out"] = out
+        buf["out"] = out.detach()
 
     step()
     torch.cuda.synchronize()
@@ -118,7 +115,7 @@ def test_ccn1_graph_replay_with_plan_equals_eager():
     with torch.no_grad():
         assert torch.equal(net.forward_batch(X, A, nb), ref_out)
     torch.cuda.synchronize()
-    g = _capture(step, buf)
+    g = _capture(step)
     for _ in range(3):
         g.replay()
     torch.cuda.synchronize()

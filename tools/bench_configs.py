@@ -13,6 +13,8 @@ forward" roofline):
   cfg2csr the config-2 step on a CsrBatch from the native batcher (no dense W -> no dense dW)
   cfg2train / cfg2train_csr  the whole train_with_mnb step on the device (TrainStep: + MSE + Adamax)
   cfg3   CCN_1D(5, 1, 2, 2), 256 QM9-shape graphs (A + I), per-graph MSE summed
+  cfg3_pergraph  the same 256 graphs one at a time as scripts/train_ccn.py runs them (forward,
+         MSE, backward, Adamax step per graph)
   cfg4   GNN_lg d=128 order 2 L=5, 512 QM9-shape graphs (one GPU's share of 4096)
   cfg5   CCN_2D(5, 1, 2, 2), 64 SBM N=200 graphs (A + I)
 
@@ -213,6 +215,31 @@ def run_ccn(name, order, graphs, desc, steps, warmup, graph=False):
                 roofline=ccn_roofline(order, net, sd, sd2, sd3, sec))
 
 
+def run_ccn_pergraph(name, order, graphs, desc, steps, warmup):
+    """The reference driver's CCN step as it is written (scripts/train_ccn.py:31-73): per graph,
+    A + I, net(X, A) (the drop-in per-graph forward), MSE against t[task], backward and an
+    Adamax step (scripts/main_ccn_qm9.py:178) -- one optimizer step per graph.  A "step" here is a
+    pass over all the graphs; inputs already resident on the device."""
+    from models.compnets.model_ccn import CCN_1D, CCN_2D
+    torch.manual_seed(0)
+    net = (CCN_1D if order == 1 else CCN_2D)(5, 1, 2, 2).cuda()
+    opt = torch.optim.Adamax(net.parameters(), lr=1e-3)
+    crit = torch.nn.MSELoss()
+    data = [(x.cuda(), (a + torch.eye(a.shape[0])).cuda(), t[0].view(1).cuda()) for x, a, t in graphs]
+
+    def epoch():
+        for x, a, t in data:
+            opt.zero_grad()
+            loss = crit(net(x, a), t)
+            loss.backward()
+            opt.step()
+
+    sec = timeit(epoch, steps, warmup)
+    return dict(config=name, workload=desc, graphs_per_step=len(graphs), ms_per_step=round(sec * 1e3, 4),
+                ms_per_graph=round(sec * 1e3 / len(graphs), 4), value=round(len(graphs) / sec, 2),
+                unit="graphs/s", dtype="fp32")
+
+
 def ccn_roofline(order, net, sd, sd2, sd3, sec, bw=8.0e12, peak=157.3e12):
     """SURVEY.md §8 d CCN formulas over the step's batch (Σd, Σd², Σd³ with the self loop):
     per layer, CCN-1D bytes 4(Σd·C_in + Σd·h + Σd²), FLOPs 2Σd²·C + 4Σd·C·h; CCN-2D bytes
@@ -266,6 +293,10 @@ def main():
                                 "CCN_1D(5,1,2,2) fwd+bwd, 256 QM9-shape graphs", a.steps, a.warmup),
         "cfg3g": lambda: run_ccn("cfg3", 1, dg.qm9_shape_dataset(256, seed=0),
                                  "CCN_1D(5,1,2,2) fwd+bwd, 256 QM9-shape graphs", a.steps, a.warmup, graph=True),
+        "cfg3_pergraph": lambda: run_ccn_pergraph(
+            "cfg3_pergraph", 1, dg.qm9_shape_dataset(256, seed=0),
+            "CCN_1D(5,1,2,2) per graph as scripts/train_ccn.py: net(X, A+I), MSE, backward, Adamax step; "
+            "256 QM9-shape graphs", max(2, a.steps // 5), 1),
         "cfg4": lambda: run_lg("cfg4", "GNN_lg d=128 order 2 L=5 fwd+bwd, 512 QM9-shape (1 GPU of 4096)", 128, 2,
                                512, a.steps, a.warmup),
         "cfg5": lambda: run_ccn("cfg5", 2, dg.sbm_dataset(64, n=200, seed=0),

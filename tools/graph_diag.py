@@ -36,7 +36,9 @@ def step():
     out = model([X, W], Nb, mask) if kind == "simple" else model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
     torch.nn.MSELoss()(out, T).backward()
     if os.environ.get("DIAG_KEEP") == "1":
-        buf["out"] = out
+        # DIAG_DETACH=1: keep the values only -- the output's grad_fn keeps the eager step's autograd
+        # nodes (the parameters' AccumulateGrad nodes, with the stream they were created on) alive
+        buf["out"] = out.detach() if os.environ.get("DIAG_DETACH") == "1" else out
 
 
 buf = {}
