@@ -48,8 +48,10 @@ def parse():
     ap.add_argument("--settle-s", type=float, default=1.0,
                     help="untimed steps for this many seconds before the warmup steps (clock ramp)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-bs", type=int, default=512)
-    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-bs", type=int, default=128,
+                    help="graphs per step of the CPU baseline's timed protocol (bounded sample)")
+    ap.add_argument("--cpu-warmup", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--roofline", type=int, default=1)
     ap.add_argument("--fwd-line", type=int, default=1, help="also time the forward alone (cfg2f)")
     ap.add_argument("--graph", type=int, default=0,
@@ -85,11 +87,14 @@ def _cpu_model():
 
 
 def cpu_baseline(args, batch_cpu, model, gpu_res):
-    """Oracle (CPU restatement of the reference, oracle/ref_mnb.py) on the same batch and weights:
-    one warm-up fwd+bwd on a small batch, then one timed step of the full batch with forward and
-    backward timed apart.  Its outputs double as the parity check of the GPU step
-    (SURVEY.md §8 c policy, oracle/parity.py): fp32 oracle (the reference's op order) for outputs,
-    loss and every gradient, plus an fp64 forward (batched leg) as the second output leg."""
+    """Oracle (CPU restatement of the reference, oracle/ref_mnb.py) with the same weights, timed to
+    BASELINE.md §3's protocol on a bounded sample: --cpu-warmup (3) warm-up steps, then the median
+    of --cpu-steps (5) fwd+bwd steps of --cpu-bs (128) graphs of the same generator and seed, forward
+    and backward timed apart.  Then one fwd+bwd step of the full bench batch (also timed, reported
+    beside it: the reference's per-slice CopySlices backward grows faster than the batch), whose
+    outputs are the parity check of the GPU step (SURVEY.md §8 c policy, oracle/parity.py): fp32
+    oracle (the reference's op order) for outputs, loss and every gradient, plus an fp64 forward
+    (batched leg) as the second output leg."""
     from oracle import parity as PP
     from oracle import ref_mnb as R
     b = [t.clone() for t in batch_cpu]
@@ -115,15 +120,30 @@ def cpu_baseline(args, batch_cpu, model, gpu_res):
         g = {k: v.grad for k, v in p.items()} if grads else None
         return out.detach(), loss.item(), g, (Xr.grad, Wr.grad), t1 - t0, t2 - t1
 
-    run(make_batch(32, 4243))  # warm-up: allocator, thread pool, conv kernels
+    import statistics
+    small = make_batch(args.cpu_bs, 1000)
+    for _ in range(args.cpu_warmup):
+        run(small)
+    tf, tb = [], []
+    for _ in range(max(1, args.cpu_steps)):
+        r = run(small)
+        tf.append(r[4])
+        tb.append(r[5])
+    tt = [f + b_ for f, b_ in zip(tf, tb)]
+    med = statistics.median(tt)
     out32, loss32, g32, (dx32, dw32), t_f, t_b = run(b)
     out64 = run(b, torch.float64, fast=True, grads=False)[0]
     n = X.shape[0]
-    res = {"value": round(n / (t_f + t_b), 3), "unit": "graphs/s", "cores": threads, "kind": "port",
-           "cpu_model": _cpu_model(), "forward_s": round(t_f, 3), "backward_s": round(t_b, 3),
-           "sample": f"1 warm-up step on 32 graphs, then 1 timed fwd+bwd step of {n} QM9-shape graphs, "
-                     f"d={args.d}, L={args.layers}, order {args.order}, on oracle/ref_mnb.py (the reference's "
-                     f"dense per-graph loops; torch CPU, {threads} threads); {t_f + t_b:.1f} s"}
+    res = {"value": round(args.cpu_bs / med, 3), "unit": "graphs/s", "cores": threads, "kind": "port",
+           "cpu_model": _cpu_model(), "forward_s_median": round(statistics.median(tf), 4),
+           "backward_s_median": round(statistics.median(tb), 4), "step_s_all": [round(x, 4) for x in tt],
+           "full_batch_step": {"graphs": n, "value": round(n / (t_f + t_b), 3), "forward_s": round(t_f, 3),
+                               "backward_s": round(t_b, 3)},
+           "sample": f"BASELINE.md §3 protocol on a bounded sample: {args.cpu_warmup} warm-up steps, then the "
+                     f"median of {len(tt)} fwd+bwd steps of {args.cpu_bs} QM9-shape graphs (same generator and "
+                     f"seed), d={args.d}, L={args.layers}, order {args.order}, on oracle/ref_mnb.py (the reference's "
+                     f"dense per-graph loops; torch CPU, {threads} threads); full_batch_step: one step of the "
+                     f"{n}-graph bench batch, {t_f + t_b:.1f} s"}
     outp = PP.outputs_two_leg(gpu_res["out"], out32, out64)
     gr = PP.grads_global(gpu_res["grads"], g32)
     gx = PP.grads_global({"dX": gpu_res["dX"], "dW": gpu_res["dW"]}, {"dX": dx32, "dW": dw32})

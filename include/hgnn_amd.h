@@ -10,13 +10,13 @@
  * Conventions
  *  - every pointer named d_* is device memory (HBM) owned by the caller;
  *  - fp32 tensors are dense, contiguous, in the reference's layouts:
- *      X  (bs, f, Nmax)        node features, channel-major (functions/batching.py:198)
- *      XL (bs, 1, Emax)        line-graph input (functions/batching.py:201,253)
+ *      X  (bs, f, Nmax)        node features, channel-major (functions/batching.py:116, 172-174)
+ *      XL (bs, 1, Emax)        line-graph input = diag(WL[:, :, 1]) (functions/batching.py:119, 171)
  *      W  (bs, Nmax, Nmax, J+2)  graph operators (functions/operators.py:19-29)
  *      WL (bs, Emax, Emax, J+2)  line-graph operators (functions/operators.py:39-81)
  *      Pm, Pd (bs, Nmax, Emax)   incidence operators (functions/operators.py:43-66)
- *      mask (bs, Nmax, Nmax), mask_lg (bs, Emax, Emax)  (functions/batching.py:195-196)
- *      N_batch, E_batch (bs,) int64  (functions/batching.py:181-185)
+ *      mask (bs, Nmax, Nmax), mask_lg (bs, Emax, Emax)  (functions/batching.py:113-114, 182-183)
+ *      N_batch, E_batch (bs,) int64  (functions/batching.py:99-103)
  *  - outputs are caller-allocated; scratch comes from a caller-allocated
  *    workspace whose size is queried first (no allocation inside any call, so
  *    every call can be captured into a hipGraph);
@@ -31,9 +31,11 @@
  * Size limits (a call outside them returns HGNN_ERR_UNSUPPORTED or HGNN_ERR_ARG before anything
  * is enqueued, or -- for data-dependent bounds -- sets a device error bit; the reference has no
  * such limits, the Python layer raises RuntimeError):
- *  - networks: J + 2 in [3, 5]; 2d <= 512; the GEMMs address each operand through a 32-bit
- *    buffer resource, so every per-call operand must stay under 2 GB -- about 12 K QM9-shape
- *    graphs per call at d = 64 (the 640-wide edge aggregate is the largest; split larger batches);
+ *  - networks: J + 2 in [3, 5]; any d with 2d <= 512 (odd 2d runs the same MFMA GEMMs over a
+ *    row stride padded to 4); the GEMMs address each operand through a 32-bit buffer resource,
+ *    so every per-call operand must stay under 2 GB -- about 12 K QM9-shape graphs per call at
+ *    d = 64 (the 640-wide edge aggregate is the largest; split larger batches); the dense
+ *    operator gradient (need_dw) keeps a graph's rows in LDS: Nmax <= ~1200 at J + 2 = 3;
  *  - CCN: receptive-field degree <= 1024 (CCN-1D) / 64 (CCN-2D), f_in and hidden <= 16
  *    (HGNN_DEVERR_CCN_DEGREE for the degree, an error status for the channel counts).
  */
