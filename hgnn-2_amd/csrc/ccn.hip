@@ -125,10 +125,16 @@ __global__ void __launch_bounds__(256) k_ccn_scan(const int* deg, const int* tot
 }
 
 // pos[off2[i] + a*d_i + x] = index of nbr_i[x] in nbr_{nbr_i[a]} (binary search), or -1
-__global__ void __launch_bounds__(256) k_ccn_pos(CcnPlanView v, const int* total_nodes, int* pos) {
+__global__ void __launch_bounds__(256) k_ccn_pos(CcnPlanView v, const int* total_nodes, int* pos, long long pos_cap,
+                                                 uint32_t* err) {
     const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     if (i >= *total_nodes) return;
+    // an asynchronous plan sized pos by a bound: a batch beyond it is refused, never overrun
+    if ((long long)v.off2[*total_nodes] > pos_cap) {
+        if (i == 0 && lane == 0) atomicOr(err, (uint32_t)ERR_SIZES);
+        return;
+    }
     const int n = v.deg[i];
     if (n > CCN1_MAXD) return;
     const int* ni = v.nbr + (long long)i * v.nmax;
@@ -1228,10 +1234,9 @@ size_t hgnn_ccn_plan_bytes(const hgnn_ccn_config* cfg, long long max_sum_d2) {
     return ccn_layout(cfg, 0, max_sum_d2).plan_bytes;
 }
 
-int hgnn_ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t* d_n_batch, void* plan_ws,
-                  long long max_sum_d2, long long* h_sums, void* stream) {
+static int ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t* d_n_batch, void* plan_ws,
+                    long long max_sum_d2, long long* h_sums, hipStream_t s, bool sync) {
     if (!ccn_ok(cfg) || !d_adj || !d_n_batch || !plan_ws || !h_sums) return HGNN_ERR_ARG;
-    hipStream_t s = (hipStream_t)stream;
     const CcnLayout L = ccn_layout(cfg, 0, max_sum_d2);
     BatchMeta m;
     m.node_off = P<int>(plan_ws, L.node_off);
@@ -1249,18 +1254,38 @@ int hgnn_ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t*
     hipLaunchKernelGGL(k_ccn_scan, dim3(1), dim3(256), 0, s, P<int>(plan_ws, L.deg), m.totals,
                        P<int>(plan_ws, L.off1), P<int>(plan_ws, L.off2), m.totals + 2);
     HGNN_LAUNCH_CHECK();
-    int hbuf[4] = {0, 0, 0, 0};
-    HGNN_HOST_CHECK(hipMemcpyAsync(hbuf, m.totals, 16, hipMemcpyDeviceToHost, s));
-    HGNN_HOST_CHECK(hipStreamSynchronize(s));
-    const long long nodes = hbuf[0];
-    h_sums[0] = hbuf[2];
-    h_sums[1] = hbuf[3];
-    h_sums[2] = nodes;
-    if (h_sums[1] > max_sum_d2) return HGNN_ERR_ARG;  // caller re-plans with a larger bound
+    long long nodes = (long long)cfg->bs * cfg->nmax;
+    if (sync) {
+        int hbuf[4] = {0, 0, 0, 0};
+        HGNN_HOST_CHECK(hipMemcpyAsync(hbuf, m.totals, 16, hipMemcpyDeviceToHost, s));
+        HGNN_HOST_CHECK(hipStreamSynchronize(s));
+        nodes = hbuf[0];
+        h_sums[0] = hbuf[2];
+        h_sums[1] = hbuf[3];
+        h_sums[2] = nodes;
+        if (h_sums[1] > max_sum_d2) return HGNN_ERR_ARG;  // caller re-plans with a larger bound
+    } else {
+        // bounds, no host sync: every graph's d_i <= n_b <= nmax; the kernels read the device totals
+        h_sums[0] = nodes * cfg->nmax;
+        h_sums[1] = max_sum_d2;
+        h_sums[2] = nodes;
+    }
     hipLaunchKernelGGL(k_ccn_pos, dim3((unsigned)((nodes + 3) / 4 > 0 ? (nodes + 3) / 4 : 1)), dim3(256), 0, s, v,
-                       m.totals, P<int>(plan_ws, L.pos));
+                       m.totals, P<int>(plan_ws, L.pos), max_sum_d2, m.err);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
+}
+
+int hgnn_ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t* d_n_batch, void* plan_ws,
+                  long long max_sum_d2, long long* h_sums, void* stream) {
+    return ccn_plan(cfg, d_adj, d_n_batch, plan_ws, max_sum_d2, h_sums, (hipStream_t)stream, true);
+}
+
+int hgnn_ccn_plan_async(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t* d_n_batch, void* plan_ws,
+                        long long max_sum_d2, long long* h_sums_bound, void* stream) {
+    // the bound must hold for any content, so no later kernel can meet an unplanned position map
+    if (!cfg || max_sum_d2 < (long long)cfg->bs * cfg->nmax * cfg->nmax * cfg->nmax) return HGNN_ERR_ARG;
+    return ccn_plan(cfg, d_adj, d_n_batch, plan_ws, max_sum_d2, h_sums_bound, (hipStream_t)stream, false);
 }
 
 uint32_t* hgnn_ccn_error_word(const hgnn_ccn_config* cfg, void* plan_ws, long long max_sum_d2) {

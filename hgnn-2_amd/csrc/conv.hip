@@ -159,10 +159,10 @@ int hgnn_conv1x1_backward(const float* d_x, const float* d_w, const float* d_dy,
                        d_w, cout, cin, wc, cinp, wt, coutp);
     HGNN_LAUNCH_CHECK();
     // dW = dYrows^T . Xrows (TN, row-chunk slabs) -> reduce; db = column sums of dY
-    const int kc = dw3_kchunk((int)rows, cout, cin);
-    int r = launch_gemm3_dw(yt, coutp, xt, cinp, cnt, (int)rows, cout, cin, kc, slabs, s);
+    const int nz = dw3_chunks((int)rows, cout, cin);
+    int r = launch_gemm3_dw(yt, coutp, xt, cinp, cnt, (int)rows, cout, cin, nz, slabs, s);
     if (r) return r;
-    r = launch_dw_reduce2(slabs, cnt, kc, cout, cout, cin, cout, d_dw, d_dw, nullptr, nullptr, nullptr, s);
+    r = launch_dw_reduce2(slabs, cnt, nz, cout, cout, cin, cout, d_dw, d_dw, nullptr, nullptr, nullptr, s);
     if (r) return r;
     hipLaunchKernelGGL(k_bias_grad, dim3(cout), dim3(256), 0, s, d_dy, bs, cout, n, d_db);
     HGNN_LAUNCH_CHECK();

@@ -13,6 +13,8 @@
 // edge fwd 79 -> 51 us, edge dA 64 -> 48 us.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace hgnn {
@@ -409,7 +411,7 @@ template <int BM, int BN, int BK, int WGM, int WGN>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __restrict__ A, int lda,
                                                              const float* __restrict__ B, int ldb,
                                                              float* __restrict__ slabs, int M, int N,
-                                                             const int* __restrict__ r_valid, int kchunk,
+                                                             const int* __restrict__ r_valid, int nz,
                                                              int xcd_remap) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 32, AN = TN / 32;
@@ -435,6 +437,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
     }
     const int m0 = bx * BM, n0 = by * BN;
     const int R = *r_valid;
+    const int kchunk = dw3_kc(R, nz);
     const int kbeg = bz * kchunk, kend = min(R, kbeg + kchunk);
     if (kbeg >= kend) return;  // the reduce only sums the chunks that hold rows
     float4 ra[AF4], rb[BF4];
@@ -764,18 +767,16 @@ static int dw3_target_blocks() {
     return t;
 }
 
-int dw3_kchunk(int r_cap, int o, int k) {
+int dw3_chunks(int r_cap, int o, int k) {
     const int tiles = ceil_div(o, 128) * ceil_div(k, 128);
     int chunks = dw3_target_blocks() / (tiles > 0 ? tiles : 1);
+    // never more chunks than 64-row pieces of the capacity; a multiple of 8 (XCD-aware order)
+    chunks = std::min(chunks, ceil_div(r_cap > 0 ? r_cap : 1, 64));
     if (chunks < 1) chunks = 1;
-    int kc = ceil_div(r_cap > 0 ? r_cap : 1, chunks);
-    kc = ceil_div(kc, 32) * 32;
-    return kc < 64 ? 64 : kc;
+    return ceil_div(chunks, 8) * 8;
 }
 
-size_t dw3_slab_floats(int r_cap, int o, int k) {
-    return (size_t)ceil_div(r_cap > 0 ? r_cap : 1, dw3_kchunk(r_cap, o, k)) * o * k;
-}
+size_t dw3_slab_floats(int r_cap, int o, int k) { return (size_t)dw3_chunks(r_cap, o, k) * o * k; }
 
 // slabs[z][o][k] = sum_{r in chunk z} dY[r, o] A[r, k]
 int launch_gemm3_da_bn(const BnBwdArgs& bn, const int* m_valid, int m_cap, int o, const float* wt, int ldw, int kout,
@@ -812,16 +813,15 @@ int launch_gemm3_da_bn(const BnBwdArgs& bn, const int* m_valid, int m_cap, int o
 }
 
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
-                    int kchunk, float* slabs, hipStream_t s) {
+                    int nz, float* slabs, hipStream_t s) {
     if (r_cap <= 0) return 0;
+    if (nz <= 0 || nz % 8 != 0) return HGNN_ERR_ARG;
     static const bool xcd = [] {
         const char* e = getenv("HGNN_DW_XCD");
         return !e || e[0] != '0';
     }();
-    const int z = ceil_div(r_cap, kchunk);
-    const int zg = xcd ? ceil_div(z, 8) * 8 : z;  // padded chunks exit at once (no rows)
-    hipLaunchKernelGGL((k_gemm3_tn<128, 128, 32, 4, 2>), dim3(ceil_div(o, 128), ceil_div(k, 128), zg), dim3(512), 0, s,
-                       dy, lddy, a, lda, slabs, o, k, r_valid, kchunk, xcd ? 1 : 0);
+    hipLaunchKernelGGL((k_gemm3_tn<128, 128, 32, 4, 2>), dim3(ceil_div(o, 128), ceil_div(k, 128), nz), dim3(512), 0, s,
+                       dy, lddy, a, lda, slabs, o, k, r_valid, nz, xcd ? 1 : 0);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

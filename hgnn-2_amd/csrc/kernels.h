@@ -205,14 +205,22 @@ int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int
                      int mfma16 = 0);
 int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, int o, const float* wt, int ldw,
                     int kout, float* da, int ldda, hipStream_t s);
-int dw3_kchunk(int r_cap, int o, int k);
+// dW split-K: the host fixes the number of row chunks nz (a multiple of 8, ~dw3_target_blocks() blocks with
+// the output tiles); the kernels derive the chunk length from the device row count, so every chunk
+// holds rows whatever the batch's fill of its capacity
+int dw3_chunks(int r_cap, int o, int k);
+__host__ __device__ inline int dw3_kc(int rows, int nz) {
+    int kc = (rows + nz - 1) / nz;
+    kc = (kc + 31) / 32 * 32;
+    return kc < 64 ? 64 : kc;
+}
 size_t dw3_slab_floats(int r_cap, int o, int k);
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
-                    int kchunk, float* slabs, hipStream_t s);
+                    int nz, float* slabs, hipStream_t s);
 // slabs [z][o][k] -> dW (rows [0, split) -> dw0, [split, o_real) -> dw1; rows >= o_real are the
 // zero padding of an odd 2d); bias grads from the BN-backward per-tile column sums of dY
 // (dbpart [tiles][o_real])
-int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int o_real, int k, int split,
+int launch_dw_reduce2(const float* slabs, const int* r_valid, int nz, int o, int o_real, int k, int split,
                       float* dw0, float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s);
 
 // ---------------------------------------------------------------- fused aggregation + GEMM (fused.hip)

@@ -899,7 +899,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     // kernels only slowed each other.)
     auto fork_dw = [&](const Half& h, int cap, const int* tot, float* dyb, float* dbp, bool ndw_side,
                        float* dab, bool da_side = false) -> int {
-        const int kc = dw3_kchunk(cap, P.c2, h.k);
+        const int nz = dw3_chunks(cap, P.c2, h.k);
         if (side) {
             HGNN_HOST_CHECK(hipEventRecord(side->fork[parity], s));
             HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, side->fork[parity], 0));
@@ -919,9 +919,9 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             if (ndw_side) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, dab, h.kp, false, 1));
             // dY rows have stride c2p; the dW GEMM's float4 loads along the 2d outputs read the zero
             // padding of an odd 2d and store only the 2d real rows of each slab
-            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(dyb, P.c2p, at<float>(ws, h.a), h.kp, tot, cap, P.c2, h.k, kc,
+            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(dyb, P.c2p, at<float>(ws, h.a), h.kp, tot, cap, P.c2, h.k, nz,
                                                at<float>(ws, P.slabs), s));
-            TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, kc, P.c2, P.c2, h.k, P.d,
+            TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, nz, P.c2, P.c2, h.k, P.d,
                                                    grads[h.pw_lin], grads[h.pw_relu], dbp, grads[h.pb_lin],
                                                    grads[h.pb_relu], s));
             if (side) r = hipEventRecord(side->join[parity], s) == hipSuccess ? 0 : HGNN_ERR_HIP;

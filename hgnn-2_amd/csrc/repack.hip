@@ -31,7 +31,7 @@ int launch_repack(const RepackTable& t, hipStream_t s) {
 // gradient of output channel o from the BN-backward tile sums (k_db_reduce's work, same order).
 template <int SG>
 __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ slabs, const int* r_valid,
-                                                    int kchunk, int M, int MR, int N, int split, float* dw0,
+                                                    int nz, int M, int MR, int N, int split, float* dw0,
                                                     float* dw1, const float* __restrict__ dbpart, float* db0,
                                                     float* db1) {
     constexpr int OUT = 256 / SG;
@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
     const int ol = threadIdx.x % OUT, g = threadIdx.x / OUT;
     const int idx = blockIdx.x * OUT + ol;
     const int rows = *r_valid;
-    const int zv = ceil_div(rows, kchunk);
+    const int zv = rows > 0 ? ceil_div(rows, dw3_kc(rows, nz)) : 0;  // the chunks k_gemm3_tn filled
     const long long st = (long long)M * N;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (idx < MR * N) {
@@ -81,18 +81,17 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
     }
 }
 
-int launch_dw_reduce2(const float* slabs, const int* r_valid, int kchunk, int o, int o_real, int k, int split,
+int launch_dw_reduce2(const float* slabs, const int* r_valid, int nz, int o, int o_real, int k, int split,
                       float* dw0, float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s) {
-    if (o_real <= 0 || o_real > o) return HGNN_ERR_ARG;
+    if (o_real <= 0 || o_real > o || nz <= 0) return HGNN_ERR_ARG;
     const int total = o_real * k;
-    // slab groups by the slab count (upper bound from the capacity is not known here: the host
-    // passes the chunk size; more groups when the chunks are short, i.e. many slabs per output)
+    // slab groups by the slab count: more groups when there are many slabs per output
     const int nb = dbpart ? o_real : 0;
-    if (kchunk <= 128) {
-        hipLaunchKernelGGL(k_dw_reduce2<16>, dim3(ceil_div(total, 16) + nb), dim3(256), 0, s, slabs, r_valid, kchunk,
+    if (nz > 32) {
+        hipLaunchKernelGGL(k_dw_reduce2<16>, dim3(ceil_div(total, 16) + nb), dim3(256), 0, s, slabs, r_valid, nz,
                            o, o_real, k, split, dw0, dw1, dbpart, db0, db1);
     } else {
-        hipLaunchKernelGGL(k_dw_reduce2<4>, dim3(ceil_div(total, 64) + nb), dim3(256), 0, s, slabs, r_valid, kchunk,
+        hipLaunchKernelGGL(k_dw_reduce2<4>, dim3(ceil_div(total, 64) + nb), dim3(256), 0, s, slabs, r_valid, nz,
                            o, o_real, k, split, dw0, dw1, dbpart, db0, db1);
     }
     HGNN_LAUNCH_CHECK();

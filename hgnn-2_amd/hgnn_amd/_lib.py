@@ -96,6 +96,8 @@ SIGNATURES = {
     "hgnn_ccn_plan_bytes": ([ctypes.POINTER(CcnConfig), ctypes.c_longlong], ctypes.c_size_t),
     "hgnn_ccn_plan": ([ctypes.POINTER(CcnConfig), _VP, _VP, _VP, ctypes.c_longlong,
                        ctypes.POINTER(ctypes.c_longlong), _VP], _I),
+    "hgnn_ccn_plan_async": ([ctypes.POINTER(CcnConfig), _VP, _VP, _VP, ctypes.c_longlong,
+                             ctypes.POINTER(ctypes.c_longlong), _VP], _I),
     "hgnn_ccn_error_word": ([ctypes.POINTER(CcnConfig), _VP, ctypes.c_longlong], _VP),
     "hgnn_ccn_workspace_bytes": ([ctypes.POINTER(CcnConfig), ctypes.POINTER(ctypes.c_longlong)], ctypes.c_size_t),
     "hgnn_ccn_forward": ([ctypes.POINTER(CcnConfig), ctypes.POINTER(ctypes.c_longlong), _VP, _VP, _VP,

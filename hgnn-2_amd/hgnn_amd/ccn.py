@@ -23,7 +23,7 @@ import ctypes
 import torch
 
 from . import _lib as L
-from .net import _require_cuda, _f32, _i64, _raise_bits
+from .net import _require_cuda, _f32, _i64, _raise_bits, check_errors, watch_word
 
 CCN_MAX_DEGREE = {1: 1024, 2: 64}  # csrc/ccn.hip CCN1_MAXD, CCN_MAXD (by order)
 CCN2_MAX_CHANNELS = 16  # csrc/ccn.hip C2_CMAX_WIDE: CCN-2D f_in and hidden
@@ -50,14 +50,32 @@ class CcnSpec:
         return shapes
 
 
+# Workspace bound (elements of the sum-d^2-sized arrays) below which the plan sizes everything from
+# the shapes alone (bs nmax^3 >= sum d_i^2 for any content) and needs no host sync: the per-graph
+# drop-in path (scripts/train_ccn.py:52, QM9 graphs: 29^3 = 24 K) and small batches.  CCN-2D keeps
+# ~13 sum-d^2 arrays per level, so its bound is lower.
+ASYNC_PLAN_BOUND = {1: 8 << 20, 2: 1 << 20}
+
+
 def _plan(cfg, adj, n_batch, stream):
     lib = L.lib()
     dev = adj.device
+    bs, nmax = adj.shape[0], adj.shape[1]
+    bound = bs * nmax ** 3
+    sums = (ctypes.c_longlong * 3)()
+    if bound <= ASYNC_PLAN_BOUND[cfg.order]:
+        max_d2 = max(bound, 1)
+        plan = torch.empty(lib.hgnn_ccn_plan_bytes(ctypes.byref(cfg), max_d2), dtype=torch.uint8, device=dev)
+        L.check(lib.hgnn_ccn_plan_async(ctypes.byref(cfg), L.ptr(adj), L.ptr(n_batch), L.ptr(plan), max_d2, sums,
+                                        stream), "hgnn_ccn_plan_async")
+        base = plan.data_ptr()
+        off = int(lib.hgnn_ccn_error_word(ctypes.byref(cfg), ctypes.c_void_p(base), max_d2)) - base
+        watch_word(plan[off:off + 4].view(torch.int32))  # checked without a sync (HGNN_STRICT=1: at once)
+        return plan, max_d2, sums
     # upper bound of sum_i d_i^2 from the padded adjacency (exact when padding is zero)
     deg = (adj > 0).sum(-1)
     max_d2 = max(int((deg * deg).sum().item()), 1)
     plan = torch.empty(lib.hgnn_ccn_plan_bytes(ctypes.byref(cfg), max_d2), dtype=torch.uint8, device=dev)
-    sums = (ctypes.c_longlong * 3)()
     L.check(lib.hgnn_ccn_plan(ctypes.byref(cfg), L.ptr(adj), L.ptr(n_batch), L.ptr(plan), max_d2, sums, stream),
             "hgnn_ccn_plan")
     base = plan.data_ptr()
@@ -120,7 +138,9 @@ class _CcnFn(torch.autograd.Function):
 
 def run_ccn(spec, params, X, adj, n_batch, plan=None):
     """Batched CCN forward: X (bs,nmax,f), adj (bs,nmax,nmax), n_batch (bs,) -> (bs, n_out).
-    plan: a CcnPlan of this adj / n_batch (else the plan is built here, with one host sync)."""
+    plan: a CcnPlan of this adj / n_batch (else the plan is built here: without a host sync for
+    small shapes, ASYNC_PLAN_BOUND; with one otherwise)."""
+    check_errors(block=False)
     _require_cuda([X, adj, n_batch, *params], "CCN")
     if X.dim() != 3 or adj.dim() != 3:
         raise RuntimeError(f"hgnn_amd: CCN expects X (bs,nmax,f) and adj (bs,nmax,nmax), got {tuple(X.shape)}, "

@@ -119,15 +119,20 @@ def _capturing():
 
 
 def _watch_error_word(cfg, ws):
+    base = ws.data_ptr()
+    addr = L.lib().hgnn_net_error_word(ctypes.byref(cfg), ctypes.c_void_p(base))
+    off = int(addr) - base
+    watch_word(ws[off:off + 4].view(torch.int32))
+
+
+def watch_word(err):
+    """Check a device error word (int32 view) without synchronising the stream: copied into a
+    pinned ring slot behind an event, read by a later check_errors() (HGNN_STRICT=1: at once)."""
     if _capturing():
         # inside a HIP graph capture (bench.py --graph): the batch was validated by the eager
         # warm-up steps; no host-visible check can be part of a replayed graph
         return
     global _ring
-    base = ws.data_ptr()
-    addr = L.lib().hgnn_net_error_word(ctypes.byref(cfg), ctypes.c_void_p(base))
-    off = int(addr) - base
-    err = ws[off:off + 4].view(torch.int32)
     if strict():
         v = int(err.item())
         if v:

@@ -301,6 +301,12 @@ typedef struct hgnn_ccn_config {
 size_t hgnn_ccn_plan_bytes(const hgnn_ccn_config* cfg, long long max_sum_d2);
 int hgnn_ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t* d_n_batch,
                   void* plan_ws, long long max_sum_d2, long long* h_sums, void* stream);
+/* Same without any host synchronisation (the per-graph drop-in path, scripts/train_ccn.py:52):
+ * h_sums_bound receives upper bounds {bs nmax^2, max_sum_d2, bs nmax} that size the workspace;
+ * the kernels read the exact totals on the device.  max_sum_d2 >= bs nmax^3 (a bound for any
+ * content; HGNN_ERR_ARG otherwise), so the sizes never depend on the data. */
+int hgnn_ccn_plan_async(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t* d_n_batch,
+                        void* plan_ws, long long max_sum_d2, long long* h_sums_bound, void* stream);
 uint32_t* hgnn_ccn_error_word(const hgnn_ccn_config* cfg, void* plan_ws, long long max_sum_d2);
 size_t hgnn_ccn_workspace_bytes(const hgnn_ccn_config* cfg, const long long* sums);
 int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const float* d_X,
