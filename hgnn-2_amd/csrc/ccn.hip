@@ -26,7 +26,13 @@
 namespace hgnn {
 namespace {
 
-constexpr int CCN_MAXD = 64;     // CCN-2D degree bound (one wave per receptive field row, 64-bit ballots)
+constexpr int CCN_MAXD = 64;     // CCN-2D fast-path degree bound (one wave per receptive-field row, 64-bit ballots)
+constexpr int CCN_BIGD = 256;    // CCN-2D degree bound: degrees 65..256 take the _big kernels (rows in 64-lane
+                                 // chunks, membership as 4 x 64-bit words, position maps read from L2)
+constexpr int CCN_BW = CCN_BIGD / 64;
+
+// bit x of a multi-word set (CCN-2D common neighbourhoods of the large-degree kernels)
+__device__ __forceinline__ bool mbit(const unsigned long long* m, int x) { return (m[x >> 6] >> (x & 63)) & 1ull; }
 constexpr int CCN1_MAXD = 1024;  // CCN-1D degree bound (rows walked in 64-lane chunks; per-wave LDS row sums)
 
 struct CcnPlanView {
@@ -555,19 +561,22 @@ struct C2Grad {
 // One sweep over the n^2 entries per output o for the parameter partials (the 9 distinct
 // contraction blocks x cin accumulate in registers, then one wave-sum + LDS combine each), and one
 // sweep for the input-side gradients (every channel of an entry from one read of dpre).
-template <int CM, int HM>
+// BIG: the instantiation for degrees 65..256 (the level-0 reduction walks 64-lane chunks and
+// multi-word common-neighbour sets, dSa read from L2 instead of an n x n LDS copy).
+template <int CM, int HM, bool BIG = false>
 __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int* total_nodes,
                                                        const float* __restrict__ dF, const float* __restrict__ F,
                                                        C2Save sv, int cin, const float* __restrict__ W, int h,
                                                        C2Grad gd, float* __restrict__ ppart,
                                                        float* __restrict__ g0) {
-    __shared__ float sdq1[CCN_MAXD * CM], sdq3[CCN_MAXD * CM], sdtot[CM], sdd3[CM];
+    constexpr int MAXN = BIG ? CCN_BIGD : CCN_MAXD;
+    __shared__ float sdq1[MAXN * CM], sdq3[MAXN * CM], sdtot[CM], sdd3[CM];
     __shared__ float red[4][10 * CM];
     __shared__ float sw[HM * 18 * CM];
     const int i = blockIdx.x;
     if (i >= *total_nodes) return;
     const int n = v.deg[i];
-    if (n > CCN_MAXD || cin > CM || h > HM) return;
+    if ((BIG ? (n <= CCN_MAXD || n > CCN_BIGD) : n > CCN_MAXD) || cin > CM || h > HM) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long o2 = v.off2[i], o1 = v.off1[i];
     const float nf = (float)n;
@@ -677,6 +686,45 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
     // every j gathering them:  G[a] = m_a sum_{b in C_a} dSc[a][b] + sum_{b,z in C_a} dSa[b][z]
     //   + sum_{b in C_a} dD1[a][b] + [a in C_a] (sum_{b in C_a} dD2[a][b] + dd3),  C_a = {x: pos_a(x) >= 0}
     // dSa of one channel is staged in LDS so the masked row sums read LDS, not scattered HBM rows
+    if constexpr (BIG) {
+        __shared__ unsigned long long vmb[CCN_BIGD][CCN_BW];
+        __shared__ int smc[CCN_BIGD];
+        const int nw = (n + 63) >> 6;
+        __syncthreads();
+        for (int a = wv; a < n; a += 4) {
+            int cnt = 0;
+            for (int w = 0; w < nw; ++w) {
+                const int x = w * 64 + lane;
+                const unsigned long long m = __ballot(x < n && v.pos[o2 + (long long)a * n + x] >= 0);
+                if (lane == 0) vmb[a][w] = m;
+                cnt += __popcll(m);
+            }
+            if (lane == 0) smc[a] = cnt;
+        }
+        __syncthreads();
+        for (int c = 0; c < cin; ++c)
+            for (int a = wv; a < n; a += 4) {
+                const bool va = mbit(vmb[a], a);
+                const float mf = (float)smc[a];
+                float t = 0.f;
+                for (int b = lane; b < n; b += 64) {
+                    if (!mbit(vmb[a], b)) continue;
+                    const long long rab = (o2 + (long long)a * n + b) * cin + c;
+                    t += mf * gd.dSc[rab] + gd.dD1[rab] + (va ? gd.dD2[rab] : 0.f);
+                    for (int w = 0; w < nw; ++w) {
+                        unsigned long long zs = vmb[a][w];
+                        while (zs) {
+                            const int z = w * 64 + __ffsll((long long)zs) - 1;
+                            zs &= zs - 1ull;
+                            t += gd.dSa[(o2 + (long long)b * n + z) * cin + c];
+                        }
+                    }
+                }
+                t = wave_sum(t);
+                if (lane == 0) g0[(o1 + a) * cin + c] = t + (va ? sdd3[c] : 0.f);
+            }
+        return;
+    }
     __shared__ unsigned long long vm[CCN_MAXD];
     __shared__ float sa_l[CCN_MAXD * CCN_MAXD];
     __syncthreads();
@@ -718,16 +766,16 @@ __global__ void __launch_bounds__(256) k_ccn2_dx0(CcnPlanView v, const int* tota
     const int lane = threadIdx.x & 63;
     if (j >= *total_nodes) return;
     const int n = v.deg[j];
-    if (n > CCN_MAXD) return;
+    if (n > CCN_BIGD) return;
     const long long o2 = v.off2[j];
     const int* nj = v.nbr + (long long)j * v.nmax;
     const int sj = v.selfpos[j];
     for (int c = 0; c < cin; ++c) {
         float t = 0.f;
-        if (lane < n) {
-            const int i = nj[lane];
-            const int aj = v.pos[o2 + (long long)lane * n + sj];  // position of j in N(i)
-            t = g0[((long long)v.off1[i] + aj) * cin + c];
+        for (int x = lane; x < n; x += 64) {  // one chunk for d <= 64
+            const int i = nj[x];
+            const int aj = v.pos[o2 + (long long)x * n + sj];  // position of j in N(i)
+            t += g0[((long long)v.off1[i] + aj) * cin + c];
         }
         t = wave_sum(t);
         if (lane == 0) {
@@ -841,6 +889,381 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_gather(CcnPlanView v, const in
             if (c >= cin) break;
             if (level0) part[c] += acc[c];
             else if (lane < n) dout[(o2 + (long long)u * n + lane) * cin + c] = acc[c] + rd[c];
+        }
+    }
+    if (level0) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            if (c >= cin) break;
+            const float t = wave_sum(part[c]);
+            if (lane == 0) red[wv][c] = t;
+        }
+        __syncthreads();
+        if (threadIdx.x < cin) {
+            const int c = threadIdx.x;
+            dout[(long long)j * cin + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + (float)(n * n) * rd[c];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ CCN-2D, degrees 65..256
+// The same passes as k_ccn2_fwd / k_ccn2_bwd_node / k_ccn2_bwd_gather for the nodes whose receptive
+// field exceeds one wave (SBM graphs of several hundred nodes: d ~ 70-210): the lane index walks its
+// range in 64-lane chunks, the common-neighbour sets C_a are CCN_BW 64-bit words per row (LDS), and
+// the position maps are read from global memory (n^2 ints per node, L2-resident) instead of LDS.
+// Launched only when a batch can hold such degrees (nmax > 64); nodes with d <= 64 exit at once
+// (they are the fast kernels'), so every node is computed by exactly one of the two.
+template <int CM, int HM>
+__global__ void __launch_bounds__(256) k_ccn2_fwd_big(CcnPlanView v, const int* total_nodes,
+                                                      const float* __restrict__ fin, int level0,
+                                                      const float* __restrict__ X, int cin,
+                                                      const float* __restrict__ W, const float* __restrict__ bias,
+                                                      int h, C2Save sv, float* __restrict__ fout) {
+    __shared__ unsigned long long vmask[CCN_BIGD][CCN_BW];  // bit x of row a: x in C_a
+    __shared__ int s_j[CCN_BIGD], s_dj[CCN_BIGD], s_oj[CCN_BIGD], s_mc[CCN_BIGD];
+    __shared__ float sred[2][4][CM];
+    const int i = blockIdx.x;
+    if (i >= *total_nodes) return;
+    const int n = v.deg[i];
+    if (n <= CCN_MAXD || n > CCN_BIGD || cin > CM || h > HM) return;
+    const int nw = (n + 63) >> 6;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int* ni = v.nbr + (long long)i * v.nmax;
+    const long long o2 = v.off2[i], o1 = v.off1[i];
+    const int* sp = v.pos + o2;  // sp[a n + x]
+    for (int t = threadIdx.x; t < n; t += 256) {
+        const int j = ni[t];
+        s_j[t] = j;
+        s_dj[t] = v.deg[j];
+        s_oj[t] = v.off2[j];
+    }
+    for (int a = wv; a < n; a += 4) {
+        int cnt = 0;
+        for (int w = 0; w < nw; ++w) {
+            const int x = w * 64 + lane;
+            const unsigned long long m = __ballot(x < n && sp[(long long)a * n + x] >= 0);
+            if (lane == 0) vmask[a][w] = m;
+            cnt += __popcll(m);
+        }
+        if (lane == 0) s_mc[a] = cnt;
+    }
+    __syncthreads();
+
+    // ---- pass A: wave per neighbour a, lane b (64-lane chunks)
+    float tq[CM], td3[CM];
+#pragma unroll
+    for (int c = 0; c < CM; ++c) tq[c] = td3[c] = 0.f;
+    for (int a = wv; a < n; a += 4) {
+        const int j = s_j[a], dj = s_dj[a];
+        const bool va = mbit(vmask[a], a);
+        float qa[CM];
+#pragma unroll
+        for (int c = 0; c < CM; ++c) qa[c] = 0.f;
+        for (int b0 = 0; b0 < n; b0 += 64) {
+            const int b = b0 + lane;
+            const int pb = b < n ? sp[(long long)a * n + b] : -1;
+            const bool vb = pb >= 0;
+            float sc[CM], d1[CM], d2[CM];
+#pragma unroll
+            for (int c = 0; c < CM; ++c) sc[c] = d1[c] = d2[c] = 0.f;
+            if (level0) {
+                const float mf = (float)s_mc[a];
+#pragma unroll
+                for (int c = 0; c < CM; ++c) {
+                    if (c >= cin) break;
+                    const float xj = X[(long long)j * cin + c];
+                    sc[c] = vb ? mf * xj : 0.f;
+                    d1[c] = vb ? xj : 0.f;
+                    d2[c] = (vb && va) ? xj : 0.f;
+                }
+            } else {
+                const float* row = fin + ((long long)s_oj[a] + (long long)(vb ? pb : 0) * dj) * cin;
+                for (int w = 0; w < nw; ++w) {
+                    unsigned long long zs = vmask[a][w];
+                    while (zs) {
+                        int zz[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            zz[u] = zs ? w * 64 + __ffsll((long long)zs) - 1 : -1;
+                            zs &= zs ? zs - 1ull : 0ull;
+                        }
+                        float t[4][CM];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int pz = zz[u] >= 0 ? sp[(long long)a * n + zz[u]] : 0;
+#pragma unroll
+                            for (int c = 0; c < CM; ++c) t[u][c] = c < cin ? row[(long long)pz * cin + c] : 0.f;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int z = zz[u];
+                            if (z < 0) break;
+                            if (vb) {
+#pragma unroll
+                                for (int c = 0; c < CM; ++c) {
+                                    if (c >= cin) break;
+                                    sc[c] += t[u][c];
+                                    if (z == b) d1[c] = t[u][c];
+                                    if (z == a) d2[c] = t[u][c];
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            if (b < n) {
+                const long long r = (o2 + (long long)a * n + b) * cin;
+#pragma unroll
+                for (int c = 0; c < CM; ++c) {
+                    if (c >= cin) break;
+                    sv.Sc[r + c] = sc[c];
+                    sv.D1[r + c] = d1[c];
+                    sv.D2[r + c] = d2[c];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < CM; ++c) {
+                if (c >= cin) break;
+                qa[c] += wave_sum(sc[c]);
+                if (b == a) td3[c] += d1[c];  // T[a][a][a]
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+            if (c >= cin) break;
+            if (lane == 0) sv.q1[(o1 + a) * cin + c] = qa[c];
+            tq[c] += qa[c];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+        if (c >= cin) break;
+        const float t3 = wave_sum(td3[c]);
+        if (lane == 0) {
+            sred[0][wv][c] = tq[c];
+            sred[1][wv][c] = t3;
+        }
+    }
+
+    // ---- pass B: wave per receptive-field row b, lane z (chunks); the a with b in C_a ascending
+    for (int b = wv; b < n; b += 4) {
+        float q3[CM];
+#pragma unroll
+        for (int c = 0; c < CM; ++c) q3[c] = 0.f;
+        for (int z0 = 0; z0 < n; z0 += 64) {
+            const int z = z0 + lane;
+            float sa[CM];
+#pragma unroll
+            for (int c = 0; c < CM; ++c) sa[c] = 0.f;
+            for (int a0 = 0; a0 < n; a0 += 64) {
+                const int al = a0 + lane < n ? a0 + lane : 0;
+                unsigned long long as = __ballot(a0 + lane < n && mbit(vmask[al], b));
+                while (as) {
+                    int aa[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        aa[u] = as ? a0 + __ffsll((long long)as) - 1 : -1;
+                        as &= as ? as - 1ull : 0ull;
+                    }
+                    float t[4][CM];
+                    bool vz[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int a = aa[u] >= 0 ? aa[u] : 0;
+                        vz[u] = aa[u] >= 0 && z < n && mbit(vmask[a], z);
+                        const float* q;
+                        if (level0) {
+                            q = X + (long long)s_j[a] * cin;
+                        } else {
+                            const int pb = max(sp[(long long)a * n + b], 0), pz = vz[u] ? sp[(long long)a * n + z] : 0;
+                            q = fin + ((long long)s_oj[a] + (long long)pb * s_dj[a] + pz) * cin;
+                        }
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) t[u][c] = c < cin ? q[c] : 0.f;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (aa[u] < 0) break;
+                        if (vz[u]) {
+#pragma unroll
+                            for (int c = 0; c < CM; ++c) {
+                                if (c >= cin) break;
+                                sa[c] += t[u][c];
+                            }
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < CM; ++c) {
+                if (c >= cin) break;
+                if (z < n) sv.Sa[(o2 + (long long)b * n + z) * cin + c] = sa[c];
+                q3[c] += wave_sum(sa[c]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+            if (c >= cin) break;
+            if (lane == 0) sv.q3[(o1 + b) * cin + c] = q3[c];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < cin) {
+        const int c = threadIdx.x;
+        float t = 0.f, t3 = 0.f;
+        for (int w = 0; w < 4; ++w) {
+            t += sred[0][w][c];
+            t3 += sred[1][w][c];
+        }
+        sv.tot[(long long)i * cin + c] = t;
+        sv.d3[(long long)i * cin + c] = t3;
+    }
+    __syncthreads();
+    // output stage: as k_ccn2_fwd
+    const float nf = (float)n;
+    const int K = 18 * cin;
+    __shared__ float sw[HM * 18 * CM];
+    for (int t = threadIdx.x; t < h * K; t += 256) sw[t] = W[t];
+    __syncthreads();
+    for (int e = threadIdx.x; e < n * n; e += 256) {
+        const int x = e / n, y = e % n;
+        float s[HM];
+#pragma unroll
+        for (int o = 0; o < HM; ++o) s[o] = o < h ? bias[o] : 0.f;
+        for (int c = 0; c < cin; ++c) {
+            const float sc = sv.Sc[(o2 + e) * cin + c];
+            const float sa = sv.Sa[(o2 + e) * cin + c];
+            float blk[18];
+            blk[0] = nf * sc;
+            blk[1] = sv.q1[(o1 + x) * cin + c];
+            blk[2] = nf * sa;
+            blk[3] = sv.q3[(o1 + x) * cin + c];
+            blk[4] = x == y ? sv.tot[(long long)i * cin + c] : 0.f;
+            blk[5] = sc;
+#pragma unroll
+            for (int q = 6; q < 15; ++q) blk[q] = nf * sc;
+            blk[15] = sv.D1[(o2 + e) * cin + c];
+            blk[16] = sv.D2[(o2 + (long long)y * n + x) * cin + c];
+            blk[17] = x == y ? sv.d3[(long long)i * cin + c] : 0.f;
+#pragma unroll
+            for (int o = 0; o < HM; ++o) {
+                if (o >= h) break;
+                const float* w = sw + o * K;
+#pragma unroll
+                for (int q = 0; q < 18; ++q) s[o] = fmaf(w[q * cin + c], blk[q], s[o]);
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < HM; ++o) {
+            if (o >= h) break;
+            fout[(o2 + e) * h + o] = s[o] < 0.f ? 0.f : s[o];
+        }
+    }
+}
+
+// k_ccn2_bwd_gather for degrees 65..256: lane w of row u in 64-lane chunks, the neighbours a with
+// u in C_a in 64-wide ballot chunks (ascending: the summation order of the fast kernel's walk).
+template <int C, int NB>
+__global__ void __launch_bounds__(256) k_ccn2_bwd_gather_big(CcnPlanView v, const int* total_nodes, C2Grad gd,
+                                                             int cin, const float* __restrict__ dsum, int dsum_ld,
+                                                             int dsum_off, int level0, float* __restrict__ dout) {
+    __shared__ unsigned long long vmask[CCN_BIGD][CCN_BW];
+    __shared__ float red[4][C];
+    __shared__ int s_i[CCN_BIGD], s_di[CCN_BIGD], s_oi[CCN_BIGD], s_aj[CCN_BIGD];
+    const int j = blockIdx.x;
+    if (j >= *total_nodes) return;
+    const int n = v.deg[j];
+    if (n <= CCN_MAXD || n > CCN_BIGD || cin > C) return;
+    const int nw = (n + 63) >> 6;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long o2 = v.off2[j];
+    const int* sp = v.pos + o2;
+    const int* nj = v.nbr + (long long)j * v.nmax;
+    const int sj = v.selfpos[j];
+    const int g = v.graph[j];
+    for (int t = threadIdx.x; t < n; t += 256) {
+        const int i = nj[t];
+        s_i[t] = i;
+        s_di[t] = v.deg[i];
+        s_oi[t] = v.off2[i];
+        s_aj[t] = sp[(long long)t * n + sj];  // position of j in N(i_a)
+    }
+    for (int a = wv; a < n; a += 4)
+        for (int w = 0; w < nw; ++w) {
+            const int x = w * 64 + lane;
+            const unsigned long long m = __ballot(x < n && sp[(long long)a * n + x] >= 0);
+            if (lane == 0) vmask[a][w] = m;
+        }
+    __syncthreads();
+    float rd[C], part[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        rd[c] = (dsum && c < cin) ? dsum[(long long)g * dsum_ld + dsum_off + c] : 0.f;
+        part[c] = 0.f;
+    }
+    for (int u = wv; u < n; u += 4) {
+        for (int w0 = 0; w0 < n; w0 += 64) {
+            const int wl = w0 + lane;
+            float acc[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] = 0.f;
+            for (int a0 = 0; a0 < n; a0 += 64) {
+                const int al = a0 + lane < n ? a0 + lane : 0;
+                unsigned long long as = __ballot(a0 + lane < n && mbit(vmask[al], u));
+                while (as) {
+                    int aa[NB];
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        aa[q] = as ? a0 + __ffsll((long long)as) - 1 : -1;
+                        as &= as ? as - 1ull : 0ull;
+                    }
+                    float tsc[NB][C], tsa[NB][C], td1[NB][C], td2[NB][C], td3[NB][C];
+                    int zb[NB], zz[NB], zaj[NB];
+                    bool vz[NB];
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        const int a = aa[q] >= 0 ? aa[q] : 0;
+                        vz[q] = aa[q] >= 0 && wl < n && mbit(vmask[a], wl);
+                        const int b = max(sp[(long long)a * n + u], 0), z = vz[q] ? sp[(long long)a * n + wl] : 0;
+                        const int aj = s_aj[a], di = s_di[a], i = s_i[a];
+                        const long long oi = s_oi[a];
+                        const long long rab = (oi + (long long)aj * di + b) * cin, rbz = (oi + (long long)b * di + z) * cin;
+                        zb[q] = b;
+                        zz[q] = z;
+                        zaj[q] = aj;
+#pragma unroll
+                        for (int c = 0; c < C; ++c) {
+                            const bool ok = c < cin;
+                            tsc[q][c] = ok ? gd.dSc[rab + c] : 0.f;
+                            tsa[q][c] = ok ? gd.dSa[rbz + c] : 0.f;
+                            td1[q][c] = ok ? gd.dD1[rab + c] : 0.f;
+                            td2[q][c] = ok ? gd.dD2[rab + c] : 0.f;
+                            td3[q][c] = ok ? gd.dd3[(long long)i * cin + c] : 0.f;
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        if (aa[q] < 0) break;
+                        if (!vz[q]) continue;
+                        const int b = zb[q], z = zz[q], aj = zaj[q];
+#pragma unroll
+                        for (int c = 0; c < C; ++c) {
+                            if (c >= cin) break;
+                            float t = tsc[q][c] + tsa[q][c];
+                            if (z == b) t += td1[q][c];
+                            if (z == aj) t += td2[q][c];
+                            if (aj == b && b == z) t += td3[q][c];
+                            acc[c] += t;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (c >= cin) break;
+                if (level0) part[c] += acc[c];
+                else if (wl < n) dout[(o2 + (long long)u * n + wl) * cin + c] = acc[c] + rd[c];
+            }
         }
     }
     if (level0) {
@@ -1249,7 +1672,7 @@ static int ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_
     CcnPlanView v = plan_view(cfg, L, plan_ws);
     hipLaunchKernelGGL(k_ccn_nbrs, dim3(cfg->bs), dim3(256), 0, s, d_adj, cfg->nmax, v.node_off,
                        P<int>(plan_ws, L.deg), P<int>(plan_ws, L.nbr), P<int>(plan_ws, L.selfpos),
-                       P<int>(plan_ws, L.graph), m.err, cfg->order == 1 ? CCN1_MAXD : CCN_MAXD);
+                       P<int>(plan_ws, L.graph), m.err, cfg->order == 1 ? CCN1_MAXD : CCN_BIGD);
     HGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_ccn_scan, dim3(1), dim3(256), 0, s, P<int>(plan_ws, L.deg), m.totals,
                        P<int>(plan_ws, L.off1), P<int>(plan_ws, L.off2), m.totals + 2);
@@ -1325,13 +1748,25 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
             hipLaunchKernelGGL(k_ccn1_fwd, dim3(nodes > 0 ? (nodes + 3) / 4 : 1), dim3(256), 0, s, v, tot, fin,
                                l == 0 ? 1 : 0, d_X, cin, w, b, h, P<float>(W, L.coll[l]), P<float>(W, L.F[l]));
         } else {
-            if (cin <= C2_CMAX && h <= C2_HMAX)
+            const bool narrow = cin <= C2_CMAX && h <= C2_HMAX;
+            if (narrow)
                 hipLaunchKernelGGL((k_ccn2_fwd<C2_CMAX, C2_HMAX>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s, v, tot,
                                    fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, save_of(L, W, l), P<float>(W, L.F[l]));
             else
                 hipLaunchKernelGGL((k_ccn2_fwd<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0,
                                    s, v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, save_of(L, W, l),
                                    P<float>(W, L.F[l]));
+            HGNN_LAUNCH_CHECK();
+            if (cfg->nmax > CCN_MAXD) {  // degrees 65..256 possible: their nodes in the large-degree kernel
+                if (narrow)
+                    hipLaunchKernelGGL((k_ccn2_fwd_big<C2_CMAX, C2_HMAX>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s,
+                                       v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, save_of(L, W, l),
+                                       P<float>(W, L.F[l]));
+                else
+                    hipLaunchKernelGGL((k_ccn2_fwd_big<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nodes > 0 ? nodes : 1),
+                                       dim3(256), 0, s, v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h,
+                                       save_of(L, W, l), P<float>(W, L.F[l]));
+            }
         }
         HGNN_LAUNCH_CHECK();
     }
@@ -1392,14 +1827,23 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
         } else {
             C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
                       P<float>(W, L.g_d3)};
-            if (cin <= C2_CMAX && h <= C2_HMAX)
+            const bool narrow = cin <= C2_CMAX && h <= C2_HMAX;
+            float* g0p = l == 0 ? P<float>(W, L.g0) : nullptr;
+            if (narrow)
                 hipLaunchKernelGGL((k_ccn2_bwd_node<C2_CMAX, C2_HMAX>), dim3(nb1), dim3(256), 0, s, v, tot, dF,
-                                   P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart,
-                                   l == 0 ? P<float>(W, L.g0) : nullptr);
+                                   P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
             else
                 hipLaunchKernelGGL((k_ccn2_bwd_node<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nb1), dim3(256), 0, s, v, tot,
-                                   dF, P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart,
-                                   l == 0 ? P<float>(W, L.g0) : nullptr);
+                                   dF, P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
+            HGNN_LAUNCH_CHECK();
+            if (cfg->nmax > CCN_MAXD) {
+                if (narrow)
+                    hipLaunchKernelGGL((k_ccn2_bwd_node<C2_CMAX, C2_HMAX, true>), dim3(nb1), dim3(256), 0, s, v, tot,
+                                       dF, P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
+                else
+                    hipLaunchKernelGGL((k_ccn2_bwd_node<C2_CMAX_WIDE, C2_HMAX_WIDE, true>), dim3(nb1), dim3(256), 0, s,
+                                       v, tot, dF, P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
+            }
         }
         HGNN_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_ccn_param_reduce, dim3(h * K + h), dim3(256), 0, s, ppart, tot, h * K, h, grads[2 * l],
@@ -1417,7 +1861,7 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
             if (lvl0)
                 hipLaunchKernelGGL(k_ccn2_dx0, dim3(nb4), dim3(256), 0, s, v, tot, P<float>(W, L.g0), cin, dsum, nf,
                                    dst);
-            else
+            else {
                 if (cin <= 2)
                     hipLaunchKernelGGL((k_ccn2_bwd_gather<2, 4>), dim3(nb1), dim3(256), 0, s, v, tot, gd, cin, dsum,
                                        nf, doff, lvl0, dst);
@@ -1427,6 +1871,19 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                 else
                     hipLaunchKernelGGL((k_ccn2_bwd_gather<C2_CMAX_WIDE, 1>), dim3(nb1), dim3(256), 0, s, v, tot, gd,
                                        cin, dsum, nf, doff, lvl0, dst);
+                HGNN_LAUNCH_CHECK();
+                if (cfg->nmax > CCN_MAXD) {
+                    if (cin <= 2)
+                        hipLaunchKernelGGL((k_ccn2_bwd_gather_big<2, 4>), dim3(nb1), dim3(256), 0, s, v, tot, gd, cin,
+                                           dsum, nf, doff, lvl0, dst);
+                    else if (cin <= C2_CMAX)
+                        hipLaunchKernelGGL((k_ccn2_bwd_gather_big<C2_CMAX, 1>), dim3(nb1), dim3(256), 0, s, v, tot, gd,
+                                           cin, dsum, nf, doff, lvl0, dst);
+                    else
+                        hipLaunchKernelGGL((k_ccn2_bwd_gather_big<C2_CMAX_WIDE, 1>), dim3(nb1), dim3(256), 0, s, v, tot,
+                                           gd, cin, dsum, nf, doff, lvl0, dst);
+                }
+            }
         }
         HGNN_LAUNCH_CHECK();
         float* t = dF;

@@ -25,7 +25,7 @@ DEVERR = {
     0x2: "mask[:, :, 0] disagrees with N_batch / E_batch",
     0x4: "N_batch > Nmax, E_batch > Emax or a negative count",
     0x8: "CCN adjacency without a self loop (chi_ii undefined, functions/utils_ccn.py:137-140)",
-    0x10: "CCN vertex degree above the compiled bound (1024 for CCN-1D, 64 for CCN-2D)",
+    0x10: "CCN vertex degree above the compiled bound (1024 for CCN-1D, 256 for CCN-2D)",
     0x20: "CCN adjacency pattern is not symmetric (the batched CCN backward needs A_ij > 0 <=> A_ji > 0)",
 }
 

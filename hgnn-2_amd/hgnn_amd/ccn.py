@@ -25,7 +25,7 @@ import torch
 from . import _lib as L
 from .net import _require_cuda, _f32, _i64, _raise_bits, check_errors, watch_word
 
-CCN_MAX_DEGREE = {1: 1024, 2: 64}  # csrc/ccn.hip CCN1_MAXD, CCN_MAXD (by order)
+CCN_MAX_DEGREE = {1: 1024, 2: 256}  # csrc/ccn.hip CCN1_MAXD, CCN_BIGD (by order)
 CCN2_MAX_CHANNELS = 16  # csrc/ccn.hip C2_CMAX_WIDE: CCN-2D f_in and hidden
 
 

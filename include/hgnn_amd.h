@@ -36,7 +36,7 @@
  *    so every per-call operand must stay under 2 GB -- about 12 K QM9-shape graphs per call at
  *    d = 64 (the 640-wide edge aggregate is the largest; split larger batches); the dense
  *    operator gradient (need_dw) keeps a graph's rows in LDS: Nmax <= ~1200 at J + 2 = 3;
- *  - CCN: receptive-field degree <= 1024 (CCN-1D) / 64 (CCN-2D), f_in and hidden <= 16
+ *  - CCN: receptive-field degree <= 1024 (CCN-1D) / 256 (CCN-2D), f_in and hidden <= 16
  *    (HGNN_DEVERR_CCN_DEGREE for the degree, an error status for the channel counts).
  */
 #ifndef HGNN_AMD_H

@@ -327,3 +327,37 @@ def test_ccn2_config5_full_batch_64_sbm200():
         _grad_close(gb[0][b, :x.shape[0]], xr.grad, f"cfg5 dX graph {b}")
     for (n, _), g in zip(net.named_parameters(), g8):
         _grad_close(g, p64[n].grad, f"cfg5 grad {n}")
+
+
+@pytest.mark.parametrize("hidden", [2, 12])
+def test_ccn2_degree_above_64_vs_closed_form_oracle(hidden):
+    """CCN-2D receptive fields beyond one wave: SBM N = 300 (degrees ~40-75, so one graph mixes the
+    fast d <= 64 kernels and the large-degree ones) and N = 400 (~60-100) in one padded batch vs the
+    fp64 closed-form oracle (oracle/ref_ccn.py ccn2_forward_closed): outputs, dX, parameter grads;
+    and the per-graph drop-in forward equals the batched one."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_2D
+    from oracle import ref_ccn as RC
+    graphs = dg.sbm_dataset(1, n=300, seed=41) + dg.sbm_dataset(1, n=400, seed=42)
+    graphs = [(X, A + torch.eye(A.shape[0]), t) for X, A, t in graphs]
+    degs = [int((a > 0).sum(1).max()) for _, a, _ in graphs]
+    assert max(degs) > 64 and min(int((a > 0).sum(1).min()) for _, a, _ in graphs) <= 64, degs
+    net = CCN_2D(5, 1, hidden, 2)
+    fu.det_init(net, 64 + hidden)
+    p64 = {n: v.detach().double().clone().requires_grad_(True) for n, v in net.named_parameters()}
+    net = net.cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    Xr = X.clone().requires_grad_(True)
+    out = net.forward_batch(Xr, A, nb)
+    w = torch.tensor([[1.0], [-0.75]])
+    (out * w.cuda()).sum().backward()
+    for b, (x, a, _) in enumerate(graphs):
+        with torch.no_grad():
+            _close(net(x.cuda(), a.cuda()), out[b].detach().cpu(), f"per-graph {b}", rel=1e-6)
+        xr = x.double().requires_grad_(True)
+        ref = RC.ccn2_forward_closed(p64, xr, a.double(), 2)
+        _close(out[b], ref, f"deg>64 graph {b}")
+        (ref * w[b].double()).sum().backward()
+        _grad_close(Xr.grad[b, :x.shape[0]], xr.grad, f"deg>64 dX graph {b}")
+    for n, p in net.named_parameters():
+        _grad_close(p.grad, p64[n].grad, f"deg>64 grad {n}")
