@@ -754,15 +754,16 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm5(const float* __restric
 
 }  // namespace
 
-// Row chunk of the dW slabs: ~dw3_target_blocks() blocks of 128 x 128 output tiles, multiple of 32 rows.
-// Target block count of the dW GEMM (split-K chunks x output tiles).  512 measured +0.7 % on the
-// step against 256 (same box, alternating runs): the dW kernel shares the chip with the main
-// stream's backward, and smaller chunks leave it sooner; HGNN_DW_BLOCKS overrides.
+// Target block count of the dW GEMM (split-K chunks x output tiles).  Every launched block has rows
+// (dw3_kc): at config 2, 256 blocks (one per CU) measured 1.340 / 1.344 ms per step against 1.377 /
+// 1.378 for 512 and 1.401 / 1.404 for 1024 (same box, alternating runs) -- the dW kernel runs on the
+// side stream beside the main stream's backward, and more of its blocks crowd the main stream's
+// kernels off the CUs; HGNN_DW_BLOCKS overrides.
 static int dw3_target_blocks() {
     static const int t = [] {
         const char* e = getenv("HGNN_DW_BLOCKS");
-        const int v = e ? atoi(e) : 512;
-        return v >= 16 && v <= 4096 ? v : 512;
+        const int v = e ? atoi(e) : 256;
+        return v >= 16 && v <= 4096 ? v : 256;
     }();
     return t;
 }
