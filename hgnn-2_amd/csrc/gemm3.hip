@@ -771,10 +771,13 @@ static int dw3_target_blocks() {
 int dw3_chunks(int r_cap, int o, int k) {
     const int tiles = ceil_div(o, 128) * ceil_div(k, 128);
     int chunks = dw3_target_blocks() / (tiles > 0 ? tiles : 1);
-    // never more chunks than 64-row pieces of the capacity; a multiple of 8 (XCD-aware order)
+    // never more chunks than 64-row pieces of the capacity; a multiple of 8 (XCD-aware order),
+    // rounded DOWN so the grid stays within the target: standalone on the config-2 edge dW shape
+    // (tools/dw_lab.hip) 48 chunks x 5 tiles = 240 blocks ran 41.5 us (0.58 of the fp32 MFMA peak),
+    // 56 x 5 = 280 blocks (a second partial round on 24 CUs) 55 us
     chunks = std::min(chunks, ceil_div(r_cap > 0 ? r_cap : 1, 64));
-    if (chunks < 1) chunks = 1;
-    return ceil_div(chunks, 8) * 8;
+    chunks = chunks / 8 * 8;
+    return chunks < 8 ? 8 : chunks;
 }
 
 size_t dw3_slab_floats(int r_cap, int o, int k) { return (size_t)dw3_chunks(r_cap, o, k) * o * k; }
