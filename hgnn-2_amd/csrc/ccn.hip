@@ -550,23 +550,17 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
 }
 
 struct C2Grad {
-    float* dSc;  // [sum d^2][C]
-    float* dSa;  // [sum d^2][C]
+    float* dSc;  // [sum d^2][C]  (dSc + dq1 folded)
+    float* dSa;  // [sum d^2][C]  (dSa + dq3 + dtot folded)
     float* dD1;  // [sum d^2][C]
     float* dD2;  // [sum d^2][C]  indexed [a][b]
-    float* dq1;  // [sum d][C]    gradient of q1[a] = sum_b Sc[a][b]  (reader adds it to dSc[a][.])
-    float* dq3;  // [sum d][C]    gradient of q3[b] = sum_z Sa[b][z]  (reader adds it to dSa[b][.])
-    float* dtot; // [nodes][C]    gradient of tot = sum Sc             (reader adds it to dSa[.][.])
     float* dd3;  // [nodes][C]
 };
 
-// Block per node: dpre = dF * relu'(F); param partials; node-level gradient matrices, in ONE sweep
-// over the n^2 entries when h <= 2 (config 5: h = 2): the parameter partials of an output pair
-// (the 9 distinct contraction blocks x cin, in registers) and the input-side gradients
-// g_q = W_q^T dpre (every output's dpre of the entry) from one read of the entry's statistics.
-// (Round 2 swept the entries once per output plus once more for the input side, and added the
-// q1 / q3 / tot gradients back into dSc / dSa in a read-modify-write pass: 7.3 GB per launch at
-// config 5.)  The q1 / q3 / tot gradients are kept apart (dq1, dq3, dtot) for their readers.
+// Block per node: dpre = dF * relu'(F); param partials; node-level gradient matrices.
+// One sweep over the n^2 entries per output o for the parameter partials (the 9 distinct
+// contraction blocks x cin accumulate in registers, then one wave-sum + LDS combine each), and one
+// sweep for the input-side gradients (every channel of an entry from one read of dpre).
 // BIG: the instantiation for degrees 65..256 (the level-0 reduction walks 64-lane chunks and
 // multi-word common-neighbour sets, dSa read from L2 instead of an n x n LDS copy).
 template <int CM, int HM, bool BIG = false>
@@ -576,9 +570,8 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
                                                        C2Grad gd, float* __restrict__ ppart,
                                                        float* __restrict__ g0) {
     constexpr int MAXN = BIG ? CCN_BIGD : CCN_MAXD;
-    constexpr int OB = CM <= 8 ? 2 : 1;  // outputs per parameter sweep (registers: OB x 9 x CM accumulators)
     __shared__ float sdq1[MAXN * CM], sdq3[MAXN * CM], sdtot[CM], sdd3[CM];
-    __shared__ float red[4][OB * 10 * CM];
+    __shared__ float red[4][10 * CM];
     __shared__ float sw[HM * 18 * CM];
     const int i = blockIdx.x;
     if (i >= *total_nodes) return;
@@ -592,138 +585,107 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
     for (int t = threadIdx.x; t < h * K; t += 256) sw[t] = W[t];
     for (int t = threadIdx.x; t < n * CM; t += 256) sdq1[t] = sdq3[t] = 0.f;
     if (threadIdx.x < cin) sdtot[threadIdx.x] = sdd3[threadIdx.x] = 0.f;
-    __syncthreads();
+    // parameter partials: dW[o][q*C + c] = sum_xy dpre[x][y][o] * block_q[x][y][c]
     // distinct blocks: 0 (n Sc; also 6..14), 1 q1, 2 n Sa, 3 q3, 4 tot (diag), 5 Sc, 15 D1, 16 D2^T, 17 d3 (diag)
-    for (int o0 = 0; o0 < h; o0 += OB) {
-        const bool last = o0 + OB >= h;  // the input-side gradients need every output's dpre: last sweep
-        float acc[OB][9][CM];
-        float sb[OB];
+    for (int o = 0; o < h; ++o) {
+        float acc[9][CM];
+        float sb = 0.f;
 #pragma unroll
-        for (int u = 0; u < OB; ++u) {
-            sb[u] = 0.f;
+        for (int q = 0; q < 9; ++q)
 #pragma unroll
-            for (int q = 0; q < 9; ++q)
-#pragma unroll
-                for (int c = 0; c < CM; ++c) acc[u][q][c] = 0.f;
-        }
+            for (int c = 0; c < CM; ++c) acc[q][c] = 0.f;
         for (int e = threadIdx.x; e < n * n; e += 256) {
             const int x = e / n, y = e % n;
             const long long r = o2 + e;
-            float dp[HM];
+            const float dp = F[r * h + o] > 0.f ? dF[r * h + o] : 0.f;
+            sb += dp;
 #pragma unroll
-            for (int o = 0; o < HM; ++o) {
-                const bool need = o < h && (last || (o >= o0 && o < o0 + OB));
-                dp[o] = (need && F[r * h + o] > 0.f) ? dF[r * h + o] : 0.f;
-            }
-            float dpu[OB];  // dp[o0 + u], selected without a dynamic register index
-#pragma unroll
-            for (int u = 0; u < OB; ++u) {
-                dpu[u] = 0.f;
-#pragma unroll
-                for (int o = 0; o < HM; ++o)
-                    if (o == o0 + u) dpu[u] = dp[o];
-                sb[u] += dpu[u];
-            }
-#pragma unroll
-            for (int c = 0; c < CM; ++c) {  // compile-time c: acc stays in registers
+            for (int c = 0; c < CM; ++c) {
                 if (c >= cin) break;
                 const float sc = sv.Sc[r * cin + c];
-                const float b1 = sv.q1[(o1 + x) * cin + c];
-                const float sa = sv.Sa[r * cin + c];
-                const float b3 = sv.q3[(o1 + x) * cin + c];
-                const float b4 = x == y ? sv.tot[(long long)i * cin + c] : 0.f;
-                const float b15 = sv.D1[r * cin + c];
-                const float b16 = sv.D2[(o2 + (long long)y * n + x) * cin + c];
-                const float b17 = x == y ? sv.d3[(long long)i * cin + c] : 0.f;
-#pragma unroll
-                for (int u = 0; u < OB; ++u) {
-                    const float d = dpu[u];
-                    acc[u][0][c] = fmaf(d, nf * sc, acc[u][0][c]);
-                    acc[u][1][c] = fmaf(d, b1, acc[u][1][c]);
-                    acc[u][2][c] = fmaf(d, nf * sa, acc[u][2][c]);
-                    acc[u][3][c] = fmaf(d, b3, acc[u][3][c]);
-                    acc[u][4][c] = fmaf(d, b4, acc[u][4][c]);
-                    acc[u][5][c] = fmaf(d, sc, acc[u][5][c]);
-                    acc[u][6][c] = fmaf(d, b15, acc[u][6][c]);
-                    acc[u][7][c] = fmaf(d, b16, acc[u][7][c]);
-                    acc[u][8][c] = fmaf(d, b17, acc[u][8][c]);
+                acc[0][c] = fmaf(dp, nf * sc, acc[0][c]);
+                acc[1][c] = fmaf(dp, sv.q1[(o1 + x) * cin + c], acc[1][c]);
+                acc[2][c] = fmaf(dp, nf * sv.Sa[r * cin + c], acc[2][c]);
+                acc[3][c] = fmaf(dp, sv.q3[(o1 + x) * cin + c], acc[3][c]);
+                if (x == y) {
+                    acc[4][c] = fmaf(dp, sv.tot[(long long)i * cin + c], acc[4][c]);
+                    acc[8][c] = fmaf(dp, sv.d3[(long long)i * cin + c], acc[8][c]);
                 }
-            }
-            if (last) {
-                // input-side gradients of the contraction blocks: g_q = W_q^T dpre (every output's dpre)
-                for (int c = 0; c < cin; ++c) {
-                    float g[18];
-#pragma unroll
-                    for (int q = 0; q < 18; ++q) g[q] = 0.f;
-#pragma unroll
-                    for (int o = 0; o < HM; ++o) {
-                        if (o >= h) break;
-                        const float* w = sw + o * K;
-#pragma unroll
-                        for (int q = 0; q < 18; ++q) g[q] = fmaf(w[q * cin + c], dp[o], g[q]);
-                    }
-                    float s9 = 0.f;
-#pragma unroll
-                    for (int q = 6; q < 15; ++q) s9 += g[q];
-                    gd.dSc[r * cin + c] = nf * (g[0] + s9) + g[5];
-                    gd.dSa[r * cin + c] = nf * g[2];
-                    gd.dD1[r * cin + c] = g[15];
-                    gd.dD2[(o2 + (long long)y * n + x) * cin + c] = g[16];
-                    atomicAdd(&sdq1[x * CM + c], g[1]);
-                    atomicAdd(&sdq3[x * CM + c], g[3]);
-                    if (x == y) {
-                        atomicAdd(&sdtot[c], g[4]);
-                        atomicAdd(&sdd3[c], g[17]);
-                    }
-                }
+                acc[5][c] = fmaf(dp, sc, acc[5][c]);
+                acc[6][c] = fmaf(dp, sv.D1[r * cin + c], acc[6][c]);
+                acc[7][c] = fmaf(dp, sv.D2[(o2 + y * n + x) * cin + c], acc[7][c]);
             }
         }
-        // parameter partials dW[o][q*C + c] = sum_xy dpre[x][y][o] * block_q[x][y][c]: wave sums, then
-        // the 4 waves in order
 #pragma unroll
-        for (int u = 0; u < OB; ++u) {
+        for (int q = 0; q < 9; ++q)
 #pragma unroll
-            for (int q = 0; q < 9; ++q)
-#pragma unroll
-                for (int c = 0; c < CM; ++c) {
-                    if (c >= cin) break;
-                    const float t = wave_sum(acc[u][q][c]);
-                    if (lane == 0) red[wv][(u * 10 + q) * CM + c] = t;
-                }
-            const float t = wave_sum(sb[u]);
-            if (lane == 0) red[wv][(u * 10 + 9) * CM] = t;
-        }
+            for (int c = 0; c < CM; ++c) {
+                if (c >= cin) break;
+                const float t = wave_sum(acc[q][c]);
+                if (lane == 0) red[wv][q * CM + c] = t;
+            }
+        sb = wave_sum(sb);
+        if (lane == 0) red[wv][9 * CM] = sb;
         __syncthreads();
-        for (int t = threadIdx.x; t < OB * 18 * cin; t += 256) {
-            const int u = t / (18 * cin), qc = t % (18 * cin), q = qc / cin, c = qc % cin;
-            const int o = o0 + u;
-            if (o >= h) continue;
+        for (int t = threadIdx.x; t < 18 * cin; t += 256) {
+            const int q = t / cin, c = t % cin;
             const int d = q < 6 ? q : (q < 15 ? 0 : q - 9);  // distinct-block index of q
-            const int k = (u * 10 + d) * CM + c;
-            pp[o * K + q * cin + c] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+            pp[o * K + q * cin + c] = red[0][d * CM + c] + red[1][d * CM + c] + red[2][d * CM + c] +
+                                      red[3][d * CM + c];
         }
-        if (threadIdx.x < OB && o0 + (int)threadIdx.x < h) {
-            const int k = ((int)threadIdx.x * 10 + 9) * CM;
-            pp[h * K + o0 + threadIdx.x] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
-        }
+        if (threadIdx.x == 0) pp[h * K + o] = red[0][9 * CM] + red[1][9 * CM] + red[2][9 * CM] +
+                                              red[3][9 * CM];
         __syncthreads();
     }
-    // the q1 / q3 / tot gradients, kept apart for the readers (no read-modify-write of dSc / dSa)
-    for (int t = threadIdx.x; t < n * cin; t += 256) {
-        const int a = t / cin, c = t % cin;
-        gd.dq1[(o1 + a) * cin + c] = sdq1[a * CM + c];
-        gd.dq3[(o1 + a) * cin + c] = sdq3[a * CM + c];
+    // input-side gradients of the contraction blocks: g_q = W_q^T dpre
+    for (int e = threadIdx.x; e < n * n; e += 256) {
+        const int x = e / n, y = e % n;
+        const long long r = o2 + e;
+        float dp[HM];
+#pragma unroll
+        for (int o = 0; o < HM; ++o) dp[o] = (o < h && F[r * h + o] > 0.f) ? dF[r * h + o] : 0.f;
+        for (int c = 0; c < cin; ++c) {
+            float g[18];
+#pragma unroll
+            for (int q = 0; q < 18; ++q) g[q] = 0.f;
+#pragma unroll
+            for (int o = 0; o < HM; ++o) {
+                if (o >= h) break;
+                const float* w = sw + o * K;
+#pragma unroll
+                for (int q = 0; q < 18; ++q) g[q] = fmaf(w[q * cin + c], dp[o], g[q]);
+            }
+            float s9 = 0.f;
+#pragma unroll
+            for (int q = 6; q < 15; ++q) s9 += g[q];
+            gd.dSc[r * cin + c] = nf * (g[0] + s9) + g[5];
+            gd.dSa[r * cin + c] = nf * g[2];
+            gd.dD1[r * cin + c] = g[15];
+            gd.dD2[(o2 + y * n + x) * cin + c] = g[16];
+            atomicAdd(&sdq1[x * CM + c], g[1]);
+            atomicAdd(&sdq3[x * CM + c], g[3]);
+            if (x == y) {
+                atomicAdd(&sdtot[c], g[4]);
+                atomicAdd(&sdd3[c], g[17]);
+            }
+        }
     }
-    if (threadIdx.x < cin) {
-        gd.dtot[(long long)i * cin + threadIdx.x] = sdtot[threadIdx.x];
-        gd.dd3[(long long)i * cin + threadIdx.x] = sdd3[threadIdx.x];
+    __syncthreads();
+    for (int e = threadIdx.x; e < n * n; e += 256) {
+        const int a = e / n;
+        const long long r = o2 + e;
+        for (int c = 0; c < cin; ++c) {
+            gd.dSc[r * cin + c] += sdq1[a * CM + c];                 // q1[a] = sum_b Sc[a][b]
+            gd.dSa[r * cin + c] += sdq3[a * CM + c] + sdtot[c];      // q3[b] = sum_z Sa[b][z]; tot: every entry
+        }
     }
+    if (threadIdx.x < cin) gd.dd3[(long long)i * cin + threadIdx.x] = sdd3[threadIdx.x];
     if (!g0) return;
     // Level 0 (F_0[j] = X[j] tiled): dX[j] needs only the sum of dT_i[a_j][b][z] over the valid (b, z),
     // so node i reduces its own gradient matrices per neighbour a (coalesced, L2-hot) instead of
-    // every j gathering them:  G[a] = m_a sum_{b in C_a} (dSc[a][b] + dq1[a]) + sum_{b,z in C_a} (dSa[b][z]
-    //   + dq3[b] + dtot) + sum_{b in C_a} dD1[a][b] + [a in C_a] (sum_{b in C_a} dD2[a][b] + dd3),
-    // C_a = {x: pos_a(x) >= 0}
+    // every j gathering them:  G[a] = m_a sum_{b in C_a} dSc[a][b] + sum_{b,z in C_a} dSa[b][z]
+    //   + sum_{b in C_a} dD1[a][b] + [a in C_a] (sum_{b in C_a} dD2[a][b] + dd3),  C_a = {x: pos_a(x) >= 0}
+    // dSa of one channel is staged in LDS so the masked row sums read LDS, not scattered HBM rows
     if constexpr (BIG) {
         __shared__ unsigned long long vmb[CCN_BIGD][CCN_BW];
         __shared__ int smc[CCN_BIGD];
@@ -748,14 +710,13 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
                 for (int b = lane; b < n; b += 64) {
                     if (!mbit(vmb[a], b)) continue;
                     const long long rab = (o2 + (long long)a * n + b) * cin + c;
-                    t += mf * (gd.dSc[rab] + sdq1[a * CM + c]) + gd.dD1[rab] + (va ? gd.dD2[rab] : 0.f);
-                    const float add = sdq3[b * CM + c] + sdtot[c];
+                    t += mf * gd.dSc[rab] + gd.dD1[rab] + (va ? gd.dD2[rab] : 0.f);
                     for (int w = 0; w < nw; ++w) {
                         unsigned long long zs = vmb[a][w];
                         while (zs) {
                             const int z = w * 64 + __ffsll((long long)zs) - 1;
                             zs &= zs - 1ull;
-                            t += gd.dSa[(o2 + (long long)b * n + z) * cin + c] + add;
+                            t += gd.dSa[(o2 + (long long)b * n + z) * cin + c];
                         }
                     }
                 }
@@ -764,8 +725,6 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
             }
         return;
     }
-    // dSa of one channel is staged in LDS (with its q3 / tot gradients added) so the masked row sums
-    // read LDS, not scattered HBM rows
     __shared__ unsigned long long vm[CCN_MAXD];
     __shared__ float sa_l[CCN_MAXD * CCN_MAXD];
     __syncthreads();
@@ -775,8 +734,7 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
     }
     for (int c = 0; c < cin; ++c) {
         __syncthreads();
-        for (int e = threadIdx.x; e < n * n; e += 256)
-            sa_l[e] = gd.dSa[(o2 + e) * cin + c] + (sdq3[(e / n) * CM + c] + sdtot[c]);
+        for (int e = threadIdx.x; e < n * n; e += 256) sa_l[e] = gd.dSa[(o2 + e) * cin + c];
         __syncthreads();
         for (int a = wv; a < n; a += 4) {
             const unsigned long long ma = vm[a];
@@ -786,7 +744,7 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
             float t = 0.f;
             if (vb) {
                 const long long rab = (o2 + (long long)a * n + lane) * cin + c;
-                t = mf * (gd.dSc[rab] + sdq1[a * CM + c]) + gd.dD1[rab] + (va ? gd.dD2[rab] : 0.f);
+                t = mf * gd.dSc[rab] + gd.dD1[rab] + (va ? gd.dD2[rab] : 0.f);
                 unsigned long long zs = ma;
                 while (zs) {
                     const int z = __ffsll((long long)zs) - 1;
@@ -896,7 +854,6 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_gather(CcnPlanView v, const in
                 const int b = max(sp[a * n + u], 0), z = vz[q] ? sp[a * n + lane] : 0;
                 const int aj = s_aj[a], di = s_di[a], i = s_i[a];
                 const long long oi = s_oi[a];
-                const long long oq1 = (long long)v.off1[i] * cin;  // q1 / q3 gradients of node i
                 const long long rab = (oi + (long long)aj * di + b) * cin, rbz = (oi + (long long)b * di + z) * cin;
                 zb[q] = b;
                 zz[q] = z;
@@ -904,8 +861,8 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_gather(CcnPlanView v, const in
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
                     const bool ok = c < cin;
-                    tsc[q][c] = ok ? gd.dSc[rab + c] + gd.dq1[oq1 + aj * cin + c] : 0.f;
-                    tsa[q][c] = ok ? gd.dSa[rbz + c] + (gd.dq3[oq1 + b * cin + c] + gd.dtot[(long long)i * cin + c]) : 0.f;
+                    tsc[q][c] = ok ? gd.dSc[rab + c] : 0.f;
+                    tsa[q][c] = ok ? gd.dSa[rbz + c] : 0.f;
                     td1[q][c] = ok ? gd.dD1[rab + c] : 0.f;
                     td2[q][c] = ok ? gd.dD2[rab + c] : 0.f;
                     td3[q][c] = ok ? gd.dd3[(long long)i * cin + c] : 0.f;
@@ -1270,7 +1227,6 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_gather_big(CcnPlanView v, cons
                         const int b = max(sp[(long long)a * n + u], 0), z = vz[q] ? sp[(long long)a * n + wl] : 0;
                         const int aj = s_aj[a], di = s_di[a], i = s_i[a];
                         const long long oi = s_oi[a];
-                        const long long oq1 = (long long)v.off1[i] * cin;  // q1 / q3 gradients of node i
                         const long long rab = (oi + (long long)aj * di + b) * cin, rbz = (oi + (long long)b * di + z) * cin;
                         zb[q] = b;
                         zz[q] = z;
@@ -1278,8 +1234,8 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_gather_big(CcnPlanView v, cons
 #pragma unroll
                         for (int c = 0; c < C; ++c) {
                             const bool ok = c < cin;
-                            tsc[q][c] = ok ? gd.dSc[rab + c] + gd.dq1[oq1 + aj * cin + c] : 0.f;
-                            tsa[q][c] = ok ? gd.dSa[rbz + c] + (gd.dq3[oq1 + b * cin + c] + gd.dtot[(long long)i * cin + c]) : 0.f;
+                            tsc[q][c] = ok ? gd.dSc[rab + c] : 0.f;
+                            tsa[q][c] = ok ? gd.dSa[rbz + c] : 0.f;
                             td1[q][c] = ok ? gd.dD1[rab + c] : 0.f;
                             td2[q][c] = ok ? gd.dD2[rab + c] : 0.f;
                             td3[q][c] = ok ? gd.dd3[(long long)i * cin + c] : 0.f;
@@ -1553,7 +1509,7 @@ struct CcnLayout {
     std::vector<size_t> F, coll;    // per level 1..L
     std::vector<C2Save> dummy;
     size_t sc[16], sa[16], d1[16], d2[16], q1[16], q3[16], tot[16], d3[16];
-    size_t feat, rpart, g0, dsum, ppart, dF[2], dcoll, g_sc, g_sa, g_d1, g_d2, g_d3, g_q1, g_q3, g_tot, xp, dxp;
+    size_t feat, rpart, g0, dsum, ppart, dF[2], dcoll, g_sc, g_sa, g_d1, g_d2, g_d3, xp, dxp;
     size_t bytes;
 };
 
@@ -1624,9 +1580,6 @@ CcnLayout ccn_layout(const hgnn_ccn_config* c, long long sum_d, long long sum_d2
         L.g_d1 = take(4 * (size_t)sum_d2 * cmax);
         L.g_d2 = take(4 * (size_t)sum_d2 * cmax);
         L.g_d3 = take(4 * (size_t)nodes * cmax);
-        L.g_q1 = take(4 * (size_t)(sum_d > 0 ? sum_d : 1) * cmax);
-        L.g_q3 = take(4 * (size_t)(sum_d > 0 ? sum_d : 1) * cmax);
-        L.g_tot = take(4 * (size_t)nodes * cmax);
     }
     L.xp = take(4 * (size_t)nodes * f);
     L.dxp = take(4 * (size_t)nodes * f);
@@ -1873,7 +1826,7 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                                P<float>(W, L.coll[l]), cin, w, h, P<float>(W, L.dcoll), ppart);
         } else {
             C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
-                      P<float>(W, L.g_q1), P<float>(W, L.g_q3), P<float>(W, L.g_tot), P<float>(W, L.g_d3)};
+                      P<float>(W, L.g_d3)};
             const bool narrow = cin <= C2_CMAX && h <= C2_HMAX;
             float* g0p = l == 0 ? P<float>(W, L.g0) : nullptr;
             if (narrow)
@@ -1904,7 +1857,7 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                                nf, doff, lvl0, dst);
         } else {
             C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
-                      P<float>(W, L.g_q1), P<float>(W, L.g_q3), P<float>(W, L.g_tot), P<float>(W, L.g_d3)};
+                      P<float>(W, L.g_d3)};
             if (lvl0)
                 hipLaunchKernelGGL(k_ccn2_dx0, dim3(nb4), dim3(256), 0, s, v, tot, P<float>(W, L.g0), cin, dsum, nf,
                                    dst);
