@@ -48,27 +48,35 @@ struct CcnPlanView {
 };
 
 // ------------------------------------------------------------------ plan
+// Row r of graph b (wave per row, CCN_NB_ROWS rows per block): the neighbour list (ascending), degree and
+// self position, and the row's pattern as a bit set over the graph's local node ids (64-bit words) with
+// the exclusive prefix count of each word, from which k_ccn_pos reads positions by popcount.
+constexpr int CCN_NB_ROWS = 16;
 __global__ void __launch_bounds__(256) k_ccn_nbrs(const float* __restrict__ adj, int nmax, const int* node_off,
-                                                  int* deg, int* nbr, int* selfpos, int* graph, uint32_t* err,
-                                                  int maxd) {
+                                                  int* deg, int* nbr, int* selfpos, int* graph,
+                                                  unsigned long long* bits, int* bcnt, uint32_t* err, int maxd) {
     const int b = blockIdx.x;
     const int n0 = node_off[b];
     const int nb = node_off[b + 1] - n0;
+    const int nw = (nmax + 63) >> 6;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const float* A = adj + (long long)b * nmax * nmax;
-    for (int r = wv; r < nb; r += 4) {
+    const int r1 = min(nb, (int)(blockIdx.y + 1) * CCN_NB_ROWS);
+    for (int r = blockIdx.y * CCN_NB_ROWS + wv; r < r1; r += 4) {
         const int gi = n0 + r;
         int cnt = 0, sp = -1;
         for (int c0 = 0; c0 < nb; c0 += 64) {
             const int c = c0 + lane;
             const bool nz = c < nb && A[(long long)r * nmax + c] > 0.f;   // utils_ccn.py:195 (A > 0)
-            // the gather-form backward walks N(j) for the readers of F_j: needs a symmetric pattern
-            if (c < nb && nz != (A[(long long)c * nmax + r] > 0.f)) atomicOr(err, (uint32_t)ERR_CCN_ASYM);
             const unsigned long long m = __ballot(nz);
             const int p = __popcll(m & ((1ull << lane) - 1ull));
             if (nz) {
                 nbr[(long long)gi * nmax + cnt + p] = n0 + c;
                 if (c == r) sp = cnt + p;
+            }
+            if (lane == 0) {
+                bits[(long long)gi * nw + (c0 >> 6)] = m;
+                bcnt[(long long)gi * nw + (c0 >> 6)] = cnt;
             }
             cnt += __popcll(m);
         }
@@ -90,48 +98,54 @@ __global__ void __launch_bounds__(256) k_ccn_nbrs(const float* __restrict__ adj,
     }
 }
 
-// exclusive scans of deg and deg^2 over all nodes (single block); totals[0..1]
-__global__ void __launch_bounds__(256) k_ccn_scan(const int* deg, const int* total_nodes, int* off1, int* off2,
-                                                  int* totals) {
-    __shared__ int s1[256], s2[256], carry[2];
+// exclusive scans of deg and deg^2 over all nodes (single block of 1024: a serial run of consecutive
+// nodes per thread, then a scan of the 1024 run totals); totals[0..1]
+__global__ void __launch_bounds__(1024) k_ccn_scan(const int* deg, const int* total_nodes, int* off1, int* off2,
+                                                   int* totals) {
+    __shared__ int s1[1024], s2[1024];
     const int t = threadIdx.x;
     const int n = *total_nodes;
-    if (t == 0) carry[0] = carry[1] = 0;
+    const int per = (n + 1023) / 1024;
+    const int i0 = min(n, t * per), i1 = min(n, i0 + per);
+    int a1 = 0, a2 = 0;
+    for (int i = i0; i < i1; ++i) {
+        const int d = deg[i];
+        a1 += d;
+        a2 += d * d;
+    }
+    s1[t] = a1;
+    s2[t] = a2;
     __syncthreads();
-    for (int base = 0; base < n; base += 256) {
-        const int i = base + t;
-        const int d = i < n ? deg[i] : 0;
-        s1[t] = d;
-        s2[t] = d * d;
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int b1 = t >= o ? s1[t - o] : 0, b2 = t >= o ? s2[t - o] : 0;
         __syncthreads();
-        for (int o = 1; o < 256; o <<= 1) {
-            const int a1 = t >= o ? s1[t - o] : 0, a2 = t >= o ? s2[t - o] : 0;
-            __syncthreads();
-            s1[t] += a1;
-            s2[t] += a2;
-            __syncthreads();
-        }
-        if (i < n) {
-            off1[i] = carry[0] + s1[t] - d;
-            off2[i] = carry[1] + s2[t] - d * d;
-        }
-        __syncthreads();
-        if (t == 255) {
-            carry[0] += s1[255];
-            carry[1] += s2[255];
-        }
+        s1[t] += b1;
+        s2[t] += b2;
         __syncthreads();
     }
-    if (t == 0) {
-        off1[n] = carry[0];
-        off2[n] = carry[1];
-        totals[0] = carry[0];
-        totals[1] = carry[1];
+    int c1 = s1[t] - a1, c2 = s2[t] - a2;
+    for (int i = i0; i < i1; ++i) {
+        const int d = deg[i];
+        off1[i] = c1;
+        off2[i] = c2;
+        c1 += d;
+        c2 += d * d;
+    }
+    if (t == 1023) {
+        off1[n] = s1[1023];
+        off2[n] = s2[1023];
+        totals[0] = s1[1023];
+        totals[1] = s2[1023];
     }
 }
 
-// pos[off2[i] + a*d_i + x] = index of nbr_i[x] in nbr_{nbr_i[a]} (binary search), or -1
-__global__ void __launch_bounds__(256) k_ccn_pos(CcnPlanView v, const int* total_nodes, int* pos, long long pos_cap,
+// pos[off2[i] + a*d_i + x] = index of nbr_i[x] in nbr_{nbr_i[a]}, or -1: the count of j's neighbours
+// below u = nbr_i[x] in j's row bit set (prefix count of u's word + popcount of the bits below u).
+// The position of i itself in N(j) must exist for every j in N(i): the gather-form backward walks
+// N(j) for the readers of F_j, so the pattern has to be symmetric.
+__global__ void __launch_bounds__(256) k_ccn_pos(CcnPlanView v, const int* total_nodes,
+                                                 const unsigned long long* __restrict__ bits,
+                                                 const int* __restrict__ bcnt, int* pos, long long pos_cap,
                                                  uint32_t* err) {
     const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
@@ -143,28 +157,34 @@ __global__ void __launch_bounds__(256) k_ccn_pos(CcnPlanView v, const int* total
     }
     const int n = v.deg[i];
     if (n > CCN1_MAXD) return;
+    const int nw = (v.nmax + 63) >> 6;
+    const int n0 = v.node_off[v.graph[i]];
+    const int si = v.selfpos[i];
     const int* ni = v.nbr + (long long)i * v.nmax;
+    const long long pb = v.off2[i];
     for (int x0 = 0; x0 < n; x0 += 64) {
         const int x = x0 + lane;
-        const int me = x < n ? ni[x] : -1;
-        for (int a = 0; a < n; ++a) {
-            const int j = ni[a];
-            const int dj = v.deg[j];
-            const int* nj = v.nbr + (long long)j * v.nmax;
-            int p = -1;
-            if (x < n) {
-                int lo = 0, hi = dj - 1;
-                while (lo <= hi) {
-                    const int mid = (lo + hi) >> 1;
-                    const int val = nj[mid];
-                    if (val == me) {
-                        p = mid;
-                        break;
-                    }
-                    if (val < me) lo = mid + 1;
-                    else hi = mid - 1;
+        const int u = x < n ? ni[x] - n0 : 0;
+        const int uw = u >> 6;
+        const unsigned long long below = (1ull << (u & 63)) - 1ull;
+        for (int a = 0; a < n; a += 4) {
+            unsigned long long w[4];
+            int c[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = ni[a + q < n ? a + q : a];
+                w[q] = bits[(long long)j * nw + uw];
+                c[q] = bcnt[(long long)j * nw + uw];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (a + q >= n) break;
+                if (x < n) {
+                    const bool in = (w[q] >> (u & 63)) & 1ull;
+                    const int p = in ? c[q] + __popcll(w[q] & below) : -1;
+                    pos[pb + (long long)(a + q) * n + x] = p;
+                    if (x == si && p < 0) atomicOr(err, (uint32_t)ERR_CCN_ASYM);
                 }
-                pos[v.off2[i] + (long long)a * n + x] = p;
             }
         }
     }
@@ -309,43 +329,79 @@ struct C2Save {
     float* d3;   // [nodes][C]
 };
 
-// Block per node i (n = d_i).  T[a][b][z] = F_{j_a}[p_a(b)][p_a(z)] is nonzero only where both
-// positions exist, i.e. b, z in the common neighbourhood C_a = N(i) n N(j_a) (|C_a| = m_a, 10.9 on
-// average on SBM-200 against d = 36), so the contraction statistics are gathered over C_a x C_a
-// only: sum_a m_a^2 instead of d^3 (9x less on config 5).  Zero terms are skipped, not added, so
-// the sums are those of the dense loops.  Two wave-parallel passes, no atomics (deterministic):
-//   pass A, wave per a, lane b:  Sc[a][b] = sum_{z in C_a} T, D1[a][b] = T[a][b][b],
-//           D2[a][b] = T[a][b][a], q1[a] = sum_b Sc (wave sum), d3 += T[a][a][a]
-//   pass B, wave per b, lane z:  Sa[b][z] = sum_{a: b in C_a} T, q3[b] = sum_z Sa (wave sum)
-// The validity of the loop index (z in pass A, a in pass B) is wave-uniform, so each wave walks
-// the set bits of a ballot.  Level 0 (F_0[j] = X[j] tiled, utils_ccn.py:167-172) needs no gather.
 constexpr int C2_CMAX = 8;  // channels of a CCN-2D level (f_in or hidden) handled per pass (narrow kernels)
 constexpr int C2_HMAX = 8;  // hidden size bound of the fused output stage (narrow kernels)
 constexpr int C2_CMAX_WIDE = 16;  // the wide instantiations: f_in, hidden <= 16
 constexpr int C2_HMAX_WIDE = 16;
 
-template <int CM, int HM>
-__global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* total_nodes, const float* __restrict__ fin,
-                                                  int level0, const float* __restrict__ X, int cin,
-                                                  const float* __restrict__ W, const float* __restrict__ bias, int h,
-                                                  C2Save sv, float* __restrict__ fout) {
-    __shared__ int sp[CCN_MAXD * CCN_MAXD];
-    __shared__ unsigned long long vmask[CCN_MAXD];  // bit x of vmask[a]: x in C_a
-    __shared__ float sred[2][4][CM];           // per-wave partial q1-total and d3
-    __shared__ int s_j[CCN_MAXD], s_dj[CCN_MAXD], s_oj[CCN_MAXD];  // neighbour a: node, degree, 2D row offset
-    const int i = blockIdx.x;
-    if (i >= *total_nodes) return;
-    const int n = v.deg[i];
-    if (n > CCN_MAXD || cin > CM || h > HM) return;
+// CCN-2D layer, receptive fields of degree <= 64 (SBM-200: d ~ 20-60; QM9: d <= 6).
+//
+// Block per node i (n = d_i), one wave per receptive-field row b.  The wave walks the neighbours a
+// with b in C_a (C_a = {x : p_a(x) >= 0}, the common neighbourhood N(i) n N(j_a), ascending) and
+// loads the row segment t[z] = T[a][b][z] = F_{j_a}[p_a(b)][p_a(z)] (lane z, z in C_a: one
+// coalesced piece of a row of F_{j_a}).  Every contraction statistic comes from that one load:
+//   Sa[b][z] += t                         lane z; the wave owns row b of Sa
+//   Sc[a][b]  = sum_z t                   wave total (DPP)           -> entry (a, b)
+//   D1[a][b]  = t[b]                      lane b's value             -> entry (a, b)
+//   D2[a][b]  = t[a]                      lane a's value (a in C_a)  -> entry (b, a), lane a here
+//   q1[a]    += Sc[a][b] (W1-projected, per-wave LDS partials), d3 = sum_b t[b] at a == b
+// The Linear of the 18 blocks (q0 = n Sc, q1, q2 = n Sa, q3, q4 = [x=y] tot, q5 = Sc,
+// q6..14 = n Sc, q15 = D1, q16 = D2^T, q17 = [x=y] d3) is applied with combined weights
+// (A = W0 + W6 + ... + W14: alpha = n A + W5 multiplies Sc) and assembled in LDS:
+//   pre[x][y] = P[x][y] + W1 q1[x] + W3 q3[x] + [x = y](W4 tot + W17 d3) + bias,
+// where P[x][y] receives at most two additions onto zero -- the row wave's part (n W2 Sa + W16 D2^T)
+// and the column wave's (alpha Sc + W15 D1) -- so its value does not depend on their order.
+// Nothing but F_out is written: the backward (k_c2_bwd) recomputes these sums instead of reading
+// saved n^2 C arrays.  Level 0 (F_0[j] = X[j] tiled, utils_ccn.py:167-172): t = X[j_a] on C_a,
+// Sc = m_a X[j_a], D1 = X[j_a], no gather and no reduction.
+// Output channels are processed HC at a time (one pass each; h = 2 -- the reference's default --
+// is one pass).  Dynamic LDS: P [ncap^2][HC] floats, then the position map [ncap^2] int16.
+constexpr int C2_NCAP = 64;
+enum { WA, WB, WQ1, WQ2, WQ3, WQ4, WQ15, WQ16, WQ17, NWC };
+
+size_t c2_dyn_lds(int ncap, int hc_max) { return (size_t)ncap * ncap * (4 * hc_max + 2); }
+
+// combined weights of output channels [o0, o0 + hc): wc[k][o][c]
+template <int HC, int CM>
+__device__ __forceinline__ void c2_weights(float (*wc)[HC][CM], const float* __restrict__ W, int cin, int o0, int hc) {
+    const int K = 18 * cin;
+    for (int t = threadIdx.x; t < HC * CM; t += blockDim.x) {
+        const int o = t / CM, c = t % CM;
+        const bool ok = o < hc && c < cin;
+        const float* w = W + (long long)(o0 + (ok ? o : 0)) * K;
+        float a = 0.f;
+        if (ok) {
+            a = w[c];
+            for (int q = 6; q < 15; ++q) a += w[q * cin + c];
+        }
+        wc[WA][o][c] = a;
+        wc[WB][o][c] = ok ? w[5 * cin + c] : 0.f;
+        wc[WQ1][o][c] = ok ? w[1 * cin + c] : 0.f;
+        wc[WQ2][o][c] = ok ? w[2 * cin + c] : 0.f;
+        wc[WQ3][o][c] = ok ? w[3 * cin + c] : 0.f;
+        wc[WQ4][o][c] = ok ? w[4 * cin + c] : 0.f;
+        wc[WQ15][o][c] = ok ? w[15 * cin + c] : 0.f;
+        wc[WQ16][o][c] = ok ? w[16 * cin + c] : 0.f;
+        wc[WQ17][o][c] = ok ? w[17 * cin + c] : 0.f;
+    }
+}
+
+// node prologue shared by k_c2_fwd / k_c2_bwd: position map (int16) and neighbour data in LDS,
+// then the common-neighbourhood masks
+template <int CM>
+__device__ __forceinline__ void c2_prologue(const CcnPlanView& v, int i, int n, int level0, const float* __restrict__ X,
+                                            int cin, short* sp, unsigned long long* vmask, int* s_oj, int* s_dj,
+                                            float (*s_x)[CM]) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int* ni = v.nbr + (long long)i * v.nmax;
-    const long long o2 = v.off2[i], o1 = v.off1[i];
-    for (int e = threadIdx.x; e < n * n; e += 256) sp[e] = v.pos[o2 + e];
-    if (threadIdx.x < n) {
+    const long long o2 = v.off2[i];
+    for (int e = threadIdx.x; e < n * n; e += 256) sp[e] = (short)v.pos[o2 + e];
+    if ((int)threadIdx.x < n) {
         const int j = ni[threadIdx.x];
-        s_j[threadIdx.x] = j;
-        s_dj[threadIdx.x] = v.deg[j];
         s_oj[threadIdx.x] = v.off2[j];
+        s_dj[threadIdx.x] = v.deg[j];
+#pragma unroll
+        for (int c = 0; c < CM; ++c) s_x[threadIdx.x][c] = (level0 && c < cin) ? X[(long long)j * cin + c] : 0.f;
     }
     __syncthreads();
     for (int a = wv; a < n; a += 4) {
@@ -353,199 +409,268 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd(CcnPlanView v, const int* tota
         if (lane == 0) vmask[a] = m;
     }
     __syncthreads();
+}
 
-    // ---- pass A: wave per neighbour a, lane b
-    float tq[CM], td3[CM];
+// next NB set bits of a 64-bit wave-uniform set, ascending (-1 past the end)
+template <int NB>
+__device__ __forceinline__ void c2_take(unsigned long long& s, int (&aa)[NB]) {
 #pragma unroll
-    for (int c = 0; c < CM; ++c) tq[c] = td3[c] = 0.f;
-    for (int a = wv; a < n; a += 4) {
-        const int j = ni[a];
-        const unsigned long long ma = vmask[a];
-        const int pb = lane < n ? sp[a * n + lane] : -1;
-        const bool vb = pb >= 0;
-        float sc[CM], d1[CM], d2[CM];
+    for (int u = 0; u < NB; ++u) {
+        aa[u] = s ? __ffsll((long long)s) - 1 : -1;
+        s &= s ? s - 1ull : 0ull;
+    }
+}
+
+// 64-bit wave-uniform value of lane l
+__device__ __forceinline__ unsigned long long lane_value_u64(unsigned long long v, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ int lane_value_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// t[u][c] = T[a_u][b][lane] for a batch of NB neighbours (0 where lane is not in C_a or a_u < 0); lane a of
+// my_mask / my_oj / my_dj holds neighbour a's common-neighbourhood mask, 2-D row offset and degree
+template <int CM, int NB>
+__device__ __forceinline__ void c2_load_rows(const float* __restrict__ fin, int cin, int n, int b, const int (&aa)[NB],
+                                             const short* sp, unsigned long long my_mask, int my_oj, int my_dj,
+                                             float (&t)[NB][CM]) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
-        for (int c = 0; c < CM; ++c) sc[c] = d1[c] = d2[c] = 0.f;
-        if (level0) {
-            const float mf = (float)__popcll(ma);
-            const bool va = (ma >> a) & 1ull;
+    for (int u = 0; u < NB; ++u) {
+        const int a = aa[u] >= 0 ? aa[u] : 0;
+        const bool vz = aa[u] >= 0 && ((lane_value_u64(my_mask, a) >> lane) & 1ull);
+        const int pb = uniform(max((int)sp[a * n + b], 0));
+        const int pz = vz ? (int)sp[a * n + lane] : 0;
+        const float* q = fin + ((long long)lane_value_i(my_oj, a) + (long long)pb * lane_value_i(my_dj, a)) * cin;
 #pragma unroll
-            for (int c = 0; c < CM; ++c) {
-                if (c >= cin) break;
-                const float xj = X[(long long)j * cin + c];
-                sc[c] = vb ? mf * xj : 0.f;
-                d1[c] = vb ? xj : 0.f;
-                d2[c] = (vb && va) ? xj : 0.f;
+        for (int c = 0; c < CM; ++c) t[u][c] = c < cin ? q[(long long)pz * cin + c] : 0.f;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) t[u][c] = vz ? t[u][c] : 0.f;
+    }
+}
+
+template <int CM, int HC, int NB, bool L0>
+__global__ void __launch_bounds__(256) k_c2_fwd(CcnPlanView v, const int* total_nodes, const float* __restrict__ fin,
+                                                const float* __restrict__ X, int cin, const float* __restrict__ W,
+                                                const float* __restrict__ bias, int h, int ncap,
+                                                float* __restrict__ fout) {
+    extern __shared__ float c2_dyn[];
+    __shared__ unsigned long long vmask[C2_NCAP];
+    __shared__ int s_oj[C2_NCAP], s_dj[C2_NCAP];
+    __shared__ float s_x[C2_NCAP][CM];
+    __shared__ float wc[NWC][HC][CM];
+    __shared__ float qw[4][C2_NCAP][HC];  // per-wave sums of W1 Sc[a][b] over the wave's rows b (W1 q1[a])
+    __shared__ float q3p[C2_NCAP][HC];    // W3 q3[b]
+    __shared__ float q3s[C2_NCAP][CM];    // q3[b] (tot = sum_b q3[b])
+    __shared__ float d3s[C2_NCAP][CM];    // T[b][b][b]
+    __shared__ float s_diag[HC];
+    const int i = blockIdx.x;
+    if (i >= *total_nodes) return;
+    const int n = v.deg[i];
+    if (n > C2_NCAP || n > ncap || cin > CM) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float* P = c2_dyn;
+    short* sp = reinterpret_cast<short*>(c2_dyn + ncap * ncap * HC);
+    c2_prologue<CM>(v, i, n, L0 ? 1 : 0, X, cin, sp, vmask, s_oj, s_dj, s_x);
+    const long long o2 = v.off2[i];
+    const float nf = (float)n;
+    // lane a holds neighbour a's mask, row offset and degree (read by the walks with readlane)
+    const bool la = lane < n;
+    const unsigned long long my_mask = la ? vmask[lane] : 0ull;
+    const int my_oj = la ? s_oj[lane] : 0, my_dj = la ? s_dj[lane] : 0;
+    for (int o0 = 0; o0 < h; o0 += HC) {
+        const int hc = min(HC, h - o0);
+        c2_weights<HC, CM>(wc, W, cin, o0, hc);
+        for (int e = threadIdx.x; e < n * n * HC; e += 256) P[e] = 0.f;
+        __syncthreads();
+        float vacc[HC];  // lane a: sum over this wave's rows b of W1 Sc[a][b]
+#pragma unroll
+        for (int o = 0; o < HC; ++o) vacc[o] = 0.f;
+        if constexpr (L0) {
+            // T = X[j_a] on C_a x C_a: every block of the Linear is a per-neighbour vector (lane a)
+            //   Sc[a][b] = m_a X_a, D1[a][b] = X_a, D2[a][b] = [a in C_a] X_a (b in C_a),
+            //   Sa[b][z] = sum_{a: b,z in C_a} X_a, q1[a] = m_a^2 X_a, q3[b] = sum_{a: b in C_a} m_a X_a,
+            //   tot = sum_a m_a^2 X_a, d3 = sum_a [a in C_a] X_a
+            const float mf = (float)__popcll(my_mask);
+            const bool va = la && ((my_mask >> lane) & 1ull);
+            float u[HC], dl[HC], bx[HC], q3a[HC];
+#pragma unroll
+            for (int o = 0; o < HC; ++o) {
+                u[o] = dl[o] = bx[o] = q3a[o] = 0.f;
+#pragma unroll
+                for (int c = 0; c < CM; ++c) {
+                    if (c >= cin) break;
+                    const float x = la ? s_x[lane][c] : 0.f;
+                    u[o] = fmaf(fmaf(fmaf(nf, wc[WA][o][c], wc[WB][o][c]), mf, wc[WQ15][o][c]), x, u[o]);
+                    dl[o] = fmaf(wc[WQ16][o][c], x, dl[o]);
+                    bx[o] = fmaf(nf * wc[WQ2][o][c], x, bx[o]);
+                    vacc[o] = fmaf(wc[WQ1][o][c], x, vacc[o]);
+                    q3a[o] = fmaf(wc[WQ3][o][c], x, q3a[o]);
+                }
+                dl[o] = va ? dl[o] : 0.f;
+                vacc[o] *= mf * mf;  // W1 q1[a]
+                q3a[o] *= mf;
             }
+            if (wv == 0) {
+                float dg[HC];
+#pragma unroll
+                for (int o = 0; o < HC; ++o) dg[o] = 0.f;
+#pragma unroll
+                for (int c = 0; c < CM; ++c) {
+                    if (c >= cin) break;
+                    const float x = la ? s_x[lane][c] : 0.f;
+                    const float tt = wave_total(mf * mf * x), dd = wave_total(va ? x : 0.f);
+#pragma unroll
+                    for (int o = 0; o < HC; ++o) dg[o] = fmaf(wc[WQ4][o][c], tt, fmaf(wc[WQ17][o][c], dd, dg[o]));
+                }
+                if (lane < HC) {
+#pragma unroll
+                    for (int o = 0; o < HC; ++o)
+                        if (lane == o) s_diag[o] = dg[o];
+                }
+            }
+            for (int b = wv; b < n; b += 4) {
+                const unsigned long long ab = __ballot(la && ((my_mask >> b) & 1ull));  // a with b in C_a
+                const bool in = (ab >> lane) & 1ull;
+                float s[HC];
+#pragma unroll
+                for (int o = 0; o < HC; ++o) {
+                    if (in && o < hc) atomicAdd(&P[(lane * n + b) * HC + o], u[o]);  // entry (a, b): alpha Sc + W15 D1
+                    s[o] = in ? dl[o] : 0.f;                                            // entry (b, a): W16 D2[a][b]
+                    const float q = wave_total(in ? q3a[o] : 0.f);
+                    if (lane == 0) q3p[b][o] = q;
+                }
+                unsigned long long as = ab;
+                while (as) {
+                    const int a = __ffsll((long long)as) - 1;
+                    as &= as - 1ull;
+                    const bool vz = (lane_value_u64(my_mask, a) >> lane) & 1ull;
+#pragma unroll
+                    for (int o = 0; o < HC; ++o) s[o] += vz ? lane_value(bx[o], a) : 0.f;  // n W2 Sa[b][z]
+                }
+                if (la)
+#pragma unroll
+                    for (int o = 0; o < HC; ++o)
+                        if (o < hc) atomicAdd(&P[(b * n + lane) * HC + o], s[o]);
+            }
+            if (wv != 0)
+#pragma unroll
+                for (int o = 0; o < HC; ++o) vacc[o] = 0.f;  // W1 q1[a] once (wave 0's copy)
         } else {
-            const int dj = s_dj[a];
-            const float* row = fin + ((long long)s_oj[a] + (long long)(vb ? pb : 0) * dj) * cin;
-            // the common neighbours z (wave-uniform) in batches of 4: all loads of a batch in flight
-            // before any is used (a one-at-a-time walk paid one memory latency per z); same order of
-            // summation
-            unsigned long long zs = ma;
-            while (zs) {
-                int zz[4];
+            for (int b = wv; b < n; b += 4) {
+                float sa[CM], sd[HC], ua[HC];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    zz[u] = zs ? __ffsll((long long)zs) - 1 : -1;
-                    zs &= zs ? zs - 1ull : 0ull;
-                }
-                float t[4][CM];
+                for (int c = 0; c < CM; ++c) sa[c] = 0.f;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int pz = zz[u] >= 0 ? sp[a * n + zz[u]] : 0;  // valid row: loads need no mask
+                for (int o = 0; o < HC; ++o) sd[o] = ua[o] = 0.f;
+                if (lane == 0)
 #pragma unroll
-                    for (int c = 0; c < CM; ++c) t[u][c] = c < cin ? row[(long long)pz * cin + c] : 0.f;
-                }
+                    for (int c = 0; c < CM; ++c) d3s[b][c] = 0.f;
+                const unsigned long long ab = __ballot(la && ((my_mask >> b) & 1ull));
+                unsigned long long as = ab;
+                while (as) {
+                    int aa[NB];
+                    c2_take<NB>(as, aa);
+                    float t[NB][CM];
+                    c2_load_rows<CM, NB>(fin, cin, n, b, aa, sp, my_mask, my_oj, my_dj, t);
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int z = zz[u];
-                    if (z < 0) break;
-                    if (vb) {
+                    for (int u = 0; u < NB; ++u) {
+                        const int a = aa[u];
+                        if (a < 0) break;
+                        float sc[CM], d1[CM];
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
-                            if (c >= cin) break;
-                            sc[c] += t[u][c];
-                            if (z == lane) d1[c] = t[u][c];
-                            if (z == a) d2[c] = t[u][c];
+                            if (c >= cin) {
+                                sc[c] = d1[c] = 0.f;
+                                continue;
+                            }
+                            sc[c] = wave_total(t[u][c]);
+                            d1[c] = lane_value(t[u][c], b);
                         }
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) sa[c] += t[u][c];
+#pragma unroll
+                        for (int o = 0; o < HC; ++o) {
+                            float U = 0.f, V = 0.f, D = 0.f;
+#pragma unroll
+                            for (int c = 0; c < CM; ++c) {
+                                if (c >= cin) break;
+                                U = fmaf(fmaf(nf, wc[WA][o][c], wc[WB][o][c]), sc[c], U);
+                                U = fmaf(wc[WQ15][o][c], d1[c], U);
+                                V = fmaf(wc[WQ1][o][c], sc[c], V);
+                                D = fmaf(wc[WQ16][o][c], t[u][c], D);
+                            }
+                            ua[o] = lane == a ? U : ua[o];       // entry (a, b): alpha Sc + W15 D1
+                            vacc[o] += lane == a ? V : 0.f;     // q1[a]
+                            sd[o] += lane == a ? D : 0.f;       // entry (b, a): W16 D2[a][b]
+                        }
+                        if (a == b && lane == b)
+#pragma unroll
+                            for (int c = 0; c < CM; ++c) d3s[b][c] = t[u][c];
                     }
                 }
-            }
-        }
-        if (lane < n) {
-            const long long r = (o2 + (long long)a * n + lane) * cin;
+                // row b done: the column part of P[a][b] (lanes a in A_b), the row part of P[b][z], q3[b]
+                float q3[CM];
 #pragma unroll
-            for (int c = 0; c < CM; ++c) {
-                if (c >= cin) break;
-                sv.Sc[r + c] = sc[c];
-                sv.D1[r + c] = d1[c];
-                sv.D2[r + c] = d2[c];
-            }
-        }
+                for (int c = 0; c < CM; ++c) q3[c] = c < cin ? wave_total(sa[c]) : 0.f;
+                const bool in = (ab >> lane) & 1ull;
 #pragma unroll
-        for (int c = 0; c < CM; ++c) {
-            if (c >= cin) break;
-            const float q = wave_sum(sc[c]);           // q1[a] = sum_b Sc[a][b]
-            if (lane == 0) sv.q1[(o1 + a) * cin + c] = q;
-            tq[c] += q;
-            if (lane == a) td3[c] += d1[c];            // T[a][a][a]
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < CM; ++c) {
-        if (c >= cin) break;
-        const float t3 = wave_sum(td3[c]);
-        if (lane == 0) {
-            sred[0][wv][c] = tq[c];
-            sred[1][wv][c] = t3;
-        }
-    }
-
-    // ---- pass B: wave per receptive-field row b, lane z
-    for (int b = wv; b < n; b += 4) {
-        float sa[CM];
-#pragma unroll
-        for (int c = 0; c < CM; ++c) sa[c] = 0.f;
-        // the neighbours a with b in C_a, ascending, in batches of 4 (loads first, then the sums)
-        unsigned long long as = __ballot(lane < n && ((vmask[lane < n ? lane : 0] >> b) & 1ull));
-        while (as) {
-            int aa[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                aa[u] = as ? __ffsll((long long)as) - 1 : -1;
-                as &= as ? as - 1ull : 0ull;
-            }
-            float t[4][CM];
-            bool vz[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int a = aa[u] >= 0 ? aa[u] : 0;
-                const unsigned long long ma = vmask[a];
-                vz[u] = aa[u] >= 0 && lane < n && ((ma >> lane) & 1ull);
-                const float* q;
-                if (level0) {
-                    q = X + (long long)s_j[a] * cin;
-                } else {
-                    const int pb = max(sp[a * n + b], 0), pz = vz[u] ? sp[a * n + lane] : 0;
-                    q = fin + ((long long)s_oj[a] + (long long)pb * s_dj[a] + pz) * cin;
-                }
-#pragma unroll
-                for (int c = 0; c < CM; ++c) t[u][c] = c < cin ? q[c] : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (aa[u] < 0) break;
-                if (vz[u]) {
+                for (int o = 0; o < HC; ++o) {
+                    if (o >= hc) break;
+                    if (in) atomicAdd(&P[(lane * n + b) * HC + o], ua[o]);
+                    float S = sd[o];
 #pragma unroll
                     for (int c = 0; c < CM; ++c) {
                         if (c >= cin) break;
-                        sa[c] += t[u][c];
+                        S = fmaf(nf * wc[WQ2][o][c], sa[c], S);
+                    }
+                    if (la) atomicAdd(&P[(b * n + lane) * HC + o], S);
+                    if (lane == 0) {
+                        float q = 0.f;
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) q = fmaf(wc[WQ3][o][c], q3[c], q);
+                        q3p[b][o] = q;
                     }
                 }
+                if (lane == 0)
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) q3s[b][c] = q3[c];
+            }
+            __syncthreads();
+            if ((int)threadIdx.x < hc) {  // [x = y](W4 tot + W17 d3), sums over b in a fixed order
+                const int o = threadIdx.x;
+                float dg = 0.f;
+                for (int c = 0; c < cin; ++c) {
+                    float tt = 0.f, dd = 0.f;
+                    for (int b = 0; b < n; ++b) {
+                        tt += q3s[b][c];
+                        dd += d3s[b][c];
+                    }
+                    dg = fmaf(wc[WQ4][o][c], tt, dg);
+                    dg = fmaf(wc[WQ17][o][c], dd, dg);
+                }
+                s_diag[o] = dg;
             }
         }
+        if (la)
 #pragma unroll
-        for (int c = 0; c < CM; ++c) {
-            if (c >= cin) break;
-            if (lane < n) sv.Sa[(o2 + (long long)b * n + lane) * cin + c] = sa[c];
-            const float q3 = wave_sum(sa[c]);
-            if (lane == 0) sv.q3[(o1 + b) * cin + c] = q3;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < cin) {
-        const int c = threadIdx.x;
-        float t = 0.f, t3 = 0.f;
-        for (int w = 0; w < 4; ++w) {
-            t += sred[0][w][c];
-            t3 += sred[1][w][c];
-        }
-        sv.tot[(long long)i * cin + c] = t;
-        sv.d3[(long long)i * cin + c] = t3;
-    }
-    __syncthreads();
-    // output: out[x][y][o] = relu(sum_q W_q . block_q[x][y] + b)   (W: h x 18 C, block q at cols q*C..)
-    // the statistics of an entry are read once per channel and feed every output o (weights in LDS)
-    const float nf = (float)n;
-    const int K = 18 * cin;
-    __shared__ float sw[HM * 18 * CM];
-    for (int t = threadIdx.x; t < h * K; t += 256) sw[t] = W[t];
-    __syncthreads();
-    for (int e = threadIdx.x; e < n * n; e += 256) {
-        const int x = e / n, y = e % n;
-        float s[HM];
+            for (int o = 0; o < HC; ++o) qw[wv][lane][o] = vacc[o];
+        __syncthreads();
+        for (int e = threadIdx.x; e < n * n; e += 256) {
+            const int x = e / n, y = e - x * n;
 #pragma unroll
-        for (int o = 0; o < HM; ++o) s[o] = o < h ? bias[o] : 0.f;
-        for (int c = 0; c < cin; ++c) {
-            const float sc = sv.Sc[(o2 + x * n + y) * cin + c];
-            const float sa = sv.Sa[(o2 + x * n + y) * cin + c];
-            float blk[18];
-            blk[0] = nf * sc;
-            blk[1] = sv.q1[(o1 + x) * cin + c];
-            blk[2] = nf * sa;
-            blk[3] = sv.q3[(o1 + x) * cin + c];
-            blk[4] = x == y ? sv.tot[(long long)i * cin + c] : 0.f;
-            blk[5] = sc;
-#pragma unroll
-            for (int q = 6; q < 15; ++q) blk[q] = nf * sc;
-            blk[15] = sv.D1[(o2 + x * n + y) * cin + c];
-            blk[16] = sv.D2[(o2 + y * n + x) * cin + c];
-            blk[17] = x == y ? sv.d3[(long long)i * cin + c] : 0.f;
-#pragma unroll
-            for (int o = 0; o < HM; ++o) {
-                if (o >= h) break;
-                const float* w = sw + o * K;
-#pragma unroll
-                for (int q = 0; q < 18; ++q) s[o] = fmaf(w[q * cin + c], blk[q], s[o]);
+            for (int o = 0; o < HC; ++o) {
+                if (o >= hc) break;
+                float s = bias[o0 + o] + P[e * HC + o];
+                s += (qw[0][x][o] + qw[1][x][o]) + (qw[2][x][o] + qw[3][x][o]);
+                s += q3p[x][o];
+                if (x == y) s += s_diag[o];
+                fout[(o2 + e) * h + o0 + o] = s < 0.f ? 0.f : s;
             }
         }
-#pragma unroll
-        for (int o = 0; o < HM; ++o) {
-            if (o >= h) break;
-            fout[(o2 + e) * h + o] = s[o] < 0.f ? 0.f : s[o];
-        }
+        __syncthreads();
     }
 }
 
@@ -557,26 +682,28 @@ struct C2Grad {
     float* dd3;  // [nodes][C]
 };
 
-// Block per node: dpre = dF * relu'(F); param partials; node-level gradient matrices.
+// Backward node pass of the degrees 65..256 (their forward: k_ccn2_fwd_big, which saves the
+// contraction statistics C2Save): parameter partials from the saved statistics, the gradient
+// matrices of the contraction blocks (C2Grad, this node only) and, at level 0, the per-neighbour
+// sums G[a] for k_ccn2_dx0; the dp format for the gather kernels follows in k_c2_dp_big.
 // One sweep over the n^2 entries per output o for the parameter partials (the 9 distinct
 // contraction blocks x cin accumulate in registers, then one wave-sum + LDS combine each), and one
-// sweep for the input-side gradients (every channel of an entry from one read of dpre).
-// BIG: the instantiation for degrees 65..256 (the level-0 reduction walks 64-lane chunks and
-// multi-word common-neighbour sets, dSa read from L2 instead of an n x n LDS copy).
-template <int CM, int HM, bool BIG = false>
-__global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int* total_nodes,
+// sweep for the input-side gradients (every channel of an entry from one read of dpre); the level-0
+// reduction walks 64-lane chunks and multi-word common-neighbour sets.
+template <int CM, int HM>
+__global__ void __launch_bounds__(256) k_ccn2_bwd_node_big(CcnPlanView v, const int* total_nodes,
                                                        const float* __restrict__ dF, const float* __restrict__ F,
                                                        C2Save sv, int cin, const float* __restrict__ W, int h,
                                                        C2Grad gd, float* __restrict__ ppart,
                                                        float* __restrict__ g0) {
-    constexpr int MAXN = BIG ? CCN_BIGD : CCN_MAXD;
+    constexpr int MAXN = CCN_BIGD;
     __shared__ float sdq1[MAXN * CM], sdq3[MAXN * CM], sdtot[CM], sdd3[CM];
     __shared__ float red[4][10 * CM];
     __shared__ float sw[HM * 18 * CM];
     const int i = blockIdx.x;
     if (i >= *total_nodes) return;
     const int n = v.deg[i];
-    if ((BIG ? (n <= CCN_MAXD || n > CCN_BIGD) : n > CCN_MAXD) || cin > CM || h > HM) return;
+    if (n <= CCN_MAXD || n > CCN_BIGD || cin > CM || h > HM) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long o2 = v.off2[i], o1 = v.off1[i];
     const float nf = (float)n;
@@ -686,76 +813,42 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_node(CcnPlanView v, const int*
     // every j gathering them:  G[a] = m_a sum_{b in C_a} dSc[a][b] + sum_{b,z in C_a} dSa[b][z]
     //   + sum_{b in C_a} dD1[a][b] + [a in C_a] (sum_{b in C_a} dD2[a][b] + dd3),  C_a = {x: pos_a(x) >= 0}
     // dSa of one channel is staged in LDS so the masked row sums read LDS, not scattered HBM rows
-    if constexpr (BIG) {
-        __shared__ unsigned long long vmb[CCN_BIGD][CCN_BW];
-        __shared__ int smc[CCN_BIGD];
-        const int nw = (n + 63) >> 6;
-        __syncthreads();
-        for (int a = wv; a < n; a += 4) {
-            int cnt = 0;
-            for (int w = 0; w < nw; ++w) {
-                const int x = w * 64 + lane;
-                const unsigned long long m = __ballot(x < n && v.pos[o2 + (long long)a * n + x] >= 0);
-                if (lane == 0) vmb[a][w] = m;
-                cnt += __popcll(m);
-            }
-            if (lane == 0) smc[a] = cnt;
-        }
-        __syncthreads();
-        for (int c = 0; c < cin; ++c)
-            for (int a = wv; a < n; a += 4) {
-                const bool va = mbit(vmb[a], a);
-                const float mf = (float)smc[a];
-                float t = 0.f;
-                for (int b = lane; b < n; b += 64) {
-                    if (!mbit(vmb[a], b)) continue;
-                    const long long rab = (o2 + (long long)a * n + b) * cin + c;
-                    t += mf * gd.dSc[rab] + gd.dD1[rab] + (va ? gd.dD2[rab] : 0.f);
-                    for (int w = 0; w < nw; ++w) {
-                        unsigned long long zs = vmb[a][w];
-                        while (zs) {
-                            const int z = w * 64 + __ffsll((long long)zs) - 1;
-                            zs &= zs - 1ull;
-                            t += gd.dSa[(o2 + (long long)b * n + z) * cin + c];
-                        }
-                    }
-                }
-                t = wave_sum(t);
-                if (lane == 0) g0[(o1 + a) * cin + c] = t + (va ? sdd3[c] : 0.f);
-            }
-        return;
-    }
-    __shared__ unsigned long long vm[CCN_MAXD];
-    __shared__ float sa_l[CCN_MAXD * CCN_MAXD];
+    __shared__ unsigned long long vmb[CCN_BIGD][CCN_BW];
+    __shared__ int smc[CCN_BIGD];
+    const int nw = (n + 63) >> 6;
     __syncthreads();
     for (int a = wv; a < n; a += 4) {
-        const unsigned long long m = __ballot(lane < n && v.pos[o2 + a * n + lane] >= 0);
-        if (lane == 0) vm[a] = m;
+        int cnt = 0;
+        for (int w = 0; w < nw; ++w) {
+            const int x = w * 64 + lane;
+            const unsigned long long m = __ballot(x < n && v.pos[o2 + (long long)a * n + x] >= 0);
+            if (lane == 0) vmb[a][w] = m;
+            cnt += __popcll(m);
+        }
+        if (lane == 0) smc[a] = cnt;
     }
-    for (int c = 0; c < cin; ++c) {
-        __syncthreads();
-        for (int e = threadIdx.x; e < n * n; e += 256) sa_l[e] = gd.dSa[(o2 + e) * cin + c];
-        __syncthreads();
+    __syncthreads();
+    for (int c = 0; c < cin; ++c)
         for (int a = wv; a < n; a += 4) {
-            const unsigned long long ma = vm[a];
-            const bool vb = lane < n && ((ma >> lane) & 1ull);
-            const bool va = (ma >> a) & 1ull;
-            const float mf = (float)__popcll(ma);
+            const bool va = mbit(vmb[a], a);
+            const float mf = (float)smc[a];
             float t = 0.f;
-            if (vb) {
-                const long long rab = (o2 + (long long)a * n + lane) * cin + c;
-                t = mf * gd.dSc[rab] + gd.dD1[rab] + (va ? gd.dD2[rab] : 0.f);
-                unsigned long long zs = ma;
-                while (zs) {
-                    const int z = __ffsll((long long)zs) - 1;
-                    zs &= zs - 1ull;
-                    t += sa_l[lane * n + z];
+            for (int b = lane; b < n; b += 64) {
+                if (!mbit(vmb[a], b)) continue;
+                const long long rab = (o2 + (long long)a * n + b) * cin + c;
+                t += mf * gd.dSc[rab] + gd.dD1[rab] + (va ? gd.dD2[rab] : 0.f);
+                for (int w = 0; w < nw; ++w) {
+                    unsigned long long zs = vmb[a][w];
+                    while (zs) {
+                        const int z = w * 64 + __ffsll((long long)zs) - 1;
+                        zs &= zs - 1ull;
+                        t += gd.dSa[(o2 + (long long)b * n + z) * cin + c];
+                    }
                 }
             }
             t = wave_sum(t);
             if (lane == 0) g0[(o1 + a) * cin + c] = t + (va ? sdd3[c] : 0.f);
         }
-    }
 }
 
 // dX[j] (level 0) = sum over neighbours i of G_i[a_j] (k_ccn2_bwd_node) + d_j^2 dsum0.
@@ -770,49 +863,422 @@ __global__ void __launch_bounds__(256) k_ccn2_dx0(CcnPlanView v, const int* tota
     const long long o2 = v.off2[j];
     const int* nj = v.nbr + (long long)j * v.nmax;
     const int sj = v.selfpos[j];
-    for (int c = 0; c < cin; ++c) {
-        float t = 0.f;
-        for (int x = lane; x < n; x += 64) {  // one chunk for d <= 64
-            const int i = nj[x];
-            const int aj = v.pos[o2 + (long long)x * n + sj];  // position of j in N(i)
-            t += g0[((long long)v.off1[i] + aj) * cin + c];
-        }
-        t = wave_sum(t);
+    const int g = v.graph[j];
+    float t[C2_CMAX_WIDE];
+#pragma unroll
+    for (int c = 0; c < C2_CMAX_WIDE; ++c) t[c] = 0.f;
+    for (int x = lane; x < n; x += 64) {  // one chunk for d <= 64; the indices once for every channel
+        const int i = nj[x];
+        const int aj = v.pos[o2 + (long long)x * n + sj];  // position of j in N(i)
+        const float* gi = g0 + ((long long)v.off1[i] + aj) * cin;
+#pragma unroll
+        for (int c = 0; c < C2_CMAX_WIDE; ++c)
+            if (c < cin) t[c] += gi[c];
+    }
+#pragma unroll
+    for (int c = 0; c < C2_CMAX_WIDE; ++c) {
+        if (c >= cin) break;
+        const float s = wave_sum(t[c]);
         if (lane == 0) {
-            const float rd = dsum ? dsum[(long long)v.graph[j] * dsum_ld + c] : 0.f;
-            dout[(long long)j * cin + c] = t + (float)(n * n) * rd;
+            const float rd = dsum ? dsum[(long long)g * dsum_ld + c] : 0.f;
+            dout[(long long)j * cin + c] = s + (float)(n * n) * rd;
         }
     }
 }
 
-// Block per node j: dF_prev[j][u][w] = sum over neighbours i of the gradient of the entry of T_i that
-// read F_j[u][w] (+ readout); level 0: dX[j] = sum over (u, w) (+ d_j^2 dsum0).  As in the forward,
-// F_j[u][w] is read by T_i only where u, w are both common neighbours of i and j: wave per row u,
-// lane w, walking the neighbours a with u in C_a (wave-uniform), lanes gathering where w in C_a.
-template <int C, int NB>
-__global__ void __launch_bounds__(256) k_ccn2_bwd_gather(CcnPlanView v, const int* total_nodes, C2Grad gd, int cin,
-                                                         const float* __restrict__ dsum, int dsum_ld, int dsum_off,
-                                                         int level0, float* __restrict__ dout) {
-    // C: channel bound of this instantiation (cin <= C); NB: neighbours gathered per batch
-    __shared__ int sp[CCN_MAXD * CCN_MAXD];
-    __shared__ unsigned long long vmask[CCN_MAXD];
-    __shared__ float red[4][C];
-    __shared__ int s_i[CCN_MAXD], s_di[CCN_MAXD], s_oi[CCN_MAXD], s_aj[CCN_MAXD];  // neighbour a of j
+// Backward of one CCN-2D level for the nodes of degree <= 64, block per node i:
+//   dp = dF * relu'(F_out) (written back in place of dF), rdp[x] = sum_y dp[x][y], tr = sum_x dp[x][x]
+//   -- the "dp format" the gather kernels rebuild dT from (k_c2_gather);
+//   parameter partials  dW_q[o][c] = sum_xy dp[x][y][o] block_q[x][y][c], db[o] = sum dp, with
+//     P0 = sum dp Sc, P1 = sum_x rdp[x] q1[x], P2 = sum dp Sa, P3 = sum_x rdp[x] q3[x],
+//     P15 = sum dp D1, P16 = sum dp[x][y] D2[y][x], tot, d3:
+//     dW_{0,6..14} = n P0, dW_5 = P0, dW_1 = P1, dW_2 = n P2, dW_3 = P3, dW_4 = tr tot, dW_15 = P15,
+//     dW_16 = P16, dW_17 = tr d3.
+// Level >= 1: the forward's row walk again (same loads), every sum lane-level (dp[a][b] . t summed
+// over the walk, wave totals once at the end).  Level 0 (T = X[j_a] on C_a) in closed form from the
+// per-neighbour masked sums R1[a] = sum_{b in C_a} dp[a][b], R2[a] = sum_{b in C_a} dp[b][a],
+// R3[a] = sum_{b in C_a} rdp[b], BS[a] = sum_{b,z in C_a} dp[b][z], which also give dX's per-node
+// terms  G[a] = sum_{b,z in C_a} dT[a][b][z]  (k_ccn2_dx0 adds them up per input node).
+// dW_q[o][c] of the 18 contraction blocks from the distinct sums (see k_c2_bwd)
+__device__ __forceinline__ void c2_write_partials(float* row, int cin, int c, float nf, float p0, float p1, float p2,
+                                                  float p3, float p15, float p16, float p4, float p17) {
+    row[0 * cin + c] = nf * p0;
+    row[1 * cin + c] = p1;
+    row[2 * cin + c] = nf * p2;
+    row[3 * cin + c] = p3;
+    row[4 * cin + c] = p4;
+    row[5 * cin + c] = p0;
+    for (int q = 6; q < 15; ++q) row[q * cin + c] = nf * p0;
+    row[15 * cin + c] = p15;
+    row[16 * cin + c] = p16;
+    row[17 * cin + c] = p17;
+}
+
+constexpr int C2_NACC = 6;  // P0, P1, P2, P3, P15, P16
+template <int CM, int HC, int NB, bool L0>
+__global__ void __launch_bounds__(256) k_c2_bwd(CcnPlanView v, const int* total_nodes, float* __restrict__ dF,
+                                                const float* __restrict__ F, const float* __restrict__ fin,
+                                                const float* __restrict__ X, int cin,
+                                                const float* __restrict__ W, int h, int ncap,
+                                                float* __restrict__ rdp_g, float* __restrict__ trd_g,
+                                                float* __restrict__ ppart, float* __restrict__ g0) {
+    extern __shared__ float c2_dyn[];
+    __shared__ unsigned long long vmask[C2_NCAP];
+    __shared__ int s_oj[C2_NCAP], s_dj[C2_NCAP];
+    __shared__ float s_x[C2_NCAP][CM];
+    __shared__ float wc[NWC][HC][CM];
+    __shared__ float rdpL[C2_NCAP][HC];
+    __shared__ float trL[HC];
+    __shared__ float red[4][C2_NACC][HC][CM];
+    __shared__ float redt[4][2][CM];  // tot, d3
+    __shared__ float redb[4][HC];
+    __shared__ float gs[C2_NCAP][CM];
+    __shared__ float rs[C2_NCAP][4][HC];  // level 0: R1, R2, R3, BS per neighbour
+    const int i = blockIdx.x;
+    if (i >= *total_nodes) return;
+    const int n = v.deg[i];
+    if (n > C2_NCAP || n > ncap || cin > CM) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float* dpL = c2_dyn;
+    short* sp = reinterpret_cast<short*>(c2_dyn + ncap * ncap * HC);
+    c2_prologue<CM>(v, i, n, L0 ? 1 : 0, X, cin, sp, vmask, s_oj, s_dj, s_x);
+    const long long o2 = v.off2[i], o1 = v.off1[i];
+    const bool la = lane < n;
+    const unsigned long long my_mask = la ? vmask[lane] : 0ull;
+    const int my_oj = la ? s_oj[lane] : 0, my_dj = la ? s_dj[lane] : 0;
+    const float nf = (float)n;
+    const int K = 18 * cin;
+    float* pp = ppart + (long long)i * (h * K + h);
+    for (int e = threadIdx.x; e < C2_NCAP * CM; e += 256) (&gs[0][0])[e] = 0.f;
+    for (int o0 = 0; o0 < h; o0 += HC) {
+        const int hc = min(HC, h - o0);
+        c2_weights<HC, CM>(wc, W, cin, o0, hc);
+        float sb[HC];
+#pragma unroll
+        for (int o = 0; o < HC; ++o) sb[o] = 0.f;
+        for (int e = threadIdx.x; e < n * n; e += 256) {
+#pragma unroll
+            for (int o = 0; o < HC; ++o) {
+                float d = 0.f;
+                if (o < hc) {
+                    const long long r = (o2 + e) * h + o0 + o;
+                    d = F[r] > 0.f ? dF[r] : 0.f;
+                    dF[r] = d;
+                }
+                dpL[e * HC + o] = d;
+                sb[o] += d;
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < HC; ++o) {
+            const float t = wave_total(sb[o]);
+            if (lane == 0) redb[wv][o] = t;
+        }
+        __syncthreads();
+        // row sums and trace of dp
+        for (int x = wv; x < n; x += 4)
+#pragma unroll
+            for (int o = 0; o < HC; ++o) {
+                const float r = wave_total(lane < n ? dpL[(x * n + lane) * HC + o] : 0.f);
+                if (lane == 0) {
+                    rdpL[x][o] = r;
+                    if (o < hc) rdp_g[(o1 + x) * h + o0 + o] = r;
+                }
+            }
+        if (wv == 0)
+#pragma unroll
+            for (int o = 0; o < HC; ++o) {
+                const float r = wave_total(lane < n ? dpL[(lane * n + lane) * HC + o] : 0.f);
+                if (lane == 0) {
+                    trL[o] = r;
+                    if (o < hc) trd_g[(long long)i * h + o0 + o] = r;
+                }
+            }
+        __syncthreads();
+        if constexpr (L0) {
+            // per neighbour a (wave per a): the masked sums of dp the closed forms need
+            for (int a = wv; a < n; a += 4) {
+                const unsigned long long ma = vmask[a];
+                const bool vb = lane < n && ((ma >> lane) & 1ull);
+#pragma unroll
+                for (int o = 0; o < HC; ++o) {
+                    const float r1 = wave_total(vb ? dpL[(a * n + lane) * HC + o] : 0.f);
+                    const float r2 = wave_total(vb ? dpL[(lane * n + a) * HC + o] : 0.f);
+                    const float r3 = wave_total(vb ? rdpL[lane][o] : 0.f);
+                    float s = 0.f;
+                    unsigned long long zs = ma;
+                    while (zs) {
+                        const int z = __ffsll((long long)zs) - 1;
+                        zs &= zs - 1ull;
+                        s += vb ? dpL[(lane * n + z) * HC + o] : 0.f;
+                    }
+                    const float bs = wave_total(s);
+                    if (lane == 0) {
+                        rs[a][0][o] = r1;
+                        rs[a][1][o] = r2;
+                        rs[a][2][o] = r3;
+                        rs[a][3][o] = bs;
+                    }
+                }
+            }
+            __syncthreads();
+            // parameter partials: (o, c) pairs over the waves, lanes over the neighbours a, wave totals
+            for (int p = wv; p < hc * cin; p += 4) {
+                const int o = p / cin, c = p % cin;
+                const float mf = (float)__popcll(my_mask);
+                const bool va = la && ((my_mask >> lane) & 1ull);
+                const float x = la ? s_x[lane][c] : 0.f;
+                const float r1 = la ? rs[lane][0][o] : 0.f, r2 = la ? rs[lane][1][o] : 0.f;
+                const float r3 = la ? rs[lane][2][o] : 0.f, bs = la ? rs[lane][3][o] : 0.f;
+                const float ra = la ? rdpL[lane][o] : 0.f;
+                const float s0 = wave_total(mf * x * r1), s1 = wave_total(mf * mf * x * ra);
+                const float s2 = wave_total(x * bs), s3 = wave_total(mf * x * r3);
+                const float s15 = wave_total(x * r1), s16 = wave_total(va ? x * r2 : 0.f);
+                const float tt = wave_total(mf * mf * x), dd = wave_total(va ? x : 0.f);
+                if (lane == 0)
+                    c2_write_partials(pp + (long long)(o0 + o) * K, cin, c, nf, s0, s1, s2, s3, s15, s16, trL[o] * tt,
+                                      trL[o] * dd);
+            }
+            // G[a] = m_a sum dSc[a][.] + sum dSa + sum dD1[a][.] + [a in C_a](sum dD2[a][.] + dd3), this chunk's o
+            for (int t = threadIdx.x; t < n * cin; t += 256) {
+                const int a = t / cin, c = t % cin;
+                const unsigned long long ma = vmask[a];
+                const float mf = (float)__popcll(ma);
+                const bool va = (ma >> a) & 1ull;
+                float g = 0.f;
+                for (int o = 0; o < hc; ++o) {
+                    const float r1 = rs[a][0][o], r2 = rs[a][1][o], r3 = rs[a][2][o], bs = rs[a][3][o];
+                    float s = mf * fmaf(fmaf(nf, wc[WA][o][c], wc[WB][o][c]), r1, mf * wc[WQ1][o][c] * rdpL[a][o]);
+                    s = fmaf(nf * wc[WQ2][o][c], bs, s);
+                    s = fmaf(mf * wc[WQ3][o][c], r3, s);
+                    s = fmaf(mf * mf * wc[WQ4][o][c], trL[o], s);
+                    s = fmaf(wc[WQ15][o][c], r1, s);
+                    if (va) s = fmaf(wc[WQ16][o][c], r2, fmaf(wc[WQ17][o][c], trL[o], s));
+                    g += s;
+                }
+                gs[a][c] += g;
+            }
+        } else {
+            float acc[C2_NACC][HC][CM], tot[CM], d3[CM];
+#pragma unroll
+            for (int k = 0; k < C2_NACC; ++k)
+#pragma unroll
+                for (int o = 0; o < HC; ++o)
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) acc[k][o][c] = 0.f;
+#pragma unroll
+            for (int c = 0; c < CM; ++c) tot[c] = d3[c] = 0.f;
+            for (int b = wv; b < n; b += 4) {
+                float sa[CM];
+#pragma unroll
+                for (int c = 0; c < CM; ++c) sa[c] = 0.f;
+                unsigned long long as = __ballot(la && ((my_mask >> b) & 1ull));
+                while (as) {
+                    int aa[NB];
+                    c2_take<NB>(as, aa);
+                    float t[NB][CM];
+                    c2_load_rows<CM, NB>(fin, cin, n, b, aa, sp, my_mask, my_oj, my_dj, t);
+#pragma unroll
+                    for (int u = 0; u < NB; ++u) {
+                        const int a = aa[u];
+                        if (a < 0) break;
+#pragma unroll
+                        for (int o = 0; o < HC; ++o) {
+                            const float dab = dpL[(a * n + b) * HC + o], dba = dpL[(b * n + a) * HC + o];
+                            const float ra = rdpL[a][o];
+                            const float d15 = lane == b ? dab : 0.f, d16 = lane == a ? dba : 0.f;
+#pragma unroll
+                            for (int c = 0; c < CM; ++c) {
+                                acc[0][o][c] = fmaf(dab, t[u][c], acc[0][o][c]);
+                                acc[1][o][c] = fmaf(ra, t[u][c], acc[1][o][c]);
+                                acc[4][o][c] = fmaf(d15, t[u][c], acc[4][o][c]);
+                                acc[5][o][c] = fmaf(d16, t[u][c], acc[5][o][c]);
+                            }
+                        }
+                        if (a == b && lane == b)
+#pragma unroll
+                            for (int c = 0; c < CM; ++c) d3[c] += t[u][c];
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) sa[c] += t[u][c];
+                    }
+                }
+#pragma unroll
+                for (int o = 0; o < HC; ++o) {
+                    const float dbz = lane < n ? dpL[(b * n + lane) * HC + o] : 0.f;
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) acc[2][o][c] = fmaf(dbz, sa[c], acc[2][o][c]);
+                }
+#pragma unroll
+                for (int c = 0; c < CM; ++c) {
+                    if (c >= cin) break;
+                    const float q3 = wave_total(sa[c]);  // uniform: P3 and tot kept in lane 0 only
+                    if (lane == 0) {
+#pragma unroll
+                        for (int o = 0; o < HC; ++o) acc[3][o][c] = fmaf(rdpL[b][o], q3, acc[3][o][c]);
+                        tot[c] += q3;
+                    }
+                }
+            }
+            // lane-level sums -> wave totals (P3 and tot are lane 0's)
+#pragma unroll
+            for (int k = 0; k < C2_NACC; ++k) {
+                if (k == 3) continue;
+#pragma unroll
+                for (int o = 0; o < HC; ++o)
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) {
+                        if (c >= cin) break;
+                        acc[k][o][c] = wave_total(acc[k][o][c]);
+                    }
+            }
+#pragma unroll
+            for (int c = 0; c < CM; ++c) {
+                if (c >= cin) break;
+                d3[c] = wave_total(d3[c]);
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int k = 0; k < C2_NACC; ++k)
+#pragma unroll
+                    for (int o = 0; o < HC; ++o)
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) red[wv][k][o][c] = acc[k][o][c];
+#pragma unroll
+                for (int c = 0; c < CM; ++c) {
+                    redt[wv][0][c] = tot[c];
+                    redt[wv][1][c] = d3[c];
+                }
+            }
+            __syncthreads();
+            for (int t = threadIdx.x; t < hc * cin; t += 256) {
+                const int o = t / cin, c = t % cin;
+                float s[C2_NACC];
+#pragma unroll
+                for (int k = 0; k < C2_NACC; ++k)
+                    s[k] = (red[0][k][o][c] + red[1][k][o][c]) + (red[2][k][o][c] + red[3][k][o][c]);
+                const float tt = (redt[0][0][c] + redt[1][0][c]) + (redt[2][0][c] + redt[3][0][c]);
+                const float dd = (redt[0][1][c] + redt[1][1][c]) + (redt[2][1][c] + redt[3][1][c]);
+                c2_write_partials(pp + (long long)(o0 + o) * K, cin, c, nf, s[0], s[1], s[2], s[3], s[4], s[5],
+                                  trL[o] * tt, trL[o] * dd);
+            }
+        }
+        if ((int)threadIdx.x < hc)
+            pp[(long long)h * K + o0 + threadIdx.x] = (redb[0][threadIdx.x] + redb[1][threadIdx.x]) +
+                                                      (redb[2][threadIdx.x] + redb[3][threadIdx.x]);
+        __syncthreads();
+    }
+    if (L0 && g0) {
+        __syncthreads();
+        for (int t = threadIdx.x; t < n * cin; t += 256) g0[(o1 + t / cin) * cin + t % cin] = gs[t / cin][t % cin];
+    }
+}
+
+// Gather of one CCN-2D level's input gradient from the dp format (no atomics): node j collects, for
+// every neighbour i = i_a with u, w in C_a, the gradient of the entry of T_i that read F_j[u][w]:
+//   dF_{l-1}[j][u][w] = sum_a dT_i[aj][b][z] (+ readout),  b = p_a(u), z = p_a(w), aj = position of j in N(i),
+//   dT[a][b][z] = dSc[a][b] + dSa[b][z] + [z = b] dD1[a][b] + [z = a] dD2[a][b] + [a = b = z] dd3,
+//   dSc[a][b] = (n_i A + W5)^T dp[a][b] + W1^T rdp[a],   dSa[b][z] = n_i W2^T dp[b][z] + W3^T rdp[b] + W4^T tr,
+//   dD1[a][b] = W15^T dp[a][b],   dD2[a][b] = W16^T dp[b][a],   dd3 = W17^T tr      (A = W0 + W6 + ... + W14).
+// Per (u, a) the wave-uniform part is five h-vectors of node i, the lane part one row piece dp[b][z].
+// The level's input has cin = h channels (levels >= 1 only: level 0 goes through k_ccn2_dx0).
+template <int H>
+__device__ __forceinline__ void c2_dT_weights(float (*wc)[H][H], const float* __restrict__ W, int h) {
+    const int K = 18 * h;
+    for (int t = threadIdx.x; t < H * H; t += blockDim.x) {
+        const int o = t / H, c = t % H;
+        const bool ok = o < h && c < h;
+        const float* w = W + (long long)(ok ? o : 0) * K;
+        float a = 0.f;
+        if (ok) {
+            a = w[c];
+            for (int q = 6; q < 15; ++q) a += w[q * h + c];
+        }
+        wc[WA][o][c] = a;
+        wc[WB][o][c] = ok ? w[5 * h + c] : 0.f;
+        wc[WQ1][o][c] = ok ? w[1 * h + c] : 0.f;
+        wc[WQ2][o][c] = ok ? w[2 * h + c] : 0.f;
+        wc[WQ3][o][c] = ok ? w[3 * h + c] : 0.f;
+        wc[WQ4][o][c] = ok ? w[4 * h + c] : 0.f;
+        wc[WQ15][o][c] = ok ? w[15 * h + c] : 0.f;
+        wc[WQ16][o][c] = ok ? w[16 * h + c] : 0.f;
+        wc[WQ17][o][c] = ok ? w[17 * h + c] : 0.f;
+    }
+}
+
+struct C2Dp {
+    const float* dp;   // [sum d^2][h]
+    const float* rdp;  // [sum d][h]
+    const float* trd;  // [nodes][h]
+};
+
+// loads of one (i, a) pair: ld[0] dp[aj][b], ld[1] dp[b][aj], ld[2] rdp[aj], ld[3] rdp[b], ld[4] tr, ld[5] dp[b][z]
+template <int H>
+__device__ __forceinline__ void c2_dT_load(const C2Dp& g, int h, long long oi, long long o1i, int i, int di, int aj,
+                                           int b, int z, float (&ld)[6][H]) {
+    const float* pab = g.dp + (oi + (long long)aj * di + b) * h;
+    const float* pba = g.dp + (oi + (long long)b * di + aj) * h;
+    const float* pbz = g.dp + (oi + (long long)b * di + z) * h;
+#pragma unroll
+    for (int o = 0; o < H; ++o) {
+        const bool ok = o < h;
+        ld[0][o] = ok ? pab[o] : 0.f;
+        ld[1][o] = ok ? pba[o] : 0.f;
+        ld[2][o] = ok ? g.rdp[(o1i + aj) * h + o] : 0.f;
+        ld[3][o] = ok ? g.rdp[(o1i + b) * h + o] : 0.f;
+        ld[4][o] = ok ? g.trd[(long long)i * h + o] : 0.f;
+        ld[5][o] = ok ? pbz[o] : 0.f;
+    }
+}
+
+template <int H>
+__device__ __forceinline__ void c2_dT_add(const float (*wc)[H][H], const float (&ld)[6][H], int h, float nfi, int aj,
+                                          int b, int z, float (&acc)[H]) {
+    const bool e1 = z == b, e2 = z == aj, e3 = aj == b && b == z;
+#pragma unroll
+    for (int c = 0; c < H; ++c) {
+        if (c >= h) break;
+        float s = 0.f;
+#pragma unroll
+        for (int o = 0; o < H; ++o) {
+            if (o >= h) break;
+            s = fmaf(fmaf(nfi, wc[WA][o][c], wc[WB][o][c]), ld[0][o], s);
+            s = fmaf(wc[WQ1][o][c], ld[2][o], s);
+            s = fmaf(wc[WQ3][o][c], ld[3][o], s);
+            s = fmaf(wc[WQ4][o][c], ld[4][o], s);
+            s = fmaf(nfi * wc[WQ2][o][c], ld[5][o], s);
+            if (e1) s = fmaf(wc[WQ15][o][c], ld[0][o], s);
+            if (e2) s = fmaf(wc[WQ16][o][c], ld[1][o], s);
+            if (e3) s = fmaf(wc[WQ17][o][c], ld[4][o], s);
+        }
+        acc[c] += s;
+    }
+}
+
+template <int H, int NB>
+__global__ void __launch_bounds__(256) k_c2_gather(CcnPlanView v, const int* total_nodes, C2Dp g,
+                                                   const float* __restrict__ W, int h, const float* __restrict__ dsum,
+                                                   int dsum_ld, int dsum_off, float* __restrict__ dout) {
+    __shared__ short sp[C2_NCAP * C2_NCAP];
+    __shared__ unsigned long long vmask[C2_NCAP];
+    __shared__ int s_i[C2_NCAP], s_di[C2_NCAP], s_oi[C2_NCAP], s_o1[C2_NCAP], s_aj[C2_NCAP];
+    __shared__ float wc[NWC][H][H];
     const int j = blockIdx.x;
     if (j >= *total_nodes) return;
     const int n = v.deg[j];
-    if (n > CCN_MAXD || cin > C) return;
+    if (n > C2_NCAP || h > H) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long o2 = v.off2[j];
     const int* nj = v.nbr + (long long)j * v.nmax;
     const int sj = v.selfpos[j];
-    const int g = v.graph[j];
-    for (int e = threadIdx.x; e < n * n; e += 256) sp[e] = v.pos[o2 + e];
-    if (threadIdx.x < n) {
+    const int gr = v.graph[j];
+    c2_dT_weights<H>(wc, W, h);
+    for (int e = threadIdx.x; e < n * n; e += 256) sp[e] = (short)v.pos[o2 + e];
+    if ((int)threadIdx.x < n) {
         const int i = nj[threadIdx.x];
         s_i[threadIdx.x] = i;
         s_di[threadIdx.x] = v.deg[i];
         s_oi[threadIdx.x] = v.off2[i];
+        s_o1[threadIdx.x] = v.off1[i];
     }
     __syncthreads();
     for (int a = wv; a < n; a += 4) {
@@ -823,88 +1289,87 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_gather(CcnPlanView v, const in
         }
     }
     __syncthreads();
-    float rd[C], part[C];
+    float rd[H];
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-        rd[c] = (dsum && c < cin) ? dsum[(long long)g * dsum_ld + dsum_off + c] : 0.f;
-        part[c] = 0.f;
-    }
+    for (int c = 0; c < H; ++c) rd[c] = (dsum && c < h) ? dsum[(long long)gr * dsum_ld + dsum_off + c] : 0.f;
+    // lane a holds neighbour i_a's mask, node, degree, offsets and the position of j in N(i_a)
+    const bool la = lane < n;
+    const unsigned long long my_mask = la ? vmask[lane] : 0ull;
+    const int my_i = la ? s_i[lane] : 0, my_di = la ? s_di[lane] : 0, my_oi = la ? s_oi[lane] : 0;
+    const int my_o1 = la ? s_o1[lane] : 0, my_aj = la ? s_aj[lane] : 0;
     for (int u = wv; u < n; u += 4) {
-        float acc[C];
+        float acc[H];
 #pragma unroll
-        for (int c = 0; c < C; ++c) acc[c] = 0.f;
-        // the neighbours a with u in C_a, ascending, NB at a time: every load of a batch is in flight
-        // before the sums (the per-a walk paid ~3 dependent memory latencies per a: 2.2 -> 0.7 ms per
-        // launch at config 5)
-        unsigned long long as = __ballot(lane < n && ((vmask[lane < n ? lane : 0] >> u) & 1ull));
+        for (int c = 0; c < H; ++c) acc[c] = 0.f;
+        // the neighbours a with u in C_a, ascending, NB at a time (all loads of a batch in flight)
+        unsigned long long as = __ballot(la && ((my_mask >> u) & 1ull));
         while (as) {
             int aa[NB];
-#pragma unroll
-            for (int q = 0; q < NB; ++q) {
-                aa[q] = as ? __ffsll((long long)as) - 1 : -1;
-                as &= as ? as - 1ull : 0ull;
-            }
-            float tsc[NB][C], tsa[NB][C], td1[NB][C], td2[NB][C], td3[NB][C];
-            int zb[NB], zz[NB], zaj[NB];
+            c2_take<NB>(as, aa);
+            float ld[NB][6][H];
+            int zb[NB], zz[NB], zd[NB], zj[NB];
             bool vz[NB];
 #pragma unroll
             for (int q = 0; q < NB; ++q) {
                 const int a = aa[q] >= 0 ? aa[q] : 0;
-                vz[q] = aa[q] >= 0 && lane < n && ((vmask[a] >> lane) & 1ull);
-                const int b = max(sp[a * n + u], 0), z = vz[q] ? sp[a * n + lane] : 0;
-                const int aj = s_aj[a], di = s_di[a], i = s_i[a];
-                const long long oi = s_oi[a];
-                const long long rab = (oi + (long long)aj * di + b) * cin, rbz = (oi + (long long)b * di + z) * cin;
-                zb[q] = b;
-                zz[q] = z;
-                zaj[q] = aj;
-#pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    const bool ok = c < cin;
-                    tsc[q][c] = ok ? gd.dSc[rab + c] : 0.f;
-                    tsa[q][c] = ok ? gd.dSa[rbz + c] : 0.f;
-                    td1[q][c] = ok ? gd.dD1[rab + c] : 0.f;
-                    td2[q][c] = ok ? gd.dD2[rab + c] : 0.f;
-                    td3[q][c] = ok ? gd.dd3[(long long)i * cin + c] : 0.f;
-                }
+                vz[q] = aa[q] >= 0 && ((lane_value_u64(my_mask, a) >> lane) & 1ull);
+                zb[q] = uniform(max((int)sp[a * n + u], 0));
+                zz[q] = vz[q] ? (int)sp[a * n + lane] : 0;
+                zd[q] = lane_value_i(my_di, a);
+                zj[q] = lane_value_i(my_aj, a);
+                c2_dT_load<H>(g, h, lane_value_i(my_oi, a), lane_value_i(my_o1, a), lane_value_i(my_i, a), zd[q],
+                              zj[q], zb[q], zz[q], ld[q]);
             }
 #pragma unroll
             for (int q = 0; q < NB; ++q) {
                 if (aa[q] < 0) break;
                 if (!vz[q]) continue;
-                const int b = zb[q], z = zz[q], aj = zaj[q];
-#pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    if (c >= cin) break;
-                    float t = tsc[q][c] + tsa[q][c];
-                    if (z == b) t += td1[q][c];
-                    if (z == aj) t += td2[q][c];
-                    if (aj == b && b == z) t += td3[q][c];
-                    acc[c] += t;
-                }
+                c2_dT_add<H>(wc, ld[q], h, (float)zd[q], zj[q], zb[q], zz[q], acc);
             }
         }
+        if (lane < n)
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-            if (c >= cin) break;
-            if (level0) part[c] += acc[c];
-            else if (lane < n) dout[(o2 + (long long)u * n + lane) * cin + c] = acc[c] + rd[c];
-        }
-    }
-    if (level0) {
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            if (c >= cin) break;
-            const float t = wave_sum(part[c]);
-            if (lane == 0) red[wv][c] = t;
-        }
-        __syncthreads();
-        if (threadIdx.x < cin) {
-            const int c = threadIdx.x;
-            dout[(long long)j * cin + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + (float)(n * n) * rd[c];
-        }
+            for (int c = 0; c < H; ++c) {
+                if (c >= h) break;
+                dout[(o2 + (long long)u * n + lane) * h + c] = acc[c] + rd[c];
+            }
     }
 }
+
+// dp format for the nodes of degree 65..256 (their parameter partials and level-0 terms come from
+// k_ccn2_bwd_node_big, which reads the raw dF): dp in place, row sums, trace
+__global__ void __launch_bounds__(256) k_c2_dp_big(CcnPlanView v, const int* total_nodes, float* __restrict__ dF,
+                                                   const float* __restrict__ F, int h, float* __restrict__ rdp_g,
+                                                   float* __restrict__ trd_g) {
+    const int i = blockIdx.x;
+    if (i >= *total_nodes) return;
+    const int n = v.deg[i];
+    if (n <= C2_NCAP || n > CCN_BIGD) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long o2 = v.off2[i], o1 = v.off1[i];
+    __shared__ float trp[4];
+    for (int o = 0; o < h; ++o) {
+        float tr = 0.f;
+        for (int x = wv; x < n; x += 4) {
+            float s = 0.f;
+            for (int y = lane; y < n; y += 64) {
+                const long long r = (o2 + (long long)x * n + y) * h + o;
+                const float d = F[r] > 0.f ? dF[r] : 0.f;
+                dF[r] = d;
+                s += d;
+                if (y == x) tr += d;
+            }
+            s = wave_total(s);
+            if (lane == 0) rdp_g[(o1 + x) * h + o] = s;
+        }
+        tr = wave_total(tr);
+        if (lane == 0) trp[wv] = tr;
+        __syncthreads();
+        if (threadIdx.x == 0) trd_g[(long long)i * h + o] = (trp[0] + trp[1]) + (trp[2] + trp[3]);
+        __syncthreads();
+    }
+}
+
 
 // ------------------------------------------------------------------ CCN-2D, degrees 65..256
 // The same passes as k_ccn2_fwd / k_ccn2_bwd_node / k_ccn2_bwd_gather for the nodes whose receptive
@@ -1161,31 +1626,34 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd_big(CcnPlanView v, const int* 
     }
 }
 
-// k_ccn2_bwd_gather for degrees 65..256: lane w of row u in 64-lane chunks, the neighbours a with
-// u in C_a in 64-wide ballot chunks (ascending: the summation order of the fast kernel's walk).
-template <int C, int NB>
-__global__ void __launch_bounds__(256) k_ccn2_bwd_gather_big(CcnPlanView v, const int* total_nodes, C2Grad gd,
-                                                             int cin, const float* __restrict__ dsum, int dsum_ld,
-                                                             int dsum_off, int level0, float* __restrict__ dout) {
+// k_c2_gather for degrees 65..256: lane w of row u in 64-lane chunks, the neighbours a with u in C_a
+// in 64-wide ballot chunks (ascending), position maps read from global memory (L2-resident)
+template <int H, int NB>
+__global__ void __launch_bounds__(256) k_c2_gather_big(CcnPlanView v, const int* total_nodes, C2Dp g,
+                                                       const float* __restrict__ W, int h,
+                                                       const float* __restrict__ dsum, int dsum_ld, int dsum_off,
+                                                       float* __restrict__ dout) {
     __shared__ unsigned long long vmask[CCN_BIGD][CCN_BW];
-    __shared__ float red[4][C];
-    __shared__ int s_i[CCN_BIGD], s_di[CCN_BIGD], s_oi[CCN_BIGD], s_aj[CCN_BIGD];
+    __shared__ int s_i[CCN_BIGD], s_di[CCN_BIGD], s_oi[CCN_BIGD], s_o1[CCN_BIGD], s_aj[CCN_BIGD];
+    __shared__ float wc[NWC][H][H];
     const int j = blockIdx.x;
     if (j >= *total_nodes) return;
     const int n = v.deg[j];
-    if (n <= CCN_MAXD || n > CCN_BIGD || cin > C) return;
+    if (n <= C2_NCAP || n > CCN_BIGD || h > H) return;
     const int nw = (n + 63) >> 6;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long o2 = v.off2[j];
     const int* sp = v.pos + o2;
     const int* nj = v.nbr + (long long)j * v.nmax;
     const int sj = v.selfpos[j];
-    const int g = v.graph[j];
+    const int gr = v.graph[j];
+    c2_dT_weights<H>(wc, W, h);
     for (int t = threadIdx.x; t < n; t += 256) {
         const int i = nj[t];
         s_i[t] = i;
         s_di[t] = v.deg[i];
         s_oi[t] = v.off2[i];
+        s_o1[t] = v.off1[i];
         s_aj[t] = sp[(long long)t * n + sj];  // position of j in N(i_a)
     }
     for (int a = wv; a < n; a += 4)
@@ -1195,88 +1663,47 @@ __global__ void __launch_bounds__(256) k_ccn2_bwd_gather_big(CcnPlanView v, cons
             if (lane == 0) vmask[a][w] = m;
         }
     __syncthreads();
-    float rd[C], part[C];
+    float rd[H];
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-        rd[c] = (dsum && c < cin) ? dsum[(long long)g * dsum_ld + dsum_off + c] : 0.f;
-        part[c] = 0.f;
-    }
+    for (int c = 0; c < H; ++c) rd[c] = (dsum && c < h) ? dsum[(long long)gr * dsum_ld + dsum_off + c] : 0.f;
     for (int u = wv; u < n; u += 4) {
         for (int w0 = 0; w0 < n; w0 += 64) {
             const int wl = w0 + lane;
-            float acc[C];
+            float acc[H];
 #pragma unroll
-            for (int c = 0; c < C; ++c) acc[c] = 0.f;
+            for (int c = 0; c < H; ++c) acc[c] = 0.f;
             for (int a0 = 0; a0 < n; a0 += 64) {
                 const int al = a0 + lane < n ? a0 + lane : 0;
                 unsigned long long as = __ballot(a0 + lane < n && mbit(vmask[al], u));
                 while (as) {
                     int aa[NB];
-#pragma unroll
-                    for (int q = 0; q < NB; ++q) {
-                        aa[q] = as ? a0 + __ffsll((long long)as) - 1 : -1;
-                        as &= as ? as - 1ull : 0ull;
-                    }
-                    float tsc[NB][C], tsa[NB][C], td1[NB][C], td2[NB][C], td3[NB][C];
-                    int zb[NB], zz[NB], zaj[NB];
+                    c2_take<NB>(as, aa);
+                    float ld[NB][6][H];
+                    int zb[NB], zz[NB];
                     bool vz[NB];
 #pragma unroll
                     for (int q = 0; q < NB; ++q) {
-                        const int a = aa[q] >= 0 ? aa[q] : 0;
+                        const int a = aa[q] >= 0 ? a0 + aa[q] : 0;
                         vz[q] = aa[q] >= 0 && wl < n && mbit(vmask[a], wl);
-                        const int b = max(sp[(long long)a * n + u], 0), z = vz[q] ? sp[(long long)a * n + wl] : 0;
-                        const int aj = s_aj[a], di = s_di[a], i = s_i[a];
-                        const long long oi = s_oi[a];
-                        const long long rab = (oi + (long long)aj * di + b) * cin, rbz = (oi + (long long)b * di + z) * cin;
-                        zb[q] = b;
-                        zz[q] = z;
-                        zaj[q] = aj;
-#pragma unroll
-                        for (int c = 0; c < C; ++c) {
-                            const bool ok = c < cin;
-                            tsc[q][c] = ok ? gd.dSc[rab + c] : 0.f;
-                            tsa[q][c] = ok ? gd.dSa[rbz + c] : 0.f;
-                            td1[q][c] = ok ? gd.dD1[rab + c] : 0.f;
-                            td2[q][c] = ok ? gd.dD2[rab + c] : 0.f;
-                            td3[q][c] = ok ? gd.dd3[(long long)i * cin + c] : 0.f;
-                        }
+                        zb[q] = max(sp[(long long)a * n + u], 0);
+                        zz[q] = vz[q] ? sp[(long long)a * n + wl] : 0;
+                        c2_dT_load<H>(g, h, s_oi[a], s_o1[a], s_i[a], s_di[a], s_aj[a], zb[q], zz[q], ld[q]);
                     }
 #pragma unroll
                     for (int q = 0; q < NB; ++q) {
                         if (aa[q] < 0) break;
                         if (!vz[q]) continue;
-                        const int b = zb[q], z = zz[q], aj = zaj[q];
-#pragma unroll
-                        for (int c = 0; c < C; ++c) {
-                            if (c >= cin) break;
-                            float t = tsc[q][c] + tsa[q][c];
-                            if (z == b) t += td1[q][c];
-                            if (z == aj) t += td2[q][c];
-                            if (aj == b && b == z) t += td3[q][c];
-                            acc[c] += t;
-                        }
+                        const int a = a0 + aa[q];
+                        c2_dT_add<H>(wc, ld[q], h, (float)s_di[a], s_aj[a], zb[q], zz[q], acc);
                     }
                 }
             }
+            if (wl < n)
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                if (c >= cin) break;
-                if (level0) part[c] += acc[c];
-                else if (wl < n) dout[(o2 + (long long)u * n + wl) * cin + c] = acc[c] + rd[c];
-            }
-        }
-    }
-    if (level0) {
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            if (c >= cin) break;
-            const float t = wave_sum(part[c]);
-            if (lane == 0) red[wv][c] = t;
-        }
-        __syncthreads();
-        if (threadIdx.x < cin) {
-            const int c = threadIdx.x;
-            dout[(long long)j * cin + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + (float)(n * n) * rd[c];
+                for (int c = 0; c < H; ++c) {
+                    if (c >= h) break;
+                    dout[(o2 + (long long)u * n + wl) * h + c] = acc[c] + rd[c];
+                }
         }
     }
 }
@@ -1503,13 +1930,13 @@ __global__ void k_collapse6to3_bwd(const float* __restrict__ dO, float* __restri
 
 // ------------------------------------------------------------------ executor
 struct CcnLayout {
-    size_t node_off, deg, nbr, selfpos, graph, off1, off2, totals, err, pos;
+    size_t node_off, deg, nbr, selfpos, graph, off1, off2, totals, err, bits, bcnt, pos;
     size_t plan_bytes;
     // feature workspace (needs sums)
     std::vector<size_t> F, coll;    // per level 1..L
     std::vector<C2Save> dummy;
     size_t sc[16], sa[16], d1[16], d2[16], q1[16], q3[16], tot[16], d3[16];
-    size_t feat, rpart, g0, dsum, ppart, dF[2], dcoll, g_sc, g_sa, g_d1, g_d2, g_d3, xp, dxp;
+    size_t feat, rpart, g0, dsum, ppart, dF[2], dcoll, g_sc, g_sa, g_d1, g_d2, g_d3, xp, dxp, rdp, trd;
     size_t bytes;
 };
 
@@ -1539,6 +1966,9 @@ CcnLayout ccn_layout(const hgnn_ccn_config* c, long long sum_d, long long sum_d2
     L.off2 = take(4 * (nodes + 1));
     L.totals = take(16);
     L.err = take(16);
+    const int nw = (c->nmax + 63) / 64;
+    L.bits = take(8 * nodes * nw);
+    L.bcnt = take(4 * nodes * nw);
     L.pos = take(4 * (size_t)(sum_d2 > 0 ? sum_d2 : 1));
     L.plan_bytes = t;
     const long long rows = c->order == 1 ? sum_d : sum_d2;
@@ -1547,12 +1977,13 @@ CcnLayout ccn_layout(const hgnn_ccn_config* c, long long sum_d, long long sum_d2
     L.F.resize(Lv);
     L.coll.resize(Lv);
     int cmax = f > h ? f : h;
+    const bool big = c->order == 2 && c->nmax > CCN_MAXD;  // degrees above 64 possible
     for (int l = 0; l < Lv; ++l) {
         const int cin = l == 0 ? f : h;
         L.F[l] = take(4 * (size_t)rows * h);
         if (c->order == 1) {
             L.coll[l] = take(4 * (size_t)rows * 2 * cin);
-        } else {
+        } else if (big) {  // C2Save: only the large-degree kernels keep contraction statistics
             L.sc[l] = take(4 * (size_t)sum_d2 * cin);
             L.sa[l] = take(4 * (size_t)sum_d2 * cin);
             L.d1[l] = take(4 * (size_t)sum_d2 * cin);
@@ -1575,11 +2006,15 @@ CcnLayout ccn_layout(const hgnn_ccn_config* c, long long sum_d, long long sum_d2
     if (c->order == 1) {
         L.dcoll = take(4 * (size_t)rows * 2 * cmax);
     } else {
-        L.g_sc = take(4 * (size_t)sum_d2 * cmax);
-        L.g_sa = take(4 * (size_t)sum_d2 * cmax);
-        L.g_d1 = take(4 * (size_t)sum_d2 * cmax);
-        L.g_d2 = take(4 * (size_t)sum_d2 * cmax);
-        L.g_d3 = take(4 * (size_t)nodes * cmax);
+        L.rdp = take(4 * (size_t)(sum_d > 0 ? sum_d : 1) * h);  // dp format: row sums and trace of dp
+        L.trd = take(4 * (size_t)nodes * h);
+        if (big) {  // C2Grad of the large-degree backward node pass
+            L.g_sc = take(4 * (size_t)sum_d2 * cmax);
+            L.g_sa = take(4 * (size_t)sum_d2 * cmax);
+            L.g_d1 = take(4 * (size_t)sum_d2 * cmax);
+            L.g_d2 = take(4 * (size_t)sum_d2 * cmax);
+            L.g_d3 = take(4 * (size_t)nodes * cmax);
+        }
     }
     L.xp = take(4 * (size_t)nodes * f);
     L.dxp = take(4 * (size_t)nodes * f);
@@ -1617,6 +2052,85 @@ C2Save save_of(const CcnLayout& L, void* ws, int l) {
     s.tot = P<float>(ws, L.tot[l]);
     s.d3 = P<float>(ws, L.d3[l]);
     return s;
+}
+
+// The CCN-2D kernels of degrees <= 64 take the receptive-field bound ncap = min(nmax, 64) for their
+// dynamic LDS (P or dp [ncap^2][HC] fp32 + the int16 position map): 40 KB at ncap = 64.
+// Instantiations by channel count: cin <= 2 (the reference's hidden_size = 2 levels), <= 8, <= 16.
+int c2_ncap(int nmax) { return nmax < C2_NCAP ? nmax : C2_NCAP; }
+
+template <int CM, int HC, int NB, bool L0>
+int launch_c2_fwd_t(const CcnPlanView& v, const int* tot, const float* fin, const float* X, int cin, const float* W,
+                    const float* b, int h, int ncap, int nodes, float* fout, hipStream_t s) {
+    const size_t lds = c2_dyn_lds(ncap, HC);
+    hipLaunchKernelGGL((k_c2_fwd<CM, HC, NB, L0>), dim3(nodes > 0 ? nodes : 1), dim3(256), lds, s, v, tot, fin, X, cin,
+                       W, b, h, ncap, fout);
+    HGNN_LAUNCH_CHECK();
+    return HGNN_OK;
+}
+
+int launch_c2_fwd(const CcnPlanView& v, const int* tot, const float* fin, int level0, const float* X, int cin,
+                  const float* W, const float* b, int h, int nmax, int nodes, float* fout, hipStream_t s) {
+    const int ncap = c2_ncap(nmax);
+    if (level0) {
+        if (cin <= 8) return launch_c2_fwd_t<8, 2, 1, true>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
+        return launch_c2_fwd_t<16, 2, 1, true>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
+    }
+    if (cin <= 2) return launch_c2_fwd_t<2, 2, 4, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
+    if (cin <= 8) return launch_c2_fwd_t<8, 2, 4, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
+    return launch_c2_fwd_t<16, 2, 2, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
+}
+
+template <int CM, int HC, int NB, bool L0>
+int launch_c2_bwd_t(const CcnPlanView& v, const int* tot, float* dF, const float* F, const float* fin, const float* X,
+                    int cin, const float* W, int h, int ncap, int nodes, float* rdp, float* trd, float* ppart,
+                    float* g0, hipStream_t s) {
+    const size_t lds = c2_dyn_lds(ncap, HC);
+    hipLaunchKernelGGL((k_c2_bwd<CM, HC, NB, L0>), dim3(nodes > 0 ? nodes : 1), dim3(256), lds, s, v, tot, dF, F, fin,
+                       X, cin, W, h, ncap, rdp, trd, ppart, g0);
+    HGNN_LAUNCH_CHECK();
+    return HGNN_OK;
+}
+
+int launch_c2_bwd(const CcnPlanView& v, const int* tot, float* dF, const float* F, const float* fin, int level0,
+                  const float* X, int cin, const float* W, int h, int nmax, int nodes, float* rdp, float* trd,
+                  float* ppart, float* g0, hipStream_t s) {
+    const int ncap = c2_ncap(nmax);
+    if (level0) {
+        if (cin <= 8)
+            return launch_c2_bwd_t<8, 2, 1, true>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+        return launch_c2_bwd_t<16, 2, 1, true>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+    }
+    if (cin <= 2)
+        return launch_c2_bwd_t<2, 2, 4, false>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+    if (cin <= 8)
+        return launch_c2_bwd_t<8, 2, 4, false>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+    return launch_c2_bwd_t<16, 1, 2, false>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+}
+
+int launch_c2_gather(const CcnPlanView& v, const int* tot, const C2Dp& g, const float* W, int h, const float* dsum,
+                     int dsum_ld, int dsum_off, int nmax, int nodes, float* dout, hipStream_t s) {
+    const dim3 grid(nodes > 0 ? nodes : 1);
+    if (h <= 2)
+        hipLaunchKernelGGL((k_c2_gather<2, 4>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
+    else if (h <= 8)
+        hipLaunchKernelGGL((k_c2_gather<8, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
+    else
+        hipLaunchKernelGGL((k_c2_gather<16, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
+    HGNN_LAUNCH_CHECK();
+    if (nmax > C2_NCAP) {
+        if (h <= 2)
+            hipLaunchKernelGGL((k_c2_gather_big<2, 4>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld,
+                               dsum_off, dout);
+        else if (h <= 8)
+            hipLaunchKernelGGL((k_c2_gather_big<8, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld,
+                               dsum_off, dout);
+        else
+            hipLaunchKernelGGL((k_c2_gather_big<16, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld,
+                               dsum_off, dout);
+        HGNN_LAUNCH_CHECK();
+    }
+    return HGNN_OK;
 }
 
 }  // namespace
@@ -1670,11 +2184,12 @@ static int ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_
     int r = launch_plan(d_n_batch, nullptr, cfg->bs, cfg->nmax, 0, m, s);
     if (r) return r;
     CcnPlanView v = plan_view(cfg, L, plan_ws);
-    hipLaunchKernelGGL(k_ccn_nbrs, dim3(cfg->bs), dim3(256), 0, s, d_adj, cfg->nmax, v.node_off,
-                       P<int>(plan_ws, L.deg), P<int>(plan_ws, L.nbr), P<int>(plan_ws, L.selfpos),
-                       P<int>(plan_ws, L.graph), m.err, cfg->order == 1 ? CCN1_MAXD : CCN_BIGD);
+    hipLaunchKernelGGL(k_ccn_nbrs, dim3(cfg->bs, (cfg->nmax + CCN_NB_ROWS - 1) / CCN_NB_ROWS), dim3(256), 0, s, d_adj,
+                       cfg->nmax, v.node_off, P<int>(plan_ws, L.deg), P<int>(plan_ws, L.nbr),
+                       P<int>(plan_ws, L.selfpos), P<int>(plan_ws, L.graph), P<unsigned long long>(plan_ws, L.bits),
+                       P<int>(plan_ws, L.bcnt), m.err, cfg->order == 1 ? CCN1_MAXD : CCN_BIGD);
     HGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ccn_scan, dim3(1), dim3(256), 0, s, P<int>(plan_ws, L.deg), m.totals,
+    hipLaunchKernelGGL(k_ccn_scan, dim3(1), dim3(1024), 0, s, P<int>(plan_ws, L.deg), m.totals,
                        P<int>(plan_ws, L.off1), P<int>(plan_ws, L.off2), m.totals + 2);
     HGNN_LAUNCH_CHECK();
     long long nodes = (long long)cfg->bs * cfg->nmax;
@@ -1694,7 +2209,8 @@ static int ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_
         h_sums[2] = nodes;
     }
     hipLaunchKernelGGL(k_ccn_pos, dim3((unsigned)((nodes + 3) / 4 > 0 ? (nodes + 3) / 4 : 1)), dim3(256), 0, s, v,
-                       m.totals, P<int>(plan_ws, L.pos), max_sum_d2, m.err);
+                       m.totals, P<unsigned long long>(plan_ws, L.bits), P<int>(plan_ws, L.bcnt),
+                       P<int>(plan_ws, L.pos), max_sum_d2, m.err);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
 }
@@ -1749,14 +2265,9 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
                                l == 0 ? 1 : 0, d_X, cin, w, b, h, P<float>(W, L.coll[l]), P<float>(W, L.F[l]));
         } else {
             const bool narrow = cin <= C2_CMAX && h <= C2_HMAX;
-            if (narrow)
-                hipLaunchKernelGGL((k_ccn2_fwd<C2_CMAX, C2_HMAX>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s, v, tot,
-                                   fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, save_of(L, W, l), P<float>(W, L.F[l]));
-            else
-                hipLaunchKernelGGL((k_ccn2_fwd<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0,
-                                   s, v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, save_of(L, W, l),
-                                   P<float>(W, L.F[l]));
-            HGNN_LAUNCH_CHECK();
+            const int r = launch_c2_fwd(v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, cfg->nmax, nodes,
+                                        P<float>(W, L.F[l]), s);
+            if (r) return r;
             if (cfg->nmax > CCN_MAXD) {  // degrees 65..256 possible: their nodes in the large-degree kernel
                 if (narrow)
                     hipLaunchKernelGGL((k_ccn2_fwd_big<C2_CMAX, C2_HMAX>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s,
@@ -1825,25 +2336,26 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
             hipLaunchKernelGGL(k_ccn1_bwd_node, dim3(nb4), dim3(256), 0, s, v, tot, dF, P<float>(W, L.F[l]),
                                P<float>(W, L.coll[l]), cin, w, h, P<float>(W, L.dcoll), ppart);
         } else {
-            C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
-                      P<float>(W, L.g_d3)};
             const bool narrow = cin <= C2_CMAX && h <= C2_HMAX;
             float* g0p = l == 0 ? P<float>(W, L.g0) : nullptr;
-            if (narrow)
-                hipLaunchKernelGGL((k_ccn2_bwd_node<C2_CMAX, C2_HMAX>), dim3(nb1), dim3(256), 0, s, v, tot, dF,
-                                   P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
-            else
-                hipLaunchKernelGGL((k_ccn2_bwd_node<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nb1), dim3(256), 0, s, v, tot,
-                                   dF, P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
-            HGNN_LAUNCH_CHECK();
-            if (cfg->nmax > CCN_MAXD) {
+            const float* fin = l == 0 ? nullptr : P<float>(W, L.F[l - 1]);
+            if (cfg->nmax > CCN_MAXD) {  // the large-degree nodes read the raw dF: before the dp rewrite
+                C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
+                          P<float>(W, L.g_d3)};
                 if (narrow)
-                    hipLaunchKernelGGL((k_ccn2_bwd_node<C2_CMAX, C2_HMAX, true>), dim3(nb1), dim3(256), 0, s, v, tot,
-                                       dF, P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
+                    hipLaunchKernelGGL((k_ccn2_bwd_node_big<C2_CMAX, C2_HMAX>), dim3(nb1), dim3(256), 0, s, v, tot, dF,
+                                       P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
                 else
-                    hipLaunchKernelGGL((k_ccn2_bwd_node<C2_CMAX_WIDE, C2_HMAX_WIDE, true>), dim3(nb1), dim3(256), 0, s,
-                                       v, tot, dF, P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
+                    hipLaunchKernelGGL((k_ccn2_bwd_node_big<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nb1), dim3(256), 0, s, v,
+                                       tot, dF, P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
+                HGNN_LAUNCH_CHECK();
+                hipLaunchKernelGGL(k_c2_dp_big, dim3(nb1), dim3(256), 0, s, v, tot, dF, P<float>(W, L.F[l]), h,
+                                   P<float>(W, L.rdp), P<float>(W, L.trd));
+                HGNN_LAUNCH_CHECK();
             }
+            const int r = launch_c2_bwd(v, tot, dF, P<float>(W, L.F[l]), fin, l == 0 ? 1 : 0, P<float>(W, L.xp), cin,
+                                        w, h, cfg->nmax, nodes, P<float>(W, L.rdp), P<float>(W, L.trd), ppart, g0p, s);
+            if (r) return r;
         }
         HGNN_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_ccn_param_reduce, dim3(h * K + h), dim3(256), 0, s, ppart, tot, h * K, h, grads[2 * l],
@@ -1856,33 +2368,13 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
             hipLaunchKernelGGL(k_ccn1_bwd_gather, dim3(nb4), dim3(256), 0, s, v, tot, P<float>(W, L.dcoll), cin, dsum,
                                nf, doff, lvl0, dst);
         } else {
-            C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
-                      P<float>(W, L.g_d3)};
-            if (lvl0)
+            if (lvl0) {
                 hipLaunchKernelGGL(k_ccn2_dx0, dim3(nb4), dim3(256), 0, s, v, tot, P<float>(W, L.g0), cin, dsum, nf,
                                    dst);
-            else {
-                if (cin <= 2)
-                    hipLaunchKernelGGL((k_ccn2_bwd_gather<2, 4>), dim3(nb1), dim3(256), 0, s, v, tot, gd, cin, dsum,
-                                       nf, doff, lvl0, dst);
-                else if (cin <= C2_CMAX)
-                    hipLaunchKernelGGL((k_ccn2_bwd_gather<C2_CMAX, 1>), dim3(nb1), dim3(256), 0, s, v, tot, gd, cin,
-                                       dsum, nf, doff, lvl0, dst);
-                else
-                    hipLaunchKernelGGL((k_ccn2_bwd_gather<C2_CMAX_WIDE, 1>), dim3(nb1), dim3(256), 0, s, v, tot, gd,
-                                       cin, dsum, nf, doff, lvl0, dst);
-                HGNN_LAUNCH_CHECK();
-                if (cfg->nmax > CCN_MAXD) {
-                    if (cin <= 2)
-                        hipLaunchKernelGGL((k_ccn2_bwd_gather_big<2, 4>), dim3(nb1), dim3(256), 0, s, v, tot, gd, cin,
-                                           dsum, nf, doff, lvl0, dst);
-                    else if (cin <= C2_CMAX)
-                        hipLaunchKernelGGL((k_ccn2_bwd_gather_big<C2_CMAX, 1>), dim3(nb1), dim3(256), 0, s, v, tot, gd,
-                                           cin, dsum, nf, doff, lvl0, dst);
-                    else
-                        hipLaunchKernelGGL((k_ccn2_bwd_gather_big<C2_CMAX_WIDE, 1>), dim3(nb1), dim3(256), 0, s, v, tot,
-                                           gd, cin, dsum, nf, doff, lvl0, dst);
-                }
+            } else {
+                const C2Dp g{dF, P<float>(W, L.rdp), P<float>(W, L.trd)};
+                const int r = launch_c2_gather(v, tot, g, w, h, dsum, nf, doff, cfg->nmax, nodes, dst, s);
+                if (r) return r;
             }
         }
         HGNN_LAUNCH_CHECK();

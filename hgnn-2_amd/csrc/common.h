@@ -53,6 +53,27 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// The same total on DPP moves (no LDS round trip), returned uniform (lane 63's value).  Every lane
+// of the wave must be active.  quad_perm [1,0,3,2] / [2,3,0,1] sum quads, row_half_mirror and
+// row_mirror finish each 16-lane row, row_bcast:15 / :31 carry rows 0 -> 1, 2 -> 3 and 1 -> 2, 3.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_moved(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
+__device__ __forceinline__ float wave_total(float v) {
+    v += dpp_moved<0xB1, 0xF>(v);
+    v += dpp_moved<0x4E, 0xF>(v);
+    v += dpp_moved<0x141, 0xF>(v);
+    v += dpp_moved<0x140, 0xF>(v);
+    v += dpp_moved<0x142, 0xA>(v);
+    v += dpp_moved<0x143, 0xC>(v);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+// value of v in lane l (l wave-uniform)
+__device__ __forceinline__ float lane_value(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 template <typename T>
