@@ -99,7 +99,7 @@ __global__ void __launch_bounds__(256) k_ccn_nbrs(const float* __restrict__ adj,
 }
 
 // exclusive scans of deg and deg^2 over all nodes (single block of 1024: a serial run of consecutive
-// nodes per thread, then a scan of the 1024 run totals); totals[0..1]
+// nodes per thread, then a scan of the 1024 run totals); totals[0..1] = the sums, totals[2] = max degree
 __global__ void __launch_bounds__(1024) k_ccn_scan(const int* deg, const int* total_nodes, int* off1, int* off2,
                                                    int* totals) {
     __shared__ int s1[1024], s2[1024];
@@ -107,14 +107,18 @@ __global__ void __launch_bounds__(1024) k_ccn_scan(const int* deg, const int* to
     const int n = *total_nodes;
     const int per = (n + 1023) / 1024;
     const int i0 = min(n, t * per), i1 = min(n, i0 + per);
-    int a1 = 0, a2 = 0;
+    __shared__ int smax[16];
+    int a1 = 0, a2 = 0, dm = 0;
     for (int i = i0; i < i1; ++i) {
         const int d = deg[i];
         a1 += d;
         a2 += d * d;
+        dm = max(dm, d);
     }
     s1[t] = a1;
     s2[t] = a2;
+    for (int o = 32; o > 0; o >>= 1) dm = max(dm, __shfl_xor(dm, o, 64));
+    if ((t & 63) == 0) smax[t >> 6] = dm;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
         const int b1 = t >= o ? s1[t - o] : 0, b2 = t >= o ? s2[t - o] : 0;
@@ -136,6 +140,9 @@ __global__ void __launch_bounds__(1024) k_ccn_scan(const int* deg, const int* to
         off2[n] = s2[1023];
         totals[0] = s1[1023];
         totals[1] = s2[1023];
+        int m = 0;
+        for (int w = 0; w < 16; ++w) m = max(m, smax[w]);
+        totals[2] = m;  // largest receptive field
     }
 }
 
@@ -1073,6 +1080,14 @@ __global__ void __launch_bounds__(256) k_c2_bwd(CcnPlanView v, const int* total_
 #pragma unroll
                 for (int c = 0; c < CM; ++c) sa[c] = 0.f;
                 unsigned long long as = __ballot(la && ((my_mask >> b) & 1ull));
+                // lane a: dp[a][b], dp[b][a], rdp[a] of this row (read once, then by readlane)
+                float my_ab[HC], my_ba[HC], my_ra[HC];
+#pragma unroll
+                for (int o = 0; o < HC; ++o) {
+                    my_ab[o] = la ? dpL[(lane * n + b) * HC + o] : 0.f;
+                    my_ba[o] = la ? dpL[(b * n + lane) * HC + o] : 0.f;
+                    my_ra[o] = la ? rdpL[lane][o] : 0.f;
+                }
                 while (as) {
                     int aa[NB];
                     c2_take<NB>(as, aa);
@@ -1084,8 +1099,8 @@ __global__ void __launch_bounds__(256) k_c2_bwd(CcnPlanView v, const int* total_
                         if (a < 0) break;
 #pragma unroll
                         for (int o = 0; o < HC; ++o) {
-                            const float dab = dpL[(a * n + b) * HC + o], dba = dpL[(b * n + a) * HC + o];
-                            const float ra = rdpL[a][o];
+                            const float dab = lane_value(my_ab[o], a), dba = lane_value(my_ba[o], a);
+                            const float ra = lane_value(my_ra[o], a);
                             const float d15 = lane == b ? dab : 0.f, d16 = lane == a ? dba : 0.f;
 #pragma unroll
                             for (int c = 0; c < CM; ++c) {
@@ -1292,17 +1307,41 @@ __global__ void __launch_bounds__(256) k_c2_gather(CcnPlanView v, const int* tot
     float rd[H];
 #pragma unroll
     for (int c = 0; c < H; ++c) rd[c] = (dsum && c < h) ? dsum[(long long)gr * dsum_ld + dsum_off + c] : 0.f;
-    // lane a holds neighbour i_a's mask, node, degree, offsets and the position of j in N(i_a)
+    // lane a holds neighbour i_a's mask, node, degree, offsets, the position aj of j in N(i_a), and the
+    // row-independent parts of its dp format (rdp_i[aj], tr_i)
     const bool la = lane < n;
     const unsigned long long my_mask = la ? vmask[lane] : 0ull;
     const int my_i = la ? s_i[lane] : 0, my_di = la ? s_di[lane] : 0, my_oi = la ? s_oi[lane] : 0;
     const int my_o1 = la ? s_o1[lane] : 0, my_aj = la ? s_aj[lane] : 0;
+    float my_ra[H], my_tr[H];
+#pragma unroll
+    for (int o = 0; o < H; ++o) {
+        my_ra[o] = (la && o < h) ? g.rdp[((long long)my_o1 + my_aj) * h + o] : 0.f;
+        my_tr[o] = (la && o < h) ? g.trd[(long long)my_i * h + o] : 0.f;
+    }
     for (int u = wv; u < n; u += 4) {
         float acc[H];
 #pragma unroll
         for (int c = 0; c < H; ++c) acc[c] = 0.f;
-        // the neighbours a with u in C_a, ascending, NB at a time (all loads of a batch in flight)
-        unsigned long long as = __ballot(la && ((my_mask >> u) & 1ull));
+        // lanes a with u in C_a load the row-dependent uniform values of their neighbour at once:
+        // b = p_a(u), dp_i[aj][b], dp_i[b][aj], rdp_i[b]
+        const unsigned long long au = __ballot(la && ((my_mask >> u) & 1ull));
+        const bool in = (au >> lane) & 1ull;
+        const int my_b = in ? (int)sp[lane * n + u] : 0;
+        float my_ab[H], my_ba[H], my_rb[H];
+        {
+            const float* pab = g.dp + ((long long)my_oi + (long long)my_aj * my_di + my_b) * h;
+            const float* pba = g.dp + ((long long)my_oi + (long long)my_b * my_di + my_aj) * h;
+            const float* prb = g.rdp + ((long long)my_o1 + my_b) * h;
+#pragma unroll
+            for (int o = 0; o < H; ++o) {
+                my_ab[o] = (in && o < h) ? pab[o] : 0.f;
+                my_ba[o] = (in && o < h) ? pba[o] : 0.f;
+                my_rb[o] = (in && o < h) ? prb[o] : 0.f;
+            }
+        }
+        // the neighbours a with u in C_a, ascending, NB at a time: one row piece dp_i[b][z] per lane each
+        unsigned long long as = au;
         while (as) {
             int aa[NB];
             c2_take<NB>(as, aa);
@@ -1313,12 +1352,20 @@ __global__ void __launch_bounds__(256) k_c2_gather(CcnPlanView v, const int* tot
             for (int q = 0; q < NB; ++q) {
                 const int a = aa[q] >= 0 ? aa[q] : 0;
                 vz[q] = aa[q] >= 0 && ((lane_value_u64(my_mask, a) >> lane) & 1ull);
-                zb[q] = uniform(max((int)sp[a * n + u], 0));
+                zb[q] = lane_value_i(my_b, a);
                 zz[q] = vz[q] ? (int)sp[a * n + lane] : 0;
                 zd[q] = lane_value_i(my_di, a);
                 zj[q] = lane_value_i(my_aj, a);
-                c2_dT_load<H>(g, h, lane_value_i(my_oi, a), lane_value_i(my_o1, a), lane_value_i(my_i, a), zd[q],
-                              zj[q], zb[q], zz[q], ld[q]);
+                const float* pbz = g.dp + ((long long)lane_value_i(my_oi, a) + (long long)zb[q] * zd[q] + zz[q]) * h;
+#pragma unroll
+                for (int o = 0; o < H; ++o) {
+                    ld[q][0][o] = lane_value(my_ab[o], a);
+                    ld[q][1][o] = lane_value(my_ba[o], a);
+                    ld[q][2][o] = lane_value(my_ra[o], a);
+                    ld[q][3][o] = lane_value(my_rb[o], a);
+                    ld[q][4][o] = lane_value(my_tr[o], a);
+                    ld[q][5][o] = o < h ? pbz[o] : 0.f;
+                }
             }
 #pragma unroll
             for (int q = 0; q < NB; ++q) {
@@ -1964,7 +2011,7 @@ CcnLayout ccn_layout(const hgnn_ccn_config* c, long long sum_d, long long sum_d2
     L.graph = take(4 * nodes);
     L.off1 = take(4 * (nodes + 1));
     L.off2 = take(4 * (nodes + 1));
-    L.totals = take(16);
+    L.totals = take(32);
     L.err = take(16);
     const int nw = (c->nmax + 63) / 64;
     L.bits = take(8 * nodes * nw);
@@ -2054,10 +2101,10 @@ C2Save save_of(const CcnLayout& L, void* ws, int l) {
     return s;
 }
 
-// The CCN-2D kernels of degrees <= 64 take the receptive-field bound ncap = min(nmax, 64) for their
+// The CCN-2D kernels of degrees <= 64 take the receptive-field bound ncap = min(max degree, 64) for their
 // dynamic LDS (P or dp [ncap^2][HC] fp32 + the int16 position map): 40 KB at ncap = 64.
 // Instantiations by channel count: cin <= 2 (the reference's hidden_size = 2 levels), <= 8, <= 16.
-int c2_ncap(int nmax) { return nmax < C2_NCAP ? nmax : C2_NCAP; }
+int c2_ncap(long long dmax) { return dmax < C2_NCAP ? (int)(dmax > 1 ? dmax : 1) : C2_NCAP; }
 
 template <int CM, int HC, int NB, bool L0>
 int launch_c2_fwd_t(const CcnPlanView& v, const int* tot, const float* fin, const float* X, int cin, const float* W,
@@ -2070,13 +2117,13 @@ int launch_c2_fwd_t(const CcnPlanView& v, const int* tot, const float* fin, cons
 }
 
 int launch_c2_fwd(const CcnPlanView& v, const int* tot, const float* fin, int level0, const float* X, int cin,
-                  const float* W, const float* b, int h, int nmax, int nodes, float* fout, hipStream_t s) {
-    const int ncap = c2_ncap(nmax);
+                  const float* W, const float* b, int h, long long dmax, int nodes, float* fout, hipStream_t s) {
+    const int ncap = c2_ncap(dmax);
     if (level0) {
         if (cin <= 8) return launch_c2_fwd_t<8, 2, 1, true>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
         return launch_c2_fwd_t<16, 2, 1, true>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
     }
-    if (cin <= 2) return launch_c2_fwd_t<2, 2, 4, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
+    if (cin <= 2) return launch_c2_fwd_t<2, 2, 8, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
     if (cin <= 8) return launch_c2_fwd_t<8, 2, 4, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
     return launch_c2_fwd_t<16, 2, 2, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
 }
@@ -2093,16 +2140,16 @@ int launch_c2_bwd_t(const CcnPlanView& v, const int* tot, float* dF, const float
 }
 
 int launch_c2_bwd(const CcnPlanView& v, const int* tot, float* dF, const float* F, const float* fin, int level0,
-                  const float* X, int cin, const float* W, int h, int nmax, int nodes, float* rdp, float* trd,
+                  const float* X, int cin, const float* W, int h, long long dmax, int nodes, float* rdp, float* trd,
                   float* ppart, float* g0, hipStream_t s) {
-    const int ncap = c2_ncap(nmax);
+    const int ncap = c2_ncap(dmax);
     if (level0) {
         if (cin <= 8)
             return launch_c2_bwd_t<8, 2, 1, true>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
         return launch_c2_bwd_t<16, 2, 1, true>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
     }
     if (cin <= 2)
-        return launch_c2_bwd_t<2, 2, 4, false>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+        return launch_c2_bwd_t<2, 2, 8, false>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
     if (cin <= 8)
         return launch_c2_bwd_t<8, 2, 4, false>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
     return launch_c2_bwd_t<16, 1, 2, false>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
@@ -2112,7 +2159,7 @@ int launch_c2_gather(const CcnPlanView& v, const int* tot, const C2Dp& g, const 
                      int dsum_ld, int dsum_off, int nmax, int nodes, float* dout, hipStream_t s) {
     const dim3 grid(nodes > 0 ? nodes : 1);
     if (h <= 2)
-        hipLaunchKernelGGL((k_c2_gather<2, 4>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
+        hipLaunchKernelGGL((k_c2_gather<2, 8>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
     else if (h <= 8)
         hipLaunchKernelGGL((k_c2_gather<8, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
     else
@@ -2194,19 +2241,21 @@ static int ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_
     HGNN_LAUNCH_CHECK();
     long long nodes = (long long)cfg->bs * cfg->nmax;
     if (sync) {
-        int hbuf[4] = {0, 0, 0, 0};
-        HGNN_HOST_CHECK(hipMemcpyAsync(hbuf, m.totals, 16, hipMemcpyDeviceToHost, s));
+        int hbuf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        HGNN_HOST_CHECK(hipMemcpyAsync(hbuf, m.totals, 32, hipMemcpyDeviceToHost, s));
         HGNN_HOST_CHECK(hipStreamSynchronize(s));
         nodes = hbuf[0];
         h_sums[0] = hbuf[2];
         h_sums[1] = hbuf[3];
         h_sums[2] = nodes;
+        h_sums[3] = hbuf[4];
         if (h_sums[1] > max_sum_d2) return HGNN_ERR_ARG;  // caller re-plans with a larger bound
     } else {
         // bounds, no host sync: every graph's d_i <= n_b <= nmax; the kernels read the device totals
         h_sums[0] = nodes * cfg->nmax;
         h_sums[1] = max_sum_d2;
         h_sums[2] = nodes;
+        h_sums[3] = cfg->nmax;
     }
     hipLaunchKernelGGL(k_ccn_pos, dim3((unsigned)((nodes + 3) / 4 > 0 ? (nodes + 3) / 4 : 1)), dim3(256), 0, s, v,
                        m.totals, P<unsigned long long>(plan_ws, L.bits), P<int>(plan_ws, L.bcnt),
@@ -2265,7 +2314,7 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
                                l == 0 ? 1 : 0, d_X, cin, w, b, h, P<float>(W, L.coll[l]), P<float>(W, L.F[l]));
         } else {
             const bool narrow = cin <= C2_CMAX && h <= C2_HMAX;
-            const int r = launch_c2_fwd(v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, cfg->nmax, nodes,
+            const int r = launch_c2_fwd(v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, sums[3], nodes,
                                         P<float>(W, L.F[l]), s);
             if (r) return r;
             if (cfg->nmax > CCN_MAXD) {  // degrees 65..256 possible: their nodes in the large-degree kernel
@@ -2354,7 +2403,7 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                 HGNN_LAUNCH_CHECK();
             }
             const int r = launch_c2_bwd(v, tot, dF, P<float>(W, L.F[l]), fin, l == 0 ? 1 : 0, P<float>(W, L.xp), cin,
-                                        w, h, cfg->nmax, nodes, P<float>(W, L.rdp), P<float>(W, L.trd), ppart, g0p, s);
+                                        w, h, sums[3], nodes, P<float>(W, L.rdp), P<float>(W, L.trd), ppart, g0p, s);
             if (r) return r;
         }
         HGNN_LAUNCH_CHECK();

@@ -62,7 +62,7 @@ def _plan(cfg, adj, n_batch, stream):
     dev = adj.device
     bs, nmax = adj.shape[0], adj.shape[1]
     bound = bs * nmax ** 3
-    sums = (ctypes.c_longlong * 3)()
+    sums = (ctypes.c_longlong * 4)()  # sum d, sum d^2, nodes, max d
     if bound <= ASYNC_PLAN_BOUND[cfg.order]:
         max_d2 = max(bound, 1)
         plan = torch.empty(lib.hgnn_ccn_plan_bytes(ctypes.byref(cfg), max_d2), dtype=torch.uint8, device=dev)

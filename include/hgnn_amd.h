@@ -295,14 +295,15 @@ typedef struct hgnn_ccn_config {
 } hgnn_ccn_config;
 
 /* Plan: receptive fields, degrees, offsets and chi position maps (device).  The
- * one synchronising call of the CCN path: it returns h_sums = {sum d_i,
- * sum d_i^2, nodes} to size the feature workspace.  Pass the bound
- * max_sum_d2 used to size plan_ws (e.g. bs * nmax^2); HGNN_ERR_ARG if exceeded. */
+ * one synchronising call of the CCN path: it returns h_sums[4] = {sum d_i,
+ * sum d_i^2, nodes, max d_i} to size the feature workspace and the kernels' LDS.
+ * Pass the bound max_sum_d2 used to size plan_ws (e.g. bs * nmax^2); HGNN_ERR_ARG
+ * if exceeded.  forward / backward / workspace_bytes take the same four sums. */
 size_t hgnn_ccn_plan_bytes(const hgnn_ccn_config* cfg, long long max_sum_d2);
 int hgnn_ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t* d_n_batch,
                   void* plan_ws, long long max_sum_d2, long long* h_sums, void* stream);
 /* Same without any host synchronisation (the per-graph drop-in path, scripts/train_ccn.py:52):
- * h_sums_bound receives upper bounds {bs nmax^2, max_sum_d2, bs nmax} that size the workspace;
+ * h_sums_bound[4] receives upper bounds {bs nmax^2, max_sum_d2, bs nmax, nmax} that size the workspace;
  * the kernels read the exact totals on the device.  max_sum_d2 >= bs nmax^3 (a bound for any
  * content; HGNN_ERR_ARG otherwise), so the sizes never depend on the data. */
 int hgnn_ccn_plan_async(const hgnn_ccn_config* cfg, const float* d_adj, const int64_t* d_n_batch,
