@@ -376,20 +376,33 @@ __device__ __forceinline__ void c2_weights(float (*wc)[HC][CM], const float* __r
         const int o = t / CM, c = t % CM;
         const bool ok = o < hc && c < cin;
         const float* w = W + (long long)(o0 + (ok ? o : 0)) * K;
-        float a = 0.f;
-        if (ok) {
-            a = w[c];
-            for (int q = 6; q < 15; ++q) a += w[q * cin + c];
-        }
+        float r[18];
+#pragma unroll
+        for (int q = 0; q < 18; ++q) r[q] = ok ? w[q * cin + c] : 0.f;
+        float a = r[0];
+#pragma unroll
+        for (int q = 6; q < 15; ++q) a += r[q];
         wc[WA][o][c] = a;
-        wc[WB][o][c] = ok ? w[5 * cin + c] : 0.f;
-        wc[WQ1][o][c] = ok ? w[1 * cin + c] : 0.f;
-        wc[WQ2][o][c] = ok ? w[2 * cin + c] : 0.f;
-        wc[WQ3][o][c] = ok ? w[3 * cin + c] : 0.f;
-        wc[WQ4][o][c] = ok ? w[4 * cin + c] : 0.f;
-        wc[WQ15][o][c] = ok ? w[15 * cin + c] : 0.f;
-        wc[WQ16][o][c] = ok ? w[16 * cin + c] : 0.f;
-        wc[WQ17][o][c] = ok ? w[17 * cin + c] : 0.f;
+        wc[WB][o][c] = r[5];
+        wc[WQ1][o][c] = r[1];
+        wc[WQ2][o][c] = r[2];
+        wc[WQ3][o][c] = r[3];
+        wc[WQ4][o][c] = r[4];
+        wc[WQ15][o][c] = r[15];
+        wc[WQ16][o][c] = r[16];
+        wc[WQ17][o][c] = r[17];
+    }
+}
+
+// node i's position maps into LDS as int16, all loads of a thread in flight before the stores
+__device__ __forceinline__ void c2_copy_pos(const int* __restrict__ pos, int nn, short* sp) {
+    for (int e0 = threadIdx.x; e0 < nn; e0 += 256 * 8) {
+        int t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = e0 + k * 256 < nn ? pos[e0 + k * 256] : 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (e0 + k * 256 < nn) sp[e0 + k * 256] = (short)t[k];
     }
 }
 
@@ -402,7 +415,7 @@ __device__ __forceinline__ void c2_prologue(const CcnPlanView& v, int i, int n, 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int* ni = v.nbr + (long long)i * v.nmax;
     const long long o2 = v.off2[i];
-    for (int e = threadIdx.x; e < n * n; e += 256) sp[e] = (short)v.pos[o2 + e];
+    c2_copy_pos(v.pos + o2, n * n, sp);
     if ((int)threadIdx.x < n) {
         const int j = ni[threadIdx.x];
         s_oj[threadIdx.x] = v.off2[j];
@@ -894,7 +907,8 @@ __global__ void __launch_bounds__(256) k_ccn2_dx0(CcnPlanView v, const int* tota
 }
 
 // Backward of one CCN-2D level for the nodes of degree <= 64, block per node i:
-//   dp = dF * relu'(F_out) (written back in place of dF), rdp[x] = sum_y dp[x][y], tr = sum_x dp[x][x]
+//   dp = dF * relu'(F_out) (written back in place of dF; dF of the top level read straight from the readout's
+//   per-graph slice dtop when given), rdp[x] = sum_y dp[x][y], tr = sum_x dp[x][x]
 //   -- the "dp format" the gather kernels rebuild dT from (k_c2_gather);
 //   parameter partials  dW_q[o][c] = sum_xy dp[x][y][o] block_q[x][y][c], db[o] = sum dp, with
 //     P0 = sum dp Sc, P1 = sum_x rdp[x] q1[x], P2 = sum dp Sa, P3 = sum_x rdp[x] q3[x],
@@ -924,6 +938,7 @@ __device__ __forceinline__ void c2_write_partials(float* row, int cin, int c, fl
 constexpr int C2_NACC = 6;  // P0, P1, P2, P3, P15, P16
 template <int CM, int HC, int NB, bool L0>
 __global__ void __launch_bounds__(256) k_c2_bwd(CcnPlanView v, const int* total_nodes, float* __restrict__ dF,
+                                                const float* __restrict__ dtop, int dtop_ld,
                                                 const float* __restrict__ F, const float* __restrict__ fin,
                                                 const float* __restrict__ X, int cin,
                                                 const float* __restrict__ W, int h, int ncap,
@@ -950,6 +965,7 @@ __global__ void __launch_bounds__(256) k_c2_bwd(CcnPlanView v, const int* total_
     short* sp = reinterpret_cast<short*>(c2_dyn + ncap * ncap * HC);
     c2_prologue<CM>(v, i, n, L0 ? 1 : 0, X, cin, sp, vmask, s_oj, s_dj, s_x);
     const long long o2 = v.off2[i], o1 = v.off1[i];
+    const int gi = v.graph[i];
     const bool la = lane < n;
     const unsigned long long my_mask = la ? vmask[lane] : 0ull;
     const int my_oj = la ? s_oj[lane] : 0, my_dj = la ? s_dj[lane] : 0;
@@ -969,7 +985,7 @@ __global__ void __launch_bounds__(256) k_c2_bwd(CcnPlanView v, const int* total_
                 float d = 0.f;
                 if (o < hc) {
                     const long long r = (o2 + e) * h + o0 + o;
-                    d = F[r] > 0.f ? dF[r] : 0.f;
+                    d = F[r] > 0.f ? (dtop ? dtop[(long long)gi * dtop_ld + o0 + o] : dF[r]) : 0.f;
                     dF[r] = d;
                 }
                 dpL[e * HC + o] = d;
@@ -1203,20 +1219,21 @@ __device__ __forceinline__ void c2_dT_weights(float (*wc)[H][H], const float* __
         const int o = t / H, c = t % H;
         const bool ok = o < h && c < h;
         const float* w = W + (long long)(ok ? o : 0) * K;
-        float a = 0.f;
-        if (ok) {
-            a = w[c];
-            for (int q = 6; q < 15; ++q) a += w[q * h + c];
-        }
+        float r[18];
+#pragma unroll
+        for (int q = 0; q < 18; ++q) r[q] = ok ? w[q * h + c] : 0.f;
+        float a = r[0];
+#pragma unroll
+        for (int q = 6; q < 15; ++q) a += r[q];
         wc[WA][o][c] = a;
-        wc[WB][o][c] = ok ? w[5 * h + c] : 0.f;
-        wc[WQ1][o][c] = ok ? w[1 * h + c] : 0.f;
-        wc[WQ2][o][c] = ok ? w[2 * h + c] : 0.f;
-        wc[WQ3][o][c] = ok ? w[3 * h + c] : 0.f;
-        wc[WQ4][o][c] = ok ? w[4 * h + c] : 0.f;
-        wc[WQ15][o][c] = ok ? w[15 * h + c] : 0.f;
-        wc[WQ16][o][c] = ok ? w[16 * h + c] : 0.f;
-        wc[WQ17][o][c] = ok ? w[17 * h + c] : 0.f;
+        wc[WB][o][c] = r[5];
+        wc[WQ1][o][c] = r[1];
+        wc[WQ2][o][c] = r[2];
+        wc[WQ3][o][c] = r[3];
+        wc[WQ4][o][c] = r[4];
+        wc[WQ15][o][c] = r[15];
+        wc[WQ16][o][c] = r[16];
+        wc[WQ17][o][c] = r[17];
     }
 }
 
@@ -1287,7 +1304,7 @@ __global__ void __launch_bounds__(256) k_c2_gather(CcnPlanView v, const int* tot
     const int sj = v.selfpos[j];
     const int gr = v.graph[j];
     c2_dT_weights<H>(wc, W, h);
-    for (int e = threadIdx.x; e < n * n; e += 256) sp[e] = (short)v.pos[o2 + e];
+    c2_copy_pos(v.pos + o2, n * n, sp);
     if ((int)threadIdx.x < n) {
         const int i = nj[threadIdx.x];
         s_i[threadIdx.x] = i;
@@ -2129,34 +2146,35 @@ int launch_c2_fwd(const CcnPlanView& v, const int* tot, const float* fin, int le
 }
 
 template <int CM, int HC, int NB, bool L0>
-int launch_c2_bwd_t(const CcnPlanView& v, const int* tot, float* dF, const float* F, const float* fin, const float* X,
-                    int cin, const float* W, int h, int ncap, int nodes, float* rdp, float* trd, float* ppart,
-                    float* g0, hipStream_t s) {
+int launch_c2_bwd_t(const CcnPlanView& v, const int* tot, float* dF, const float* dtop, int dtop_ld, const float* F,
+                    const float* fin, const float* X, int cin, const float* W, int h, int ncap, int nodes, float* rdp,
+                    float* trd, float* ppart, float* g0, hipStream_t s) {
     const size_t lds = c2_dyn_lds(ncap, HC);
-    hipLaunchKernelGGL((k_c2_bwd<CM, HC, NB, L0>), dim3(nodes > 0 ? nodes : 1), dim3(256), lds, s, v, tot, dF, F, fin,
-                       X, cin, W, h, ncap, rdp, trd, ppart, g0);
+    hipLaunchKernelGGL((k_c2_bwd<CM, HC, NB, L0>), dim3(nodes > 0 ? nodes : 1), dim3(256), lds, s, v, tot, dF, dtop,
+                       dtop_ld, F, fin, X, cin, W, h, ncap, rdp, trd, ppart, g0);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
 }
 
-int launch_c2_bwd(const CcnPlanView& v, const int* tot, float* dF, const float* F, const float* fin, int level0,
+int launch_c2_bwd(const CcnPlanView& v, const int* tot, float* dF, const float* dtop, int dtop_ld, const float* F,
+                  const float* fin, int level0,
                   const float* X, int cin, const float* W, int h, long long dmax, int nodes, float* rdp, float* trd,
                   float* ppart, float* g0, hipStream_t s) {
     const int ncap = c2_ncap(dmax);
     if (level0) {
         if (cin <= 8)
-            return launch_c2_bwd_t<8, 2, 1, true>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
-        return launch_c2_bwd_t<16, 2, 1, true>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+            return launch_c2_bwd_t<8, 2, 1, true>(v, tot, dF, dtop, dtop_ld, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+        return launch_c2_bwd_t<16, 2, 1, true>(v, tot, dF, dtop, dtop_ld, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
     }
     if (cin <= 2)
-        return launch_c2_bwd_t<2, 2, 8, false>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+        return launch_c2_bwd_t<2, 2, 8, false>(v, tot, dF, dtop, dtop_ld, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
     if (cin <= 8)
-        return launch_c2_bwd_t<8, 2, 4, false>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
-    return launch_c2_bwd_t<16, 1, 2, false>(v, tot, dF, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+        return launch_c2_bwd_t<8, 2, 4, false>(v, tot, dF, dtop, dtop_ld, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
+    return launch_c2_bwd_t<16, 1, 2, false>(v, tot, dF, dtop, dtop_ld, F, fin, X, cin, W, h, ncap, nodes, rdp, trd, ppart, g0, s);
 }
 
 int launch_c2_gather(const CcnPlanView& v, const int* tot, const C2Dp& g, const float* W, int h, const float* dsum,
-                     int dsum_ld, int dsum_off, int nmax, int nodes, float* dout, hipStream_t s) {
+                     int dsum_ld, int dsum_off, long long dmax, int nodes, float* dout, hipStream_t s) {
     const dim3 grid(nodes > 0 ? nodes : 1);
     if (h <= 2)
         hipLaunchKernelGGL((k_c2_gather<2, 8>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
@@ -2165,7 +2183,7 @@ int launch_c2_gather(const CcnPlanView& v, const int* tot, const C2Dp& g, const 
     else
         hipLaunchKernelGGL((k_c2_gather<16, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
     HGNN_LAUNCH_CHECK();
-    if (nmax > C2_NCAP) {
+    if (dmax > C2_NCAP) {
         if (h <= 2)
             hipLaunchKernelGGL((k_c2_gather_big<2, 4>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld,
                                dsum_off, dout);
@@ -2317,7 +2335,7 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
             const int r = launch_c2_fwd(v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, sums[3], nodes,
                                         P<float>(W, L.F[l]), s);
             if (r) return r;
-            if (cfg->nmax > CCN_MAXD) {  // degrees 65..256 possible: their nodes in the large-degree kernel
+            if (sums[3] > CCN_MAXD) {  // degrees 65..256 present (or possible): their nodes in the large-degree kernel
                 if (narrow)
                     hipLaunchKernelGGL((k_ccn2_fwd_big<C2_CMAX, C2_HMAX>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s,
                                        v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, save_of(L, W, l),
@@ -2374,8 +2392,14 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
     // dF of the top level = readout broadcast of its slice of dsum
     float* dF = P<float>(W, L.dF[0]);
     float* dFn = P<float>(W, L.dF[1]);
-    hipLaunchKernelGGL(k_ccn_bcast, dim3(nb1), dim3(64), 0, s, v, tot, cfg->order, dsum, nf, f + (Lv - 1) * h, h, dF);
-    HGNN_LAUNCH_CHECK();
+    // CCN-2D without large-degree nodes: the top level's backward reads the broadcast slice of dsum itself
+    const bool bigd = cfg->order == 2 && sums[3] > CCN_MAXD;
+    const bool top_direct = cfg->order == 2 && !bigd;
+    if (!top_direct) {
+        hipLaunchKernelGGL(k_ccn_bcast, dim3(nb1), dim3(64), 0, s, v, tot, cfg->order, dsum, nf, f + (Lv - 1) * h, h,
+                           dF);
+        HGNN_LAUNCH_CHECK();
+    }
     for (int l = Lv - 1; l >= 0; --l) {
         const int cin = l == 0 ? f : h;
         const float* w = params[2 * l];
@@ -2388,7 +2412,7 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
             const bool narrow = cin <= C2_CMAX && h <= C2_HMAX;
             float* g0p = l == 0 ? P<float>(W, L.g0) : nullptr;
             const float* fin = l == 0 ? nullptr : P<float>(W, L.F[l - 1]);
-            if (cfg->nmax > CCN_MAXD) {  // the large-degree nodes read the raw dF: before the dp rewrite
+            if (bigd) {  // the large-degree nodes read the raw dF: before the dp rewrite
                 C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
                           P<float>(W, L.g_d3)};
                 if (narrow)
@@ -2402,8 +2426,10 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                                    P<float>(W, L.rdp), P<float>(W, L.trd));
                 HGNN_LAUNCH_CHECK();
             }
-            const int r = launch_c2_bwd(v, tot, dF, P<float>(W, L.F[l]), fin, l == 0 ? 1 : 0, P<float>(W, L.xp), cin,
-                                        w, h, sums[3], nodes, P<float>(W, L.rdp), P<float>(W, L.trd), ppart, g0p, s);
+            const float* dtop = top_direct && l == Lv - 1 ? dsum + f + (Lv - 1) * h : nullptr;
+            const int r = launch_c2_bwd(v, tot, dF, dtop, nf, P<float>(W, L.F[l]), fin, l == 0 ? 1 : 0,
+                                        P<float>(W, L.xp), cin, w, h, sums[3], nodes, P<float>(W, L.rdp),
+                                        P<float>(W, L.trd), ppart, g0p, s);
             if (r) return r;
         }
         HGNN_LAUNCH_CHECK();
@@ -2422,7 +2448,7 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                                    dst);
             } else {
                 const C2Dp g{dF, P<float>(W, L.rdp), P<float>(W, L.trd)};
-                const int r = launch_c2_gather(v, tot, g, w, h, dsum, nf, doff, cfg->nmax, nodes, dst, s);
+                const int r = launch_c2_gather(v, tot, g, w, h, dsum, nf, doff, sums[3], nodes, dst, s);
                 if (r) return r;
             }
         }
