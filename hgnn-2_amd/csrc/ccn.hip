@@ -451,24 +451,33 @@ __device__ __forceinline__ int lane_value_i(int v, int l) { return __builtin_amd
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // t[u][c] = T[a_u][b][lane] for a batch of NB neighbours (0 where lane is not in C_a or a_u < 0); lane a of
-// my_mask / my_oj / my_dj holds neighbour a's common-neighbourhood mask, 2-D row offset and degree
+// my_mask holds neighbour a's common-neighbourhood mask, lane a of my_row the row p_a(b) of F_{j_a}
+__device__ __forceinline__ const float* lane_value_ptr(const float* p, int l) {
+    const unsigned long long v = lane_value_u64((unsigned long long)(uintptr_t)p, l);
+    return reinterpret_cast<const float*>((uintptr_t)v);
+}
 template <int CM, int NB>
-__device__ __forceinline__ void c2_load_rows(const float* __restrict__ fin, int cin, int n, int b, const int (&aa)[NB],
-                                             const short* sp, unsigned long long my_mask, int my_oj, int my_dj,
-                                             float (&t)[NB][CM]) {
+__device__ __forceinline__ void c2_load_rows(int cin, int n, const int (&aa)[NB], const short* sp,
+                                             unsigned long long my_mask, const float* my_row, float (&t)[NB][CM]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
         const int a = aa[u] >= 0 ? aa[u] : 0;
         const bool vz = aa[u] >= 0 && ((lane_value_u64(my_mask, a) >> lane) & 1ull);
-        const int pb = uniform(max((int)sp[a * n + b], 0));
         const int pz = vz ? (int)sp[a * n + lane] : 0;
-        const float* q = fin + ((long long)lane_value_i(my_oj, a) + (long long)pb * lane_value_i(my_dj, a)) * cin;
+        const float* q = lane_value_ptr(my_row, a) + pz * cin;
 #pragma unroll
-        for (int c = 0; c < CM; ++c) t[u][c] = c < cin ? q[(long long)pz * cin + c] : 0.f;
+        for (int c = 0; c < CM; ++c) t[u][c] = c < cin ? q[c] : 0.f;
 #pragma unroll
         for (int c = 0; c < CM; ++c) t[u][c] = vz ? t[u][c] : 0.f;
     }
+}
+// lane a's row p_a(b) of F_{j_a} (a in A_b; any valid row otherwise)
+__device__ __forceinline__ const float* c2_row_of(const float* fin, int cin, const short* sp, int n, int b, bool in,
+                                                  int my_oj, int my_dj) {
+    const int lane = threadIdx.x & 63;
+    const int pb = in ? (int)sp[lane * n + b] : 0;
+    return fin + ((long long)my_oj + (long long)pb * my_dj) * cin;
 }
 
 template <int CM, int HC, int NB, bool L0>
@@ -568,7 +577,10 @@ __global__ void __launch_bounds__(256) k_c2_fwd(CcnPlanView v, const int* total_
                     as &= as - 1ull;
                     const bool vz = (lane_value_u64(my_mask, a) >> lane) & 1ull;
 #pragma unroll
-                    for (int o = 0; o < HC; ++o) s[o] += vz ? lane_value(bx[o], a) : 0.f;  // n W2 Sa[b][z]
+                    for (int o = 0; o < HC; ++o) {
+                        const float bxa = lane_value(bx[o], a);  // readlane outside any lane-dependent branch
+                        s[o] += vz ? bxa : 0.f;                  // n W2 Sa[b][z]
+                    }
                 }
                 if (la)
 #pragma unroll
@@ -580,51 +592,37 @@ __global__ void __launch_bounds__(256) k_c2_fwd(CcnPlanView v, const int* total_
                 for (int o = 0; o < HC; ++o) vacc[o] = 0.f;  // W1 q1[a] once (wave 0's copy)
         } else {
             for (int b = wv; b < n; b += 4) {
-                float sa[CM], sd[HC], ua[HC];
+                // lane a (a in A_b) keeps Sc[a][b], D1[a][b] = T[a][b][b] and D2[a][b] = T[a][b][a]; the
+                // projections through the weights follow once per row
+                float sa[CM], sck[CM], d1k[CM], d2k[CM];
 #pragma unroll
-                for (int c = 0; c < CM; ++c) sa[c] = 0.f;
-#pragma unroll
-                for (int o = 0; o < HC; ++o) sd[o] = ua[o] = 0.f;
+                for (int c = 0; c < CM; ++c) sa[c] = sck[c] = d1k[c] = d2k[c] = 0.f;
                 if (lane == 0)
 #pragma unroll
                     for (int c = 0; c < CM; ++c) d3s[b][c] = 0.f;
                 const unsigned long long ab = __ballot(la && ((my_mask >> b) & 1ull));
+                const bool in = (ab >> lane) & 1ull;
+                const float* my_row = c2_row_of(fin, cin, sp, n, b, in, my_oj, my_dj);
                 unsigned long long as = ab;
                 while (as) {
                     int aa[NB];
                     c2_take<NB>(as, aa);
                     float t[NB][CM];
-                    c2_load_rows<CM, NB>(fin, cin, n, b, aa, sp, my_mask, my_oj, my_dj, t);
+                    c2_load_rows<CM, NB>(cin, n, aa, sp, my_mask, my_row, t);
 #pragma unroll
                     for (int u = 0; u < NB; ++u) {
                         const int a = aa[u];
                         if (a < 0) break;
-                        float sc[CM], d1[CM];
+                        const bool me = lane == a;
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
-                            if (c >= cin) {
-                                sc[c] = d1[c] = 0.f;
-                                continue;
-                            }
-                            sc[c] = wave_total(t[u][c]);
-                            d1[c] = lane_value(t[u][c], b);
-                        }
-#pragma unroll
-                        for (int c = 0; c < CM; ++c) sa[c] += t[u][c];
-#pragma unroll
-                        for (int o = 0; o < HC; ++o) {
-                            float U = 0.f, V = 0.f, D = 0.f;
-#pragma unroll
-                            for (int c = 0; c < CM; ++c) {
-                                if (c >= cin) break;
-                                U = fmaf(fmaf(nf, wc[WA][o][c], wc[WB][o][c]), sc[c], U);
-                                U = fmaf(wc[WQ15][o][c], d1[c], U);
-                                V = fmaf(wc[WQ1][o][c], sc[c], V);
-                                D = fmaf(wc[WQ16][o][c], t[u][c], D);
-                            }
-                            ua[o] = lane == a ? U : ua[o];       // entry (a, b): alpha Sc + W15 D1
-                            vacc[o] += lane == a ? V : 0.f;     // q1[a]
-                            sd[o] += lane == a ? D : 0.f;       // entry (b, a): W16 D2[a][b]
+                            if (c >= cin) break;
+                            const float sc = wave_total(t[u][c]);
+                            const float d1 = lane_value(t[u][c], b);
+                            sck[c] = me ? sc : sck[c];
+                            d1k[c] = me ? d1 : d1k[c];
+                            d2k[c] = me ? t[u][c] : d2k[c];
+                            sa[c] += t[u][c];
                         }
                         if (a == b && lane == b)
 #pragma unroll
@@ -635,17 +633,21 @@ __global__ void __launch_bounds__(256) k_c2_fwd(CcnPlanView v, const int* total_
                 float q3[CM];
 #pragma unroll
                 for (int c = 0; c < CM; ++c) q3[c] = c < cin ? wave_total(sa[c]) : 0.f;
-                const bool in = (ab >> lane) & 1ull;
 #pragma unroll
                 for (int o = 0; o < HC; ++o) {
                     if (o >= hc) break;
-                    if (in) atomicAdd(&P[(lane * n + b) * HC + o], ua[o]);
-                    float S = sd[o];
+                    float U = 0.f, V = 0.f, S = 0.f;
 #pragma unroll
                     for (int c = 0; c < CM; ++c) {
                         if (c >= cin) break;
+                        U = fmaf(fmaf(nf, wc[WA][o][c], wc[WB][o][c]), sck[c], U);
+                        U = fmaf(wc[WQ15][o][c], d1k[c], U);
+                        V = fmaf(wc[WQ1][o][c], sck[c], V);
                         S = fmaf(nf * wc[WQ2][o][c], sa[c], S);
+                        S = fmaf(wc[WQ16][o][c], d2k[c], S);  // entry (b, a): W16 D2[a][b], lane a
                     }
+                    if (in) atomicAdd(&P[(lane * n + b) * HC + o], U);  // entry (a, b): alpha Sc + W15 D1
+                    vacc[o] += in ? V : 0.f;                            // q1[a]
                     if (la) atomicAdd(&P[(b * n + lane) * HC + o], S);
                     if (lane == 0) {
                         float q = 0.f;
@@ -1096,6 +1098,7 @@ __global__ void __launch_bounds__(256) k_c2_bwd(CcnPlanView v, const int* total_
 #pragma unroll
                 for (int c = 0; c < CM; ++c) sa[c] = 0.f;
                 unsigned long long as = __ballot(la && ((my_mask >> b) & 1ull));
+                const float* my_row = c2_row_of(fin, cin, sp, n, b, (as >> lane) & 1ull, my_oj, my_dj);
                 // lane a: dp[a][b], dp[b][a], rdp[a] of this row (read once, then by readlane)
                 float my_ab[HC], my_ba[HC], my_ra[HC];
 #pragma unroll
@@ -1108,7 +1111,7 @@ __global__ void __launch_bounds__(256) k_c2_bwd(CcnPlanView v, const int* total_
                     int aa[NB];
                     c2_take<NB>(as, aa);
                     float t[NB][CM];
-                    c2_load_rows<CM, NB>(fin, cin, n, b, aa, sp, my_mask, my_oj, my_dj, t);
+                    c2_load_rows<CM, NB>(cin, n, aa, sp, my_mask, my_row, t);
 #pragma unroll
                     for (int u = 0; u < NB; ++u) {
                         const int a = aa[u];
@@ -1340,55 +1343,88 @@ __global__ void __launch_bounds__(256) k_c2_gather(CcnPlanView v, const int* tot
         float acc[H];
 #pragma unroll
         for (int c = 0; c < H; ++c) acc[c] = 0.f;
-        // lanes a with u in C_a load the row-dependent uniform values of their neighbour at once:
-        // b = p_a(u), dp_i[aj][b], dp_i[b][aj], rdp_i[b]
+        // lanes a with u in C_a: b = p_a(u), and every part of dT_i[aj][b][.] that does not depend on z,
+        // projected through the weights once per row:
+        //   base = (n_i A + W5)^T dp[aj][b] + W1^T rdp[aj] + W3^T rdp[b] + W4^T tr,
+        //   e1 = W15^T dp[aj][b] (z = b), e2 = W16^T dp[b][aj] (z = aj), e3 = W17^T tr (aj = b = z);
+        // the walk then adds n_i W2^T dp[b][z] per lane
         const unsigned long long au = __ballot(la && ((my_mask >> u) & 1ull));
         const bool in = (au >> lane) & 1ull;
         const int my_b = in ? (int)sp[lane * n + u] : 0;
-        float my_ab[H], my_ba[H], my_rb[H];
+        const float nfi = (float)my_di;
+        float base[H], e1[H], e2[H], e3[H];
         {
             const float* pab = g.dp + ((long long)my_oi + (long long)my_aj * my_di + my_b) * h;
             const float* pba = g.dp + ((long long)my_oi + (long long)my_b * my_di + my_aj) * h;
             const float* prb = g.rdp + ((long long)my_o1 + my_b) * h;
+            float vab[H], vba[H], vrb[H];
 #pragma unroll
             for (int o = 0; o < H; ++o) {
-                my_ab[o] = (in && o < h) ? pab[o] : 0.f;
-                my_ba[o] = (in && o < h) ? pba[o] : 0.f;
-                my_rb[o] = (in && o < h) ? prb[o] : 0.f;
+                vab[o] = (in && o < h) ? pab[o] : 0.f;
+                vba[o] = (in && o < h) ? pba[o] : 0.f;
+                vrb[o] = (in && o < h) ? prb[o] : 0.f;
+            }
+#pragma unroll
+            for (int c = 0; c < H; ++c) {
+                float b0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f;
+#pragma unroll
+                for (int o = 0; o < H; ++o) {
+                    if (o >= h) break;
+                    b0 = fmaf(fmaf(nfi, wc[WA][o][c], wc[WB][o][c]), vab[o], b0);
+                    b0 = fmaf(wc[WQ1][o][c], my_ra[o], b0);
+                    b0 = fmaf(wc[WQ3][o][c], vrb[o], b0);
+                    b0 = fmaf(wc[WQ4][o][c], my_tr[o], b0);
+                    x1 = fmaf(wc[WQ15][o][c], vab[o], x1);
+                    x2 = fmaf(wc[WQ16][o][c], vba[o], x2);
+                    x3 = fmaf(wc[WQ17][o][c], my_tr[o], x3);
+                }
+                base[c] = b0;
+                e1[c] = x1;
+                e2[c] = x2;
+                e3[c] = x3;
             }
         }
+        const float* my_row = g.dp + ((long long)my_oi + (long long)my_b * my_di) * h;  // row b of dp_i
         // the neighbours a with u in C_a, ascending, NB at a time: one row piece dp_i[b][z] per lane each
         unsigned long long as = au;
         while (as) {
             int aa[NB];
             c2_take<NB>(as, aa);
-            float ld[NB][6][H];
-            int zb[NB], zz[NB], zd[NB], zj[NB];
+            float dz[NB][H];
+            int zz[NB];
             bool vz[NB];
 #pragma unroll
             for (int q = 0; q < NB; ++q) {
                 const int a = aa[q] >= 0 ? aa[q] : 0;
                 vz[q] = aa[q] >= 0 && ((lane_value_u64(my_mask, a) >> lane) & 1ull);
-                zb[q] = lane_value_i(my_b, a);
                 zz[q] = vz[q] ? (int)sp[a * n + lane] : 0;
-                zd[q] = lane_value_i(my_di, a);
-                zj[q] = lane_value_i(my_aj, a);
-                const float* pbz = g.dp + ((long long)lane_value_i(my_oi, a) + (long long)zb[q] * zd[q] + zz[q]) * h;
+                const float* pz = lane_value_ptr(my_row, a) + zz[q] * h;
 #pragma unroll
-                for (int o = 0; o < H; ++o) {
-                    ld[q][0][o] = lane_value(my_ab[o], a);
-                    ld[q][1][o] = lane_value(my_ba[o], a);
-                    ld[q][2][o] = lane_value(my_ra[o], a);
-                    ld[q][3][o] = lane_value(my_rb[o], a);
-                    ld[q][4][o] = lane_value(my_tr[o], a);
-                    ld[q][5][o] = o < h ? pbz[o] : 0.f;
-                }
+                for (int o = 0; o < H; ++o) dz[q][o] = o < h ? pz[o] : 0.f;
             }
 #pragma unroll
             for (int q = 0; q < NB; ++q) {
-                if (aa[q] < 0) break;
-                if (!vz[q]) continue;
-                c2_dT_add<H>(wc, ld[q], h, (float)zd[q], zj[q], zb[q], zz[q], acc);
+                const int a = aa[q];
+                if (a < 0) break;
+                const int b = lane_value_i(my_b, a), aj = lane_value_i(my_aj, a);
+                const float nfa = lane_value(nfi, a);
+                const bool f1 = zz[q] == b, f2 = zz[q] == aj, f3 = f1 && aj == b;
+#pragma unroll
+                for (int c = 0; c < H; ++c) {
+                    if (c >= h) break;
+                    float w2 = 0.f;
+#pragma unroll
+                    for (int o = 0; o < H; ++o) {
+                        if (o >= h) break;
+                        w2 = fmaf(wc[WQ2][o][c], dz[q][o], w2);
+                    }
+                    const float x1 = lane_value(e1[c], a), x2 = lane_value(e2[c], a), x3 = lane_value(e3[c], a);
+                    float t = fmaf(nfa, w2, lane_value(base[c], a));
+                    t += f1 ? x1 : 0.f;
+                    t += f2 ? x2 : 0.f;
+                    t += f3 ? x3 : 0.f;
+                    acc[c] += vz[q] ? t : 0.f;
+                }
             }
         }
         if (lane < n)
