@@ -484,7 +484,7 @@ template <int CM, int HC, int NB, bool L0>
 __global__ void __launch_bounds__(256) k_c2_fwd(CcnPlanView v, const int* total_nodes, const float* __restrict__ fin,
                                                 const float* __restrict__ X, int cin, const float* __restrict__ W,
                                                 const float* __restrict__ bias, int h, int ncap,
-                                                float* __restrict__ fout) {
+                                                float* __restrict__ fout, float* __restrict__ nsum) {
     extern __shared__ float c2_dyn[];
     __shared__ unsigned long long vmask[C2_NCAP];
     __shared__ int s_oj[C2_NCAP], s_dj[C2_NCAP];
@@ -495,6 +495,7 @@ __global__ void __launch_bounds__(256) k_c2_fwd(CcnPlanView v, const int* total_
     __shared__ float q3s[C2_NCAP][CM];    // q3[b] (tot = sum_b q3[b])
     __shared__ float d3s[C2_NCAP][CM];    // T[b][b][b]
     __shared__ float s_diag[HC];
+    __shared__ float s_ns[4][HC];
     const int i = blockIdx.x;
     if (i >= *total_nodes) return;
     const int n = v.deg[i];
@@ -680,6 +681,9 @@ __global__ void __launch_bounds__(256) k_c2_fwd(CcnPlanView v, const int* total_
 #pragma unroll
             for (int o = 0; o < HC; ++o) qw[wv][lane][o] = vacc[o];
         __syncthreads();
+        float ns[HC];  // this node's sum of F_out (the readout's per-level feature, model_ccn.py:102)
+#pragma unroll
+        for (int o = 0; o < HC; ++o) ns[o] = 0.f;
         for (int e = threadIdx.x; e < n * n; e += 256) {
             const int x = e / n, y = e - x * n;
 #pragma unroll
@@ -689,9 +693,20 @@ __global__ void __launch_bounds__(256) k_c2_fwd(CcnPlanView v, const int* total_
                 s += (qw[0][x][o] + qw[1][x][o]) + (qw[2][x][o] + qw[3][x][o]);
                 s += q3p[x][o];
                 if (x == y) s += s_diag[o];
-                fout[(o2 + e) * h + o0 + o] = s < 0.f ? 0.f : s;
+                s = s < 0.f ? 0.f : s;
+                fout[(o2 + e) * h + o0 + o] = s;
+                ns[o] += s;
             }
         }
+#pragma unroll
+        for (int o = 0; o < HC; ++o) {
+            const float t = wave_total(ns[o]);
+            if (lane == 0) s_ns[wv][o] = t;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < hc)
+            nsum[(long long)i * h + o0 + threadIdx.x] =
+                (s_ns[0][threadIdx.x] + s_ns[1][threadIdx.x]) + (s_ns[2][threadIdx.x] + s_ns[3][threadIdx.x]);
         __syncthreads();
     }
 }
@@ -1483,7 +1498,8 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd_big(CcnPlanView v, const int* 
                                                       const float* __restrict__ fin, int level0,
                                                       const float* __restrict__ X, int cin,
                                                       const float* __restrict__ W, const float* __restrict__ bias,
-                                                      int h, C2Save sv, float* __restrict__ fout) {
+                                                      int h, C2Save sv, float* __restrict__ fout,
+                                                      float* __restrict__ nsum) {
     __shared__ unsigned long long vmask[CCN_BIGD][CCN_BW];  // bit x of row a: x in C_a
     __shared__ int s_j[CCN_BIGD], s_dj[CCN_BIGD], s_oj[CCN_BIGD], s_mc[CCN_BIGD];
     __shared__ float sred[2][4][CM];
@@ -1690,6 +1706,9 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd_big(CcnPlanView v, const int* 
     __shared__ float sw[HM * 18 * CM];
     for (int t = threadIdx.x; t < h * K; t += 256) sw[t] = W[t];
     __syncthreads();
+    float ns[HM];  // this node's sum of F_out (readout)
+#pragma unroll
+    for (int o = 0; o < HM; ++o) ns[o] = 0.f;
     for (int e = threadIdx.x; e < n * n; e += 256) {
         const int x = e / n, y = e % n;
         float s[HM];
@@ -1721,9 +1740,21 @@ __global__ void __launch_bounds__(256) k_ccn2_fwd_big(CcnPlanView v, const int* 
 #pragma unroll
         for (int o = 0; o < HM; ++o) {
             if (o >= h) break;
-            fout[(o2 + e) * h + o] = s[o] < 0.f ? 0.f : s[o];
+            s[o] = s[o] < 0.f ? 0.f : s[o];
+            fout[(o2 + e) * h + o] = s[o];
+            ns[o] += s[o];
         }
     }
+    __shared__ float s_ns[4][HM];
+#pragma unroll
+    for (int o = 0; o < HM; ++o) {
+        const float t = wave_total(ns[o]);
+        if (lane == 0) s_ns[wv][o] = t;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < h)
+        nsum[(long long)i * h + threadIdx.x] =
+            (s_ns[0][threadIdx.x] + s_ns[1][threadIdx.x]) + (s_ns[2][threadIdx.x] + s_ns[3][threadIdx.x]);
 }
 
 // k_c2_gather for degrees 65..256: lane w of row u in 64-lane chunks, the neighbours a with u in C_a
@@ -1811,6 +1842,7 @@ __global__ void __launch_bounds__(256) k_c2_gather_big(CcnPlanView v, const int*
 // ------------------------------------------------------------------ readout
 // feat[b] = cat_l (sum over the graph's rows of F_l); level 0: sum_i d_i^order X[i]
 struct ReadoutArgs {
+    int per_node;         // F[l] holds per-node sums ([nodes][h], CCN-2D) instead of feature rows
     CcnPlanView v;
     int order, L, f, h, n_out, bs;
     const float* X;
@@ -1860,7 +1892,7 @@ __global__ void __launch_bounds__(256) k_ccn_readout_part(ReadoutArgs r, double*
         flush(acc, nc, c0);
     }
     for (int l = 0; l < r.L; ++l) {
-        const long long r0 = off[n0], r1 = off[n1];
+        const long long r0 = r.per_node ? n0 : off[n0], r1 = r.per_node ? n1 : off[n1];
         const long long len = r1 - r0, per = (len + RO_CH - 1) / RO_CH;
         const long long q0 = r0 + k * per, q1 = min(r1, q0 + per);
         for (int c0 = 0; c0 < r.h; c0 += C2_CMAX) {
@@ -2033,7 +2065,7 @@ struct CcnLayout {
     size_t node_off, deg, nbr, selfpos, graph, off1, off2, totals, err, bits, bcnt, pos;
     size_t plan_bytes;
     // feature workspace (needs sums)
-    std::vector<size_t> F, coll;    // per level 1..L
+    std::vector<size_t> F, coll, nsum;  // per level 1..L
     std::vector<C2Save> dummy;
     size_t sc[16], sa[16], d1[16], d2[16], q1[16], q3[16], tot[16], d3[16];
     size_t feat, rpart, g0, dsum, ppart, dF[2], dcoll, g_sc, g_sa, g_d1, g_d2, g_d3, xp, dxp, rdp, trd;
@@ -2076,11 +2108,13 @@ CcnLayout ccn_layout(const hgnn_ccn_config* c, long long sum_d, long long sum_d2
     const int h = c->hidden, f = c->f_in;
     L.F.resize(Lv);
     L.coll.resize(Lv);
+    L.nsum.resize(Lv);
     int cmax = f > h ? f : h;
     const bool big = c->order == 2 && c->nmax > CCN_MAXD;  // degrees above 64 possible
     for (int l = 0; l < Lv; ++l) {
         const int cin = l == 0 ? f : h;
         L.F[l] = take(4 * (size_t)rows * h);
+        if (c->order == 2) L.nsum[l] = take(4 * (size_t)nodes * h);
         if (c->order == 1) {
             L.coll[l] = take(4 * (size_t)rows * 2 * cin);
         } else if (big) {  // C2Save: only the large-degree kernels keep contraction statistics
@@ -2161,24 +2195,25 @@ int c2_ncap(long long dmax) { return dmax < C2_NCAP ? (int)(dmax > 1 ? dmax : 1)
 
 template <int CM, int HC, int NB, bool L0>
 int launch_c2_fwd_t(const CcnPlanView& v, const int* tot, const float* fin, const float* X, int cin, const float* W,
-                    const float* b, int h, int ncap, int nodes, float* fout, hipStream_t s) {
+                    const float* b, int h, int ncap, int nodes, float* fout, float* nsum, hipStream_t s) {
     const size_t lds = c2_dyn_lds(ncap, HC);
     hipLaunchKernelGGL((k_c2_fwd<CM, HC, NB, L0>), dim3(nodes > 0 ? nodes : 1), dim3(256), lds, s, v, tot, fin, X, cin,
-                       W, b, h, ncap, fout);
+                       W, b, h, ncap, fout, nsum);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
 }
 
 int launch_c2_fwd(const CcnPlanView& v, const int* tot, const float* fin, int level0, const float* X, int cin,
-                  const float* W, const float* b, int h, long long dmax, int nodes, float* fout, hipStream_t s) {
+                  const float* W, const float* b, int h, long long dmax, int nodes, float* fout, float* nsum,
+                  hipStream_t s) {
     const int ncap = c2_ncap(dmax);
     if (level0) {
-        if (cin <= 8) return launch_c2_fwd_t<8, 2, 1, true>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
-        return launch_c2_fwd_t<16, 2, 1, true>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
+        if (cin <= 8) return launch_c2_fwd_t<8, 2, 1, true>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, nsum, s);
+        return launch_c2_fwd_t<16, 2, 1, true>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, nsum, s);
     }
-    if (cin <= 2) return launch_c2_fwd_t<2, 2, 8, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
-    if (cin <= 8) return launch_c2_fwd_t<8, 2, 4, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
-    return launch_c2_fwd_t<16, 2, 2, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, s);
+    if (cin <= 2) return launch_c2_fwd_t<2, 2, 8, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, nsum, s);
+    if (cin <= 8) return launch_c2_fwd_t<8, 2, 4, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, nsum, s);
+    return launch_c2_fwd_t<16, 2, 2, false>(v, tot, fin, X, cin, W, b, h, ncap, nodes, fout, nsum, s);
 }
 
 template <int CM, int HC, int NB, bool L0>
@@ -2369,17 +2404,17 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
         } else {
             const bool narrow = cin <= C2_CMAX && h <= C2_HMAX;
             const int r = launch_c2_fwd(v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, sums[3], nodes,
-                                        P<float>(W, L.F[l]), s);
+                                        P<float>(W, L.F[l]), P<float>(W, L.nsum[l]), s);
             if (r) return r;
             if (sums[3] > CCN_MAXD) {  // degrees 65..256 present (or possible): their nodes in the large-degree kernel
                 if (narrow)
                     hipLaunchKernelGGL((k_ccn2_fwd_big<C2_CMAX, C2_HMAX>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s,
                                        v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, save_of(L, W, l),
-                                       P<float>(W, L.F[l]));
+                                       P<float>(W, L.F[l]), P<float>(W, L.nsum[l]));
                 else
                     hipLaunchKernelGGL((k_ccn2_fwd_big<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nodes > 0 ? nodes : 1),
                                        dim3(256), 0, s, v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h,
-                                       save_of(L, W, l), P<float>(W, L.F[l]));
+                                       save_of(L, W, l), P<float>(W, L.F[l]), P<float>(W, L.nsum[l]));
             }
         }
         HGNN_LAUNCH_CHECK();
@@ -2393,7 +2428,8 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
     ra.n_out = cfg->n_out;
     ra.bs = cfg->bs;
     ra.X = d_X;
-    for (int l = 0; l < cfg->layers; ++l) ra.F[l] = P<float>(W, L.F[l]);
+    ra.per_node = cfg->order == 2;  // CCN-2D: the forward kernels left each node's row sum
+    for (int l = 0; l < cfg->layers; ++l) ra.F[l] = P<float>(W, cfg->order == 2 ? L.nsum[l] : L.F[l]);
     ra.fcw = params[2 * cfg->layers];
     ra.fcb = params[2 * cfg->layers + 1];
     ra.feat = P<float>(W, L.feat);
