@@ -599,6 +599,20 @@ __global__ void __launch_bounds__(BN_SMALL_THREADS) k_bn_bwd_small(BnBwdArgs a) 
 // deterministic), and k_bn_bwd_fin disappears.  dbpart keeps its 64-row tiles.
 constexpr int BN2_THREADS = 1024, BN2_ROWS = 256;
 
+// sum over the 64 / L lane groups of a wave that hold the same channels (lanes t, t + L, ...): the
+// result is complete in lanes [0, L)
+template <int L>
+__device__ __forceinline__ float4 wave_groups_sum4(float4 v) {
+#pragma unroll
+    for (int o = L; o < 64; o <<= 1) {
+        v.x += __shfl_xor(v.x, o, 64);
+        v.y += __shfl_xor(v.y, o, 64);
+        v.z += __shfl_xor(v.z, o, 64);
+        v.w += __shfl_xor(v.w, o, 64);
+    }
+    return v;
+}
+
 __device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 template <int L>
@@ -645,20 +659,32 @@ __global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_part2(BnBwdArgs a) {
             }
         }
     }
-    // over the RG row groups, in order
-    __shared__ float4 red[BN2_THREADS];
-    float out[4] = {0.f, 0.f, 0.f, 0.f};
+    // over the RG row groups, in a fixed order: the 64 / L groups of a wave by shuffles, then the 16
+    // wave partials of all four statistics through LDS in one round (was four rounds of a 32-deep
+    // serial LDS walk)
+    constexpr int SR = L <= 32 ? 4 : 2;  // statistics per LDS round (32 KB)
+    __shared__ float4 red[SR][BN2_THREADS / 64][L];
+    const int wid = threadIdx.x >> 6;
     const int ch = threadIdx.x;  // < C: the channel this thread finishes
+    float out[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        red[threadIdx.x] = st[j];
+    for (int j = 0; j < 4; ++j) st[j] = wave_groups_sum4<L>(st[j]);
+#pragma unroll
+    for (int j0 = 0; j0 < 4; j0 += SR) {
+        if (j0 > 0) __syncthreads();
+#pragma unroll
+        for (int j = 0; j < SR; ++j)
+            if ((threadIdx.x & 63) < L) red[j][wid][lane] = st[j0 + j];
         __syncthreads();
         if (ch < C) {
-            float t = 0.f;
-            for (int q = 0; q < RG; ++q) t += f4c(red[q * L + (ch >> 2)], ch & 3);
-            out[j] = t;
+#pragma unroll
+            for (int j = 0; j < SR; ++j) {
+                float t = 0.f;
+#pragma unroll
+                for (int w = 0; w < BN2_THREADS / 64; ++w) t += f4c(red[j][w][ch >> 2], ch & 3);
+                out[j0 + j] = t;
+            }
         }
-        __syncthreads();
     }
     if (ch < C)
         *reinterpret_cast<float4*>(a.part + ((long long)tile * C + ch) * 4) = make_float4(out[0], out[1], out[2], out[3]);
@@ -675,8 +701,9 @@ __global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_apply2(BnBwdArgs a) {
     const int tiles = ceil_div(total, BN2_ROWS);
     // prologue: the per-channel sums over all tile partials, fp64, fixed order (thread (ch, sub)
     // sums tiles sub, sub + SUB, ...; then the SUB sub-sums in order)
-    __shared__ double2 pr[BN2_THREADS];
-    __shared__ double2 pt[BN2_THREADS];
+    __shared__ __attribute__((aligned(16))) double2 sbuf[2 * BN2_THREADS];  // prologue sums, then the dbpart reduction
+    double2* pr = sbuf;
+    double2* pt = sbuf + BN2_THREADS;
     __shared__ float sm1[C], sm2[C];
     {
         const int ch = threadIdx.x % C, sub = threadIdx.x / C;
@@ -776,22 +803,35 @@ __global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_apply2(BnBwdArgs a) {
         }
     }
     if (!a.dbpart) return;
-    // per-64-row-tile column sums of dY (the conv bias gradients), over the row groups in order
-    __shared__ float4 red[BN2_THREADS];
+    // per-64-row-tile column sums of dY (the conv bias gradients): every thread holds its rows' sums for
+    // the block's four tiles; over the row groups in a fixed order -- the lane groups of a wave by
+    // shuffles, then the 16 wave partials of all four tiles through LDS in one round
+    constexpr int NWV = BN2_THREADS / 64, QR = L <= 32 ? 4 : 2;  // tiles per LDS round (32 KB)
+    float4 (*red)[NWV][L] = reinterpret_cast<float4 (*)[NWV][L]>(sbuf);
+    const int wid = threadIdx.x >> 6;
     const int t64 = ceil_div(total, 64);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        red[threadIdx.x] = cs[q];
+    for (int q = 0; q < 4; ++q) cs[q] = wave_groups_sum4<L>(cs[q]);
+#pragma unroll
+    for (int q0 = 0; q0 < 4; q0 += QR) {
+        __syncthreads();  // the prologue's (or the previous round's) readers of sbuf are done
+#pragma unroll
+        for (int q = 0; q < QR; ++q)
+            if ((threadIdx.x & 63) < L) red[q][wid][lane] = cs[q0 + q];
         __syncthreads();
-        const int tq = blockIdx.x * 4 + q;
-        if (threadIdx.x < C && tq < t64) {
-            float t = 0.f;
-            for (int g = 0; g < RG; ++g) t += f4c(red[g * L + (threadIdx.x >> 2)], threadIdx.x & 3);
-            a.dbpart[(long long)tq * C + threadIdx.x] = t;
+        if (threadIdx.x < C) {
+#pragma unroll
+            for (int q = 0; q < QR; ++q) {
+                const int tq = blockIdx.x * 4 + q0 + q;
+                float t = 0.f;
+#pragma unroll
+                for (int w = 0; w < NWV; ++w) t += f4c(red[q][w][threadIdx.x >> 2], threadIdx.x & 3);
+                if (tq < t64) a.dbpart[(long long)tq * C + threadIdx.x] = t;
+            }
         }
-        __syncthreads();
     }
 }
+
 
 // ---- The same two-launch BN backward for narrow channel counts (c = 4L, L in {1, 2, 4}: the
 // GNN_simple layers of config 1).  256 rows per block, one row per lane group (256 L threads),
