@@ -845,16 +845,23 @@ int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int
     if (k % 4 != 0) return HGNN_ERR_UNSUPPORTED;  // pass the padded width (zero padding in both operands)
     if ((long long)m_cap * lda * 4 >= (1ll << 31) || (long long)n * ldw * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     // 32 x 16 wave tiles (v_mfma_f32_16x16x4_f32, LDS-DMA staging) when the 32 x 32-wave grid would
-    // leave the SIMDs unevenly loaded (under 2 waves per SIMD); HGNN_FWD_G5=0 never, 2 always
+    // leave the SIMDs unevenly loaded (under 2 waves per SIMD): the node halves.  Default (3): 64 x 32
+    // block tiles of 4 waves -- config 2's 9.7 K node rows make 608 blocks, 2-3 per CU, instead of
+    // 304 64 x 64 blocks of 8 waves that left 48 CUs with two blocks and the rest with one (22.2 vs
+    // 24.4 us per launch, same results bit for bit); HGNN_FWD_G5=1 the 64 x 64 tiles, 0 never, 2 always
     static const int g5 = [] {
         const char* e = getenv("HGNN_FWD_G5");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 3;
     }();
     const long long waves32 = (long long)ceil_div(m_cap, 64) * ceil_div(n, 64) * 4;
     if (mfma16 && g5 > 0 && n % 64 == 0 && n <= 512 && (g5 == 2 || waves32 < 2 * 1024)) {
         const int gx = ceil_div(ceil_div(m_cap, 64), 8) * 8;
-        hipLaunchKernelGGL((k_gemm5<64, 64, 2, 4, true>), dim3(gx, n / 64), dim3(512), 0, s, a, lda, wc, ldw,
-                           m_valid, m_cap, n, k, y, ldy, 1, bias, relu_from, bn_part);
+        if (g5 == 3)  // 64 x 32 tiles of 4 waves: twice the blocks, finer per-CU balance
+            hipLaunchKernelGGL((k_gemm5<64, 32, 2, 2, true>), dim3(gx, n / 32), dim3(256), 0, s, a, lda, wc, ldw,
+                               m_valid, m_cap, n, k, y, ldy, 1, bias, relu_from, bn_part);
+        else
+            hipLaunchKernelGGL((k_gemm5<64, 64, 2, 4, true>), dim3(gx, n / 64), dim3(512), 0, s, a, lda, wc, ldw,
+                               m_valid, m_cap, n, k, y, ldy, 1, bias, relu_from, bn_part);
         HGNN_LAUNCH_CHECK();
         return 0;
     }
