@@ -615,21 +615,25 @@ __device__ __forceinline__ float4 wave_groups_sum4(float4 v) {
 
 __device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
-template <int L>
+// LS: the row width in float4 (LS = L, or 2 L when a tile's channels are split over blockIdx.y: the
+// 256-channel layers of d = 128 read 512 KB per 256-row tile, too much for one CU's load pipeline --
+// two blocks per tile, each C = 4 L channels, write the same per-tile partials)
+template <int L, int LS = L>
 __global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_part2(BnBwdArgs a) {
-    constexpr int RG = BN2_THREADS / L, RPT = BN2_ROWS / RG, C = 4 * L;
+    constexpr int RG = BN2_THREADS / L, RPT = BN2_ROWS / RG, C = 4 * LS;
     const int tile = blockIdx.x;
     const int total = *a.total_rows;
     const int r0 = tile * BN2_ROWS;
     if (r0 >= total) return;
     const int r1 = min(total, r0 + BN2_ROWS);
     const float wv = *a.w;
+    const int c0 = blockIdx.y * 4 * L;  // first channel of this block
     const int lane = threadIdx.x % L, rg = threadIdx.x / L;
     float mu[4], isd[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        mu[i] = a.mean[4 * lane + i];
-        isd[i] = 1.0f / a.std[4 * lane + i];
+        mu[i] = a.mean[c0 + 4 * lane + i];
+        isd[i] = 1.0f / a.std[c0 + 4 * lane + i];
     }
     float4 st[4];
 #pragma unroll
@@ -641,8 +645,8 @@ __global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_part2(BnBwdArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const long long r = min(r0 + rg + RG * (i0 + u), r1 - 1);  // clamped: unconditional loads
-            dz[u] = ld4(a.dz + r * C + 4 * lane);
-            yv[u] = ld4(a.y + r * C + 4 * lane);
+            dz[u] = ld4(a.dz + r * C + c0 + 4 * lane);
+            yv[u] = ld4(a.y + r * C + c0 + 4 * lane);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -665,7 +669,7 @@ __global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_part2(BnBwdArgs a) {
     constexpr int SR = L <= 32 ? 4 : 2;  // statistics per LDS round (32 KB)
     __shared__ float4 red[SR][BN2_THREADS / 64][L];
     const int wid = threadIdx.x >> 6;
-    const int ch = threadIdx.x;  // < C: the channel this thread finishes
+    const int ch = threadIdx.x;  // < 4 L: the channel (of this block's slice) this thread finishes
     float out[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) st[j] = wave_groups_sum4<L>(st[j]);
@@ -676,7 +680,7 @@ __global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_part2(BnBwdArgs a) {
         for (int j = 0; j < SR; ++j)
             if ((threadIdx.x & 63) < L) red[j][wid][lane] = st[j0 + j];
         __syncthreads();
-        if (ch < C) {
+        if (ch < 4 * L) {
 #pragma unroll
             for (int j = 0; j < SR; ++j) {
                 float t = 0.f;
@@ -686,8 +690,9 @@ __global__ void __launch_bounds__(BN2_THREADS) k_bn_bwd_part2(BnBwdArgs a) {
             }
         }
     }
-    if (ch < C)
-        *reinterpret_cast<float4*>(a.part + ((long long)tile * C + ch) * 4) = make_float4(out[0], out[1], out[2], out[3]);
+    if (ch < 4 * L)
+        *reinterpret_cast<float4*>(a.part + ((long long)tile * C + c0 + ch) * 4) =
+            make_float4(out[0], out[1], out[2], out[3]);
 }
 
 template <int L>
@@ -993,7 +998,10 @@ static bool bn2_enabled() {
 template <int L>
 static void bn2_launch(const BnBwdArgs& a, hipStream_t s) {
     const int t2 = ceil_div(a.cap_rows, BN2_ROWS);
-    hipLaunchKernelGGL(k_bn_bwd_part2<L>, dim3(t2), dim3(BN2_THREADS), 0, s, a);
+    if constexpr (L == 64)  // 256 channels: two blocks of 128 per tile
+        hipLaunchKernelGGL((k_bn_bwd_part2<32, 64>), dim3(t2, 2), dim3(BN2_THREADS), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_bn_bwd_part2<L>, dim3(t2), dim3(BN2_THREADS), 0, s, a);
     hipLaunchKernelGGL(k_bn_bwd_apply2<L>, dim3(t2), dim3(BN2_THREADS), 0, s, a);
 }
 

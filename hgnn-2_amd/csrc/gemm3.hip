@@ -770,14 +770,21 @@ static int dw3_target_blocks() {
 
 int dw3_chunks(int r_cap, int o, int k) {
     const int tiles = ceil_div(o, 128) * ceil_div(k, 128);
-    int chunks = dw3_target_blocks() / (tiles > 0 ? tiles : 1);
+    // 256 blocks at config 2 (5 output tiles); twice that for the wide networks (config 4, d = 128: 20
+    // tiles, 3.39 -> 3.32 ms per step), whose main-stream kernels are long enough to leave room
+    const int target = getenv("HGNN_DW_BLOCKS") || tiles < 16 ? dw3_target_blocks() : 2 * dw3_target_blocks();
+    int chunks = target / (tiles > 0 ? tiles : 1);
     // never more chunks than 64-row pieces of the capacity; a multiple of 8 (XCD-aware order),
     // rounded DOWN so the grid stays within the target: standalone on the config-2 edge dW shape
     // (tools/dw_lab.hip) 48 chunks x 5 tiles = 240 blocks ran 41.5 us (0.58 of the fp32 MFMA peak),
     // 56 x 5 = 280 blocks (a second partial round on 24 CUs) 55 us
     chunks = std::min(chunks, ceil_div(r_cap > 0 ? r_cap : 1, 64));
-    chunks = chunks / 8 * 8;
-    return chunks < 8 ? 8 : chunks;
+    // a multiple of 8 keeps the XCD-aware order (launch_gemm3_dw); when rounding down would idle more
+    // than a fifth of the target (config 4: 20 output tiles, 12 -> 8 chunks = 160 blocks on 256 CUs)
+    // the exact count runs in the linear order instead
+    const int c8 = chunks / 8 * 8;
+    if (c8 >= 8 && 5 * c8 >= 4 * chunks) return c8;
+    return chunks < 1 ? 1 : chunks;
 }
 
 size_t dw3_slab_floats(int r_cap, int o, int k) { return (size_t)dw3_chunks(r_cap, o, k) * o * k; }
@@ -819,13 +826,13 @@ int launch_gemm3_da_bn(const BnBwdArgs& bn, const int* m_valid, int m_cap, int o
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
                     int nz, float* slabs, hipStream_t s) {
     if (r_cap <= 0) return 0;
-    if (nz <= 0 || nz % 8 != 0) return HGNN_ERR_ARG;
+    if (nz <= 0) return HGNN_ERR_ARG;
     static const bool xcd = [] {
         const char* e = getenv("HGNN_DW_XCD");
         return !e || e[0] != '0';
     }();
     hipLaunchKernelGGL((k_gemm3_tn<128, 128, 32, 4, 2>), dim3(ceil_div(o, 128), ceil_div(k, 128), nz), dim3(512), 0, s,
-                       dy, lddy, a, lda, slabs, o, k, r_valid, nz, xcd ? 1 : 0);
+                       dy, lddy, a, lda, slabs, o, k, r_valid, nz, xcd && nz % 8 == 0 ? 1 : 0);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
