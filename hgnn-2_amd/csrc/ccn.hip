@@ -34,6 +34,7 @@ constexpr int CCN_BW = CCN_BIGD / 64;
 // bit x of a multi-word set (CCN-2D common neighbourhoods of the large-degree kernels)
 __device__ __forceinline__ bool mbit(const unsigned long long* m, int x) { return (m[x >> 6] >> (x & 63)) & 1ull; }
 constexpr int CCN1_MAXD = 1024;  // CCN-1D degree bound (rows walked in 64-lane chunks; per-wave LDS row sums)
+constexpr int C1F = 8, C1H = 8;  // CCN-1D one-chunk fast path: channels (f_in / hidden) and outputs
 
 struct CcnPlanView {
     const int* node_off;   // (bs + 1)
@@ -217,6 +218,58 @@ __global__ void __launch_bounds__(256) k_ccn1_fwd(CcnPlanView v, const int* tota
     const int* pi = v.pos + v.off2[i];
     const long long r0 = v.off1[i];
     const int k2 = 2 * cin;
+    if (n <= 64 && cin <= C1F) {
+        // one chunk: lane x keeps its row sums and the column sum of neighbour a = x in registers, the
+        // four neighbours of a round load every channel at once (was one round trip per channel and a)
+        const int x = lane;
+        const bool vx = x < n;
+        float rs[C1F], colv[C1F];
+#pragma unroll
+        for (int c = 0; c < C1F; ++c) rs[c] = colv[c] = 0.f;
+        for (int a0 = 0; a0 < n; a0 += 4) {
+            float t[4][C1F];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int a = min(a0 + u, n - 1);
+                const int j = ni[a];
+                const int p = vx ? pi[(long long)a * n + x] : -1;
+                const bool ok = p >= 0 && a0 + u < n;
+                const float* src = level0 ? X + (long long)j * cin : fin + ((long long)v.off1[j] + max(p, 0)) * cin;
+#pragma unroll
+                for (int c = 0; c < C1F; ++c) t[u][c] = (c < cin && ok) ? src[c] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int a = a0 + u;
+                if (a >= n) break;
+#pragma unroll
+                for (int c = 0; c < C1F; ++c) {
+                    if (c >= cin) break;
+                    rs[c] += t[u][c];
+                    const float cs = wave_total(t[u][c]);
+                    colv[c] = lane == a ? cs : colv[c];
+                    if (lane == 0) coll[(r0 + a) * k2 + cin + c] = cs;
+                }
+            }
+        }
+        if (vx) {
+            const long long row = r0 + x;
+#pragma unroll
+            for (int c = 0; c < C1F; ++c)
+                if (c < cin) coll[row * k2 + c] = rs[c];
+            for (int o = 0; o < h; ++o) {
+                float s = bias[o];
+#pragma unroll
+                for (int c = 0; c < C1F; ++c)
+                    if (c < cin) s = fmaf(W[o * k2 + c], rs[c], s);
+#pragma unroll
+                for (int c = 0; c < C1F; ++c)
+                    if (c < cin) s = fmaf(W[o * k2 + cin + c], colv[c], s);
+                fout[row * h + o] = s < 0.f ? 0.f : s;
+            }
+        }
+        return;
+    }
     float* rs = srow[wv];  // wave-private; each position owned by one lane
     for (int c = 0; c < cin; ++c) {
         for (int x = lane; x < n; x += 64) rs[x] = 0.f;
@@ -263,6 +316,39 @@ __global__ void __launch_bounds__(256) k_ccn1_bwd_node(CcnPlanView v, const int*
     const long long r0 = v.off1[i];
     float* pp = ppart + (long long)i * (h * k2 + h);
     auto dpre = [&](long long row, int o) { return F[row * h + o] > 0.f ? dF[row * h + o] : 0.f; };
+    if (n <= 64 && cin <= C1F && h <= C1H) {  // one chunk: every value of lane x's row loaded once
+        const int x = lane;
+        const bool vx = x < n;
+        const long long row = r0 + x;
+        float dp[C1H], cl[2 * C1F];
+#pragma unroll
+        for (int o = 0; o < C1H; ++o) dp[o] = (vx && o < h) ? dpre(row, o) : 0.f;
+#pragma unroll
+        for (int k = 0; k < 2 * C1F; ++k) cl[k] = (vx && k < k2) ? coll[row * k2 + k] : 0.f;
+#pragma unroll
+        for (int o = 0; o < C1H; ++o) {
+            if (o >= h) break;
+#pragma unroll
+            for (int k = 0; k < 2 * C1F; ++k) {
+                if (k >= k2) break;
+                const float t = wave_total(dp[o] * cl[k]);
+                if (lane == 0) pp[o * k2 + k] = t;
+            }
+            const float sb = wave_total(dp[o]);
+            if (lane == 0) pp[h * k2 + o] = sb;
+        }
+        if (vx)
+#pragma unroll
+            for (int k = 0; k < 2 * C1F; ++k) {
+                if (k >= k2) break;
+                float t = 0.f;
+#pragma unroll
+                for (int o = 0; o < C1H; ++o)
+                    if (o < h) t = fmaf(W[o * k2 + k], dp[o], t);
+                dcoll[row * k2 + k] = t;
+            }
+        return;
+    }
     for (int o = 0; o < h; ++o) {
         for (int k = 0; k < k2; ++k) {
             float acc = 0.f;
@@ -301,6 +387,48 @@ __global__ void __launch_bounds__(256) k_ccn1_bwd_gather(CcnPlanView v, const in
     const int sj = v.selfpos[j];
     const int g = v.graph[j];
     const int k2 = 2 * cin;
+    if (n <= 64 && cin <= C1F) {  // one chunk: the indices of a neighbour once for every channel
+        const int u = lane;
+        const bool vu = u < n;
+        float acc[C1F];
+#pragma unroll
+        for (int c = 0; c < C1F; ++c) acc[c] = 0.f;
+        for (int a0 = 0; a0 < n; a0 += 4) {
+            float t1[4][C1F], t2[4][C1F];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int a = min(a0 + q, n - 1);
+                const int i = nj[a];
+                const int aj = pj[(long long)a * n + sj];
+                const int qq = vu ? pj[(long long)a * n + u] : -1;
+                const bool ok = qq >= 0 && a0 + q < n;
+                const long long ri = v.off1[i];
+                const float* s1 = dcoll + (ri + max(qq, 0)) * k2;
+                const float* s2 = dcoll + (ri + aj) * k2 + cin;
+#pragma unroll
+                for (int c = 0; c < C1F; ++c) {
+                    t1[q][c] = (c < cin && ok) ? s1[c] : 0.f;
+                    t2[q][c] = (c < cin && ok) ? s2[c] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int c = 0; c < C1F; ++c) acc[c] += t1[q][c] + t2[q][c];
+        }
+#pragma unroll
+        for (int c = 0; c < C1F; ++c) {
+            if (c >= cin) break;
+            const float rd = dsum ? dsum[(long long)g * dsum_ld + dsum_off + c] : 0.f;
+            if (level0) {
+                const float tot = wave_total(vu ? acc[c] : 0.f);
+                if (lane == 0) dout[(long long)j * cin + c] = tot + (float)n * rd;
+            } else if (vu) {
+                dout[((long long)v.off1[j] + u) * cin + c] = acc[c] + rd;
+            }
+        }
+        return;
+    }
     for (int c = 0; c < cin; ++c) {
         const float rd = dsum ? dsum[(long long)g * dsum_ld + dsum_off + c] : 0.f;
         float tot = 0.f;
@@ -1842,6 +1970,7 @@ __global__ void __launch_bounds__(256) k_c2_gather_big(CcnPlanView v, const int*
 // ------------------------------------------------------------------ readout
 // feat[b] = cat_l (sum over the graph's rows of F_l); level 0: sum_i d_i^order X[i]
 struct ReadoutArgs {
+    int nch;              // chunks per graph of k_ccn_readout_part
     int per_node;         // F[l] holds per-node sums ([nodes][h], CCN-2D) instead of feature rows
     CcnPlanView v;
     int order, L, f, h, n_out, bs;
@@ -1855,8 +1984,14 @@ struct ReadoutArgs {
 
 // Two stages so a graph's rows (Σd² of them per level on SBM-200: 261 K) are summed by many blocks:
 // part[b][k][col] over row chunk k of graph b (fp64, fixed order), then one block per graph adds
-// the RO_CH chunks and applies fc.
+// the chunks and applies fc.  Chunks per graph (gridDim.y of the first stage) from the rows per graph:
+// up to RO_CH for SBM-200-size levels, one for QM9-size graphs (a few hundred rows).
 constexpr int RO_CH = 32;
+int ro_chunks(long long rows, int bs) {
+    const long long per = bs > 0 ? rows / bs : rows;
+    const long long c = per / 4096 + 1;
+    return (int)(c < RO_CH ? c : RO_CH);
+}
 
 __global__ void __launch_bounds__(256) k_ccn_readout_part(ReadoutArgs r, double* __restrict__ part) {
     __shared__ double red[4][C2_CMAX];
@@ -1864,7 +1999,8 @@ __global__ void __launch_bounds__(256) k_ccn_readout_part(ReadoutArgs r, double*
     const int n0 = r.v.node_off[b], n1 = r.v.node_off[b + 1];
     const int* off = r.order == 1 ? r.v.off1 : r.v.off2;
     const int nf = r.f + r.L * r.h;
-    double* pb = part + ((long long)b * RO_CH + k) * nf;
+    const int nch = gridDim.y;
+    double* pb = part + ((long long)b * nch + k) * nf;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     auto flush = [&](double (&acc)[C2_CMAX], int nc, int col0) {
         for (int c = 0; c < nc; ++c) {
@@ -1882,7 +2018,7 @@ __global__ void __launch_bounds__(256) k_ccn_readout_part(ReadoutArgs r, double*
         const int nc = min(C2_CMAX, r.f - c0);
         double acc[C2_CMAX];
         for (int c = 0; c < C2_CMAX; ++c) acc[c] = 0.0;
-        const int len = n1 - n0, per = (len + RO_CH - 1) / RO_CH;
+        const int len = n1 - n0, per = (len + nch - 1) / nch;
         const int i0 = n0 + k * per, i1 = min(n1, i0 + per);
         for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) {
             const double d = r.v.deg[i];
@@ -1893,7 +2029,7 @@ __global__ void __launch_bounds__(256) k_ccn_readout_part(ReadoutArgs r, double*
     }
     for (int l = 0; l < r.L; ++l) {
         const long long r0 = r.per_node ? n0 : off[n0], r1 = r.per_node ? n1 : off[n1];
-        const long long len = r1 - r0, per = (len + RO_CH - 1) / RO_CH;
+        const long long len = r1 - r0, per = (len + nch - 1) / nch;
         const long long q0 = r0 + k * per, q1 = min(r1, q0 + per);
         for (int c0 = 0; c0 < r.h; c0 += C2_CMAX) {
             const int nc = min(C2_CMAX, r.h - c0);
@@ -1920,7 +2056,7 @@ __global__ void __launch_bounds__(256) k_ccn_readout(ReadoutArgs r, const double
     };
     for (int col = threadIdx.x; col < nf; col += 256) {
         double t = 0.0;
-        for (int k = 0; k < RO_CH; ++k) t += part[((long long)b * RO_CH + k) * nf + col];
+        for (int k = 0; k < r.nch; ++k) t += part[((long long)b * r.nch + k) * nf + col];
         feat[col] = (float)t;
     }
     __syncthreads();
@@ -1932,27 +2068,37 @@ __global__ void __launch_bounds__(256) k_ccn_readout(ReadoutArgs r, const double
     }
 }
 
-// dsum[b][k] = sum_o dout[b][o] fcw[o][k];  dfcw, dfcb summed over graphs (one block)
+// dsum[b][k] = sum_o dout[b][o] fcw[o][k] (blocks [0, nd)); dfcw[o][k], dfcb[o] summed over the graphs in
+// fp64, one wave per output (the remaining blocks; was one block doing all of it serially)
 __global__ void __launch_bounds__(256) k_ccn_readout_bwd(const float* __restrict__ dout, const float* __restrict__ feat,
                                                          const float* __restrict__ fcw, int bs, int n_out, int nf,
                                                          float* __restrict__ dsum, float* __restrict__ dfcw,
                                                          float* __restrict__ dfcb) {
-    for (int e = threadIdx.x; e < bs * nf; e += 256) {
-        const int b = e / nf, k = e % nf;
-        float s = 0.f;
-        for (int o = 0; o < n_out; ++o) s = fmaf(dout[b * n_out + o], fcw[o * nf + k], s);
-        dsum[e] = s;
+    const int nd = (bs * nf + 255) / 256;
+    if ((int)blockIdx.x < nd) {
+        const int e = blockIdx.x * 256 + threadIdx.x;
+        if (e < bs * nf) {
+            const int b = e / nf, k = e % nf;
+            float s = 0.f;
+            for (int o = 0; o < n_out; ++o) s = fmaf(dout[b * n_out + o], fcw[o * nf + k], s);
+            dsum[e] = s;
+        }
+        return;
     }
-    for (int e = threadIdx.x; e < n_out * nf; e += 256) {
-        const int o = e / nf, k = e % nf;
-        double s = 0.0;
-        for (int b = 0; b < bs; ++b) s += (double)dout[b * n_out + o] * (double)feat[(long long)b * nf + k];
-        dfcw[e] = (float)s;
+    const int w = ((int)blockIdx.x - nd) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w >= n_out * nf + n_out) return;
+    double s = 0.0;
+    if (w < n_out * nf) {
+        const int o = w / nf, k = w % nf;
+        for (int b = lane; b < bs; b += 64) s += (double)dout[b * n_out + o] * (double)feat[(long long)b * nf + k];
+    } else {
+        const int o = w - n_out * nf;
+        for (int b = lane; b < bs; b += 64) s += (double)dout[b * n_out + o];
     }
-    for (int o = threadIdx.x; o < n_out; o += 256) {
-        double s = 0.0;
-        for (int b = 0; b < bs; ++b) s += (double)dout[b * n_out + o];
-        dfcb[o] = (float)s;
+    s = wave_sum_d(s);
+    if (lane == 0) {
+        if (w < n_out * nf) dfcw[w] = (float)s;
+        else dfcb[w - n_out * nf] = (float)s;
     }
 }
 
@@ -2434,7 +2580,8 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
     ra.fcb = params[2 * cfg->layers + 1];
     ra.feat = P<float>(W, L.feat);
     ra.out = d_out;
-    hipLaunchKernelGGL(k_ccn_readout_part, dim3(cfg->bs, RO_CH), dim3(256), 0, s, ra, P<double>(W, L.rpart));
+    ra.nch = ro_chunks(cfg->order == 2 ? nodes : sums[0], cfg->bs);
+    hipLaunchKernelGGL(k_ccn_readout_part, dim3(cfg->bs, ra.nch), dim3(256), 0, s, ra, P<double>(W, L.rpart));
     HGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_ccn_readout, dim3(cfg->bs), dim3(256), 0, s, ra, P<double>(W, L.rpart));
     HGNN_LAUNCH_CHECK();
@@ -2455,8 +2602,10 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
     const int h = cfg->hidden, f = cfg->f_in, Lv = cfg->layers;
     const int nf = f + Lv * h;
     float* dsum = P<float>(W, L.dsum);
-    hipLaunchKernelGGL(k_ccn_readout_bwd, dim3(1), dim3(256), 0, s, d_dout, P<float>(W, L.feat), params[2 * Lv],
-                       cfg->bs, cfg->n_out, nf, dsum, grads[2 * Lv], grads[2 * Lv + 1]);
+    hipLaunchKernelGGL(k_ccn_readout_bwd,
+                       dim3((cfg->bs * nf + 255) / 256 + (cfg->n_out * nf + cfg->n_out + 3) / 4), dim3(256), 0, s,
+                       d_dout, P<float>(W, L.feat), params[2 * Lv], cfg->bs, cfg->n_out, nf, dsum, grads[2 * Lv],
+                       grads[2 * Lv + 1]);
     HGNN_LAUNCH_CHECK();
     const unsigned nb4 = nodes > 0 ? (unsigned)(nodes + 3) / 4 : 1u;
     const unsigned nb1 = nodes > 0 ? (unsigned)nodes : 1u;
