@@ -1,0 +1,601 @@
+// CCN-1D on small graphs (n <= 64 nodes): one workgroup per graph, the whole call in LDS.
+//
+// The reference's driver calls the network one graph at a time (scripts/train_ccn.py:31-73: net(X, A + I),
+// loss, backward and an optimizer step per graph), and QM9 graphs have at most 29 nodes: there the general
+// path (ccn.hip) spends the call on dispatches, not arithmetic (5 plan + 5 forward + 9 backward launches,
+// ~0.18 ms of GPU time and more of host time per graph).  Here one workgroup per graph
+//   * builds the receptive fields in LDS: row bit sets over the graph's nodes (utils_ccn.py:195-199,
+//     nbr_i = ascending nonzero(adj[i])), degrees, row offsets, and reads every chi position by popcount
+//     (index of u in N(j) = bits below u in j's row, utils_ccn.py:66-106),
+//   * runs every level (promotion + the two contractions + Linear + ReLU, utils_ccn.py:281-324) and the
+//     readout (model_ccn.py:50-64) -- forward: one dispatch,
+//   * backward: rebuilds the plan and the levels in LDS, then walks them back (one dispatch for one
+//     graph; a batch adds one reduction of the per-graph parameter partials).
+// Per level the arithmetic is the one-chunk path of k_ccn1_fwd / k_ccn1_bwd_node / k_ccn1_bwd_gather in
+// the same order, so forward values and input gradients are those of the general path; the weight
+// gradients are summed per lane over a wave's nodes, then over lanes and waves (fp32), where the general
+// path sums per node and then over nodes in fp64.
+#include "kernels.h"
+
+namespace hgnn {
+namespace {
+
+constexpr int CS_NT = 256, CS_NW = CS_NT / 64;
+constexpr int CS_CF = 8;                              // f_in and hidden bound
+constexpr int CS_LMAX = 15;
+constexpr int CS_NFMAX = CS_CF + CS_LMAX * CS_CF;     // readout width bound
+constexpr int CS_PMAX = CS_CF * 2 * CS_CF + CS_CF;    // one level's weight + bias entries
+constexpr size_t CS_FIXED = 512 + 256 + 272 + 4096 + 4 * CS_NW * CS_PMAX + 4 * CS_NFMAX + 8 * CS_NW * CS_CF;
+constexpr size_t CS_LDS_MAX = 150 * 1024;  // dynamic LDS opt-in (the forward also has a static word)
+
+struct CsArgs {
+    const float* adj;        // (bs, nmax, nmax) with self loops
+    const int64_t* n_batch;  // (bs,) or null: every graph has nmax nodes
+    const float* X;          // (bs, nmax, f)
+    int bs, nmax, f, h, L, n_out, rcap;  // rcap = nmax^2 bounds sum_i d_i of any graph
+    const float* W[CS_LMAX];
+    const float* B[CS_LMAX];
+    const float* fcw;
+    const float* fcb;
+    float* feat;             // [bs][nf] readout features (forward writes, backward reads)
+    float* out;              // (bs, n_out)
+    int* err;                // forward: atomicMax(err, tag * 256 + bits)
+    int tag;
+    const float* dout;       // backward
+    float* ppart;            // backward, bs > 1: [bs][ptot] level weight / bias partials, levels ascending
+    float* gW[CS_LMAX];      // backward, bs == 1: gradients written directly
+    float* gB[CS_LMAX];
+    float* gfcw;
+    float* gfcb;
+    float* dX;               // (bs, nmax, f), padding rows zeroed
+};
+
+struct CsLds {
+    unsigned long long* bits;  // [64] row bit sets
+    int* deg;                  // [64]
+    int* off1;                 // [65] exclusive prefix of deg
+    unsigned char* nbr;        // [64][64] ascending neighbour ids
+    float* red;                // [CS_NW][CS_PMAX]
+    float* vec;                // [CS_NFMAX] readout features (forward) / dsum (backward)
+    double* dred;              // [CS_NW][CS_CF]
+    float* F;                  // forward: 2 levels (ping-pong); backward: all L levels, [rcap][h] each
+    float* dcoll;              // backward: [rcap][2 cmax]
+    float* dF0;                // backward: [rcap][h] x 2
+    float* dF1;
+};
+
+__host__ __device__ inline size_t cs_lds_bytes(int rcap, int f, int h, int L, bool bwd) {
+    const int cmax = f > h ? f : h;
+    return CS_FIXED + 4 * (size_t)rcap * (bwd ? (size_t)h * L + 2 * cmax + 2 * h : 2 * (size_t)h);
+}
+
+__device__ inline CsLds cs_carve(char* base, const CsArgs& a, bool bwd) {
+    CsLds s;
+    size_t o = 0;
+    s.bits = reinterpret_cast<unsigned long long*>(base + o);
+    o += 512;
+    s.deg = reinterpret_cast<int*>(base + o);
+    o += 256;
+    s.off1 = reinterpret_cast<int*>(base + o);
+    o += 272;
+    s.nbr = reinterpret_cast<unsigned char*>(base + o);
+    o += 4096;
+    s.red = reinterpret_cast<float*>(base + o);
+    o += 4 * CS_NW * CS_PMAX;
+    s.vec = reinterpret_cast<float*>(base + o);
+    o += 4 * CS_NFMAX;
+    s.dred = reinterpret_cast<double*>(base + o);
+    o += 8 * CS_NW * CS_CF;
+    s.F = reinterpret_cast<float*>(base + o);
+    o += 4 * (size_t)a.rcap * a.h * (bwd ? a.L : 2);
+    s.dcoll = s.dF0 = s.dF1 = nullptr;
+    if (bwd) {
+        const int cmax = a.f > a.h ? a.f : a.h;
+        s.dcoll = reinterpret_cast<float*>(base + o);
+        o += 4 * (size_t)a.rcap * 2 * cmax;
+        s.dF0 = reinterpret_cast<float*>(base + o);
+        o += 4 * (size_t)a.rcap * a.h;
+        s.dF1 = reinterpret_cast<float*>(base + o);
+    }
+    return s;
+}
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
+    return v;
+}
+
+// Graph b's receptive fields: nbr, bits, deg, off1 in LDS.  Returns this lane's validation bits (self loop
+// missing, pattern not symmetric -- the general plan's ERR_CCN_SELFLOOP / ERR_CCN_ASYM).
+__device__ uint32_t cs_plan(const CsArgs& a, int b, int n, const CsLds& s) {
+    const float* A = a.adj + (long long)b * a.nmax * a.nmax;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t bad = 0;
+    for (int r = wv; r < n; r += CS_NW) {
+        const bool nz = lane < n && A[(long long)r * a.nmax + lane] > 0.f;  // utils_ccn.py:195 (A > 0)
+        const unsigned long long m = __ballot(nz);
+        if (nz) s.nbr[r * 64 + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned char)lane;
+        if (lane == 0) {
+            s.bits[r] = m;
+            s.deg[r] = __popcll(m);
+        }
+        if (!((m >> r) & 1ull)) bad |= ERR_CCN_SELFLOOP;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        const int d = lane < n ? s.deg[lane] : 0;
+        int x = d;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(x, o, 64);
+            if (lane >= o) x += t;
+        }
+        s.off1[lane] = x - d;
+        if (lane == 63) s.off1[64] = x;
+    }
+    // every neighbour j of r must list r (the backward gathers node j's readers from N(j))
+    for (int r = wv; r < n; r += CS_NW) {
+        const unsigned long long m = s.bits[r];
+        if (lane < n && ((m >> lane) & 1ull) && !((s.bits[lane] >> r) & 1ull)) bad |= ERR_CCN_ASYM;
+    }
+    __syncthreads();
+    return bad;
+}
+
+// Node i, lane x = receptive-field position: rs[c] = sum_a T[a][x][c] and colv[c] = the column sum of
+// neighbour a = x, T[a][x] = F_{j_a}[pos(nbr_i[x] in N(j_a))] (level 0: X[j_a] when present) -- the
+// order of k_ccn1_fwd's one-chunk path.
+template <int CF>
+__device__ __forceinline__ void cs_collect(const CsLds& s, int i, const float* __restrict__ Xg, const float* Fin,
+                                           int cin, float (&rs)[CF], float (&colv)[CF]) {
+    const int lane = threadIdx.x & 63;
+    const int d = s.deg[i];
+    const bool vx = lane < d;
+    const int u = vx ? s.nbr[i * 64 + lane] : 0;
+    const unsigned long long below = (1ull << u) - 1ull;
+#pragma unroll
+    for (int c = 0; c < CF; ++c) rs[c] = colv[c] = 0.f;
+    for (int a0 = 0; a0 < d; a0 += 4) {
+        float t[4][CF];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int a = min(a0 + q, d - 1);
+            const int j = s.nbr[i * 64 + a];
+            const unsigned long long m = s.bits[j];
+            const bool ok = vx && ((m >> u) & 1ull) && a0 + q < d;
+            const float* src = Fin ? Fin + (s.off1[j] + __popcll(m & below)) * cin : Xg + j * cin;
+#pragma unroll
+            for (int c = 0; c < CF; ++c) t[q][c] = (c < cin && ok) ? src[c] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int a = a0 + q;
+            if (a >= d) break;
+#pragma unroll
+            for (int c = 0; c < CF; ++c) {
+                if (c >= cin) break;
+                rs[c] += t[q][c];
+                const float cs = wave_total(t[q][c]);
+                colv[c] = lane == a ? cs : colv[c];
+            }
+        }
+    }
+}
+
+// F_l rows of node i: relu(b + W [rs | colv]) in k_ccn1_fwd's order
+template <int CF>
+__device__ __forceinline__ void cs_update(const CsLds& s, int i, const float (&rs)[CF], const float (&colv)[CF],
+                                          int cin, const float* __restrict__ W, const float* __restrict__ bias, int h,
+                                          float* Fout) {
+    const int lane = threadIdx.x & 63;
+    if (lane >= s.deg[i]) return;
+    const int k2 = 2 * cin;
+    const int row = s.off1[i] + lane;
+    for (int o = 0; o < h; ++o) {
+        float v = bias[o];
+#pragma unroll
+        for (int c = 0; c < CF; ++c)
+            if (c < cin) v = fmaf(W[o * k2 + c], rs[c], v);
+#pragma unroll
+        for (int c = 0; c < CF; ++c)
+            if (c < cin) v = fmaf(W[o * k2 + cin + c], colv[c], v);
+        Fout[row * h + o] = v < 0.f ? 0.f : v;
+    }
+}
+
+// Readout column sums in fp64 (k_ccn_readout_part's order for a one-chunk graph): vec[col0 + c] =
+// sum over rows r of val(r, c), rows over the 256 threads, then the waves.
+template <int CF, typename V>
+__device__ __forceinline__ void cs_colsum(const CsLds& s, int rows, int C, int col0, V val) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double acc[CF];
+#pragma unroll
+    for (int c = 0; c < CF; ++c) acc[c] = 0.0;
+    for (int r = threadIdx.x; r < rows; r += CS_NT)
+#pragma unroll
+        for (int c = 0; c < CF; ++c)
+            if (c < C) acc[c] += val(r, c);
+#pragma unroll
+    for (int c = 0; c < CF; ++c) {
+        if (c >= C) break;
+        const double t = wave_sum_d(acc[c]);
+        if (lane == 0) s.dred[wv * CS_CF + c] = t;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < C) {
+        const int c = threadIdx.x;
+        s.vec[col0 + c] = (float)(s.dred[c] + s.dred[CS_CF + c] + s.dred[2 * CS_CF + c] + s.dred[3 * CS_CF + c]);
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int cs_nodes(const CsArgs& a, int b, uint32_t& bad) {
+    int n = a.n_batch ? (int)a.n_batch[b] : a.nmax;
+    if (n < 0 || n > a.nmax) {
+        bad |= ERR_SIZES;
+        n = n < 0 ? 0 : a.nmax;
+    }
+    return n;
+}
+
+template <int CF>
+__global__ void __launch_bounds__(CS_NT) k_ccn1_small_fwd(CsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    __shared__ uint32_t sbad;
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const CsLds s = cs_carve(lds, a, false);
+    if (threadIdx.x == 0) sbad = 0;
+    uint32_t bad = 0;
+    const int n = cs_nodes(a, b, bad);
+    bad |= cs_plan(a, b, n, s);
+    const float* Xg = a.X + (long long)b * a.nmax * a.f;
+    const int h = a.h, f = a.f, nf = f + a.L * h;
+    // level 0 of the readout: sum_i d_i X[i]  (utils_ccn.py:212-216 tiles X[i] d_i times)
+    cs_colsum<CF>(s, n, f, 0, [&](int r, int c) { return (double)s.deg[r] * (double)Xg[r * f + c]; });
+    const int rows = s.off1[n];
+    const float* fin = nullptr;
+    for (int l = 0; l < a.L; ++l) {
+        const int cin = l == 0 ? f : h;
+        float* fout = s.F + (size_t)(l & 1) * a.rcap * h;
+        for (int i = wv; i < n; i += CS_NW) {
+            float rs[CF], colv[CF];
+            cs_collect<CF>(s, i, Xg, fin, cin, rs, colv);
+            cs_update<CF>(s, i, rs, colv, cin, a.W[l], a.B[l], h, fout);
+        }
+        __syncthreads();
+        cs_colsum<CF>(s, rows, h, f + l * h, [&](int r, int c) { return (double)fout[r * h + c]; });
+        fin = fout;
+    }
+    for (int k = threadIdx.x; k < nf; k += CS_NT) a.feat[(long long)b * nf + k] = s.vec[k];
+    // out = fc(feat) in fp64 (k_ccn_readout's order)
+    for (int o = 0; o < a.n_out; ++o) {
+        double acc = 0.0;
+        for (int k = threadIdx.x; k < nf; k += CS_NT) acc += (double)a.fcw[o * nf + k] * (double)s.vec[k];
+        acc = wave_sum_d(acc);
+        __syncthreads();
+        if (lane == 0) s.dred[wv] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            a.out[(long long)b * a.n_out + o] = (float)(s.dred[0] + s.dred[1] + s.dred[2] + s.dred[3] + (double)a.fcb[o]);
+    }
+    bad = wave_or(bad);
+    if (lane == 0 && bad) atomicOr(&sbad, bad);
+    __syncthreads();
+    if (threadIdx.x == 0 && sbad) atomicMax(a.err, a.tag * 256 + (int)sbad);
+}
+
+template <int CF, int CH>
+__global__ void __launch_bounds__(CS_NT) k_ccn1_small_bwd(CsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const CsLds s = cs_carve(lds, a, true);
+    uint32_t bad = 0;
+    const int n = cs_nodes(a, b, bad);
+    (void)cs_plan(a, b, n, s);  // the forward reported the batch's validation bits
+    const float* Xg = a.X + (long long)b * a.nmax * a.f;
+    const int h = a.h, f = a.f, L = a.L, nf = f + L * h;
+    // the levels again, all kept
+    for (int l = 0; l < L; ++l) {
+        const int cin = l == 0 ? f : h;
+        const float* fin = l == 0 ? nullptr : s.F + (size_t)(l - 1) * a.rcap * h;
+        float* fout = s.F + (size_t)l * a.rcap * h;
+        for (int i = wv; i < n; i += CS_NW) {
+            float rs[CF], colv[CF];
+            cs_collect<CF>(s, i, Xg, fin, cin, rs, colv);
+            cs_update<CF>(s, i, rs, colv, cin, a.W[l], a.B[l], h, fout);
+        }
+        __syncthreads();
+    }
+    // dsum[k] = sum_o dout[b][o] fcw[o][k] (k_ccn_readout_bwd's order); one graph: the fc gradients here
+    const float* dob = a.dout + (long long)b * a.n_out;
+    for (int k = threadIdx.x; k < nf; k += CS_NT) {
+        float t = 0.f;
+        for (int o = 0; o < a.n_out; ++o) t = fmaf(dob[o], a.fcw[o * nf + k], t);
+        s.vec[k] = t;
+    }
+    if (a.bs == 1)
+        for (int w = threadIdx.x; w < a.n_out * nf + a.n_out; w += CS_NT) {
+            if (w < a.n_out * nf) a.gfcw[w] = (float)((double)dob[w / nf] * (double)a.feat[w % nf]);
+            else a.gfcb[w - a.n_out * nf] = (float)(double)dob[w - a.n_out * nf];
+        }
+    __syncthreads();
+    const int p0 = h * 2 * f + h, p1 = h * 2 * h + h;
+    float* dFc = s.dF0;
+    float* dFn = s.dF1;
+    for (int l = L - 1; l >= 0; --l) {
+        const int cin = l == 0 ? f : h, k2 = 2 * cin;
+        const float* W = a.W[l];
+        const float* Fl = s.F + (size_t)l * a.rcap * h;
+        const float* fin = l == 0 ? nullptr : s.F + (size_t)(l - 1) * a.rcap * h;
+        const bool top = l == L - 1;
+        const float* dtop = s.vec + f + (L - 1) * h;
+        // node pass: dpre = dF relu', per-lane parameter sums, dcoll = W^T dpre (k_ccn1_bwd_node's order)
+        float aw[CH][CF], ac[CH][CF], ab[CH];
+#pragma unroll
+        for (int o = 0; o < CH; ++o) {
+            ab[o] = 0.f;
+#pragma unroll
+            for (int c = 0; c < CF; ++c) aw[o][c] = ac[o][c] = 0.f;
+        }
+        for (int i = wv; i < n; i += CS_NW) {
+            float rs[CF], colv[CF];
+            cs_collect<CF>(s, i, Xg, fin, cin, rs, colv);
+            const bool vx = lane < s.deg[i];
+            const int row = s.off1[i] + lane;
+            float dp[CH];
+#pragma unroll
+            for (int o = 0; o < CH; ++o) {
+                dp[o] = 0.f;
+                if (vx && o < h) {
+                    const float g = top ? dtop[o] : dFc[row * h + o];
+                    dp[o] = Fl[row * h + o] > 0.f ? g : 0.f;
+                }
+                ab[o] += dp[o];
+#pragma unroll
+                for (int c = 0; c < CF; ++c) {
+                    aw[o][c] = fmaf(dp[o], rs[c], aw[o][c]);
+                    ac[o][c] = fmaf(dp[o], colv[c], ac[o][c]);
+                }
+            }
+            if (vx)
+                for (int k = 0; k < k2; ++k) {
+                    float t = 0.f;
+#pragma unroll
+                    for (int o = 0; o < CH; ++o)
+                        if (o < h) t = fmaf(W[o * k2 + k], dp[o], t);
+                    s.dcoll[row * k2 + k] = t;
+                }
+        }
+        // level parameter gradients: lanes, then the waves in order
+#pragma unroll
+        for (int o = 0; o < CH; ++o) {
+            if (o >= h) break;
+#pragma unroll
+            for (int c = 0; c < CF; ++c) {
+                if (c >= cin) break;
+                const float tw = wave_total(aw[o][c]);
+                const float tc = wave_total(ac[o][c]);
+                if (lane == 0) {
+                    s.red[wv * CS_PMAX + o * k2 + c] = tw;
+                    s.red[wv * CS_PMAX + o * k2 + cin + c] = tc;
+                }
+            }
+            const float tb = wave_total(ab[o]);
+            if (lane == 0) s.red[wv * CS_PMAX + h * k2 + o] = tb;
+        }
+        __syncthreads();
+        const int P = h * k2 + h;
+        for (int p = threadIdx.x; p < P; p += CS_NT) {
+            const float v = s.red[p] + s.red[CS_PMAX + p] + s.red[2 * CS_PMAX + p] + s.red[3 * CS_PMAX + p];
+            if (a.bs == 1) {
+                if (p < h * k2) a.gW[l][p] = v;
+                else a.gB[l][p - h * k2] = v;
+            } else {
+                const int poff = l == 0 ? 0 : p0 + (l - 1) * p1;
+                a.ppart[(long long)b * (p0 + (L - 1) * p1) + poff + p] = v;
+            }
+        }
+        // gather: dF_{l-1}[j][u] = sum_{i in N(j)} [q valid] (drow_i[q] + dcol_i[pos of j]) + readout term;
+        // level 0: dX[j] = the sum over u + d_j dsum  (k_ccn1_bwd_gather's order)
+        for (int j = wv; j < n; j += CS_NW) {
+            const int d = s.deg[j];
+            const bool vu = lane < d;
+            const int uu = vu ? s.nbr[j * 64 + lane] : 0;
+            const unsigned long long bu = (1ull << uu) - 1ull, bj = (1ull << j) - 1ull;
+            float acc[CF];
+#pragma unroll
+            for (int c = 0; c < CF; ++c) acc[c] = 0.f;
+            for (int a0 = 0; a0 < d; a0 += 4) {
+                float t1[4][CF], t2[4][CF];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int ai = min(a0 + q, d - 1);
+                    const int i = s.nbr[j * 64 + ai];
+                    const unsigned long long m = s.bits[i];
+                    const bool ok = vu && ((m >> uu) & 1ull) && a0 + q < d;
+                    const int ri = s.off1[i];
+                    const float* s1 = s.dcoll + (ri + __popcll(m & bu)) * k2;
+                    const float* s2 = s.dcoll + (ri + __popcll(m & bj)) * k2 + cin;
+#pragma unroll
+                    for (int c = 0; c < CF; ++c) {
+                        t1[q][c] = (c < cin && ok) ? s1[c] : 0.f;
+                        t2[q][c] = (c < cin && ok) ? s2[c] : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int c = 0; c < CF; ++c) acc[c] += t1[q][c] + t2[q][c];
+            }
+            if (l > 0) {
+                if (vu)
+#pragma unroll
+                    for (int c = 0; c < CF; ++c)
+                        if (c < cin) dFn[(s.off1[j] + lane) * cin + c] = acc[c] + s.vec[f + (l - 1) * h + c];
+            } else {
+#pragma unroll
+                for (int c = 0; c < CF; ++c) {
+                    if (c >= cin) break;
+                    const float tot = wave_total(vu ? acc[c] : 0.f);
+                    if (lane == 0) a.dX[((long long)b * a.nmax + j) * f + c] = tot + (float)d * s.vec[c];
+                }
+            }
+        }
+        __syncthreads();
+        float* t = dFc;
+        dFc = dFn;
+        dFn = t;
+    }
+    for (int e = threadIdx.x; e < (a.nmax - n) * f; e += CS_NT) a.dX[((long long)b * a.nmax + n) * f + e] = 0.f;
+}
+
+// Batches: parameter gradient = sum over graphs in fp64, one wave per entry (the level entries, then fc
+// weight and bias from dout and the readout features, k_ccn_readout_bwd's order).
+__global__ void __launch_bounds__(256) k_ccn1_small_reduce(CsArgs a) {
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int h = a.h, f = a.f, L = a.L, nf = f + L * h;
+    const int p0 = h * 2 * f + h, p1 = h * 2 * h + h, ptot = p0 + (L - 1) * p1;
+    if (w >= ptot + a.n_out * nf + a.n_out) return;
+    double s = 0.0;
+    if (w < ptot) {
+        for (int b = lane; b < a.bs; b += 64) s += (double)a.ppart[(long long)b * ptot + w];
+    } else if (w < ptot + a.n_out * nf) {
+        const int o = (w - ptot) / nf, k = (w - ptot) % nf;
+        for (int b = lane; b < a.bs; b += 64) s += (double)a.dout[b * a.n_out + o] * (double)a.feat[(long long)b * nf + k];
+    } else {
+        const int o = w - ptot - a.n_out * nf;
+        for (int b = lane; b < a.bs; b += 64) s += (double)a.dout[b * a.n_out + o];
+    }
+    s = wave_sum_d(s);
+    if (lane != 0) return;
+    if (w < ptot) {
+        const int l = w < p0 ? 0 : 1 + (w - p0) / p1;
+        const int p = l == 0 ? w : (w - p0) % p1;
+        const int k2 = 2 * (l == 0 ? f : h);
+        if (p < h * k2) a.gW[l][p] = (float)s;
+        else a.gB[l][p - h * k2] = (float)s;
+    } else if (w < ptot + a.n_out * nf) {
+        a.gfcw[w - ptot] = (float)s;
+    } else {
+        a.gfcb[w - ptot - a.n_out * nf] = (float)s;
+    }
+}
+
+bool cs_ok(const hgnn_ccn_config* c) {
+    return c && c->order == 1 && c->bs > 0 && c->nmax > 0 && c->nmax <= 64 && c->f_in > 0 && c->f_in <= CS_CF &&
+           c->hidden > 0 && c->hidden <= CS_CF && c->layers >= 1 && c->layers <= CS_LMAX && c->n_out > 0 &&
+           cs_lds_bytes(c->nmax * c->nmax, c->f_in, c->hidden, c->layers, true) <= CS_LDS_MAX;
+}
+
+size_t cs_ptot(const hgnn_ccn_config* c) {
+    const int h = c->hidden, f = c->f_in;
+    return (size_t)(h * 2 * f + h) + (size_t)(c->layers - 1) * (h * 2 * h + h);
+}
+
+CsArgs cs_args(const hgnn_ccn_config* c, const float* X, const float* adj, const int64_t* nb,
+               const float* const* params, void* ws) {
+    CsArgs a{};
+    a.adj = adj;
+    a.n_batch = nb;
+    a.X = X;
+    a.bs = c->bs;
+    a.nmax = c->nmax;
+    a.f = c->f_in;
+    a.h = c->hidden;
+    a.L = c->layers;
+    a.n_out = c->n_out;
+    a.rcap = c->nmax * c->nmax;
+    for (int l = 0; l < c->layers; ++l) {
+        a.W[l] = params[2 * l];
+        a.B[l] = params[2 * l + 1];
+    }
+    a.fcw = params[2 * c->layers];
+    a.fcb = params[2 * c->layers + 1];
+    const int nf = c->f_in + c->layers * c->hidden;
+    a.feat = static_cast<float*>(ws);
+    a.ppart = reinterpret_cast<float*>(static_cast<char*>(ws) + (4 * (size_t)c->bs * nf + 255) / 256 * 256);
+    return a;
+}
+
+template <typename K>
+void cs_lds_attr(K kernel, bool& done) {
+    if (!done) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)CS_LDS_MAX);
+        (void)hipGetLastError();  // a refused opt-in shows at the launch, not here
+        done = true;
+    }
+}
+
+}  // namespace
+}  // namespace hgnn
+
+using namespace hgnn;
+
+extern "C" {
+
+int hgnn_ccn_small_supported(const hgnn_ccn_config* cfg) { return cs_ok(cfg) ? 1 : 0; }
+
+size_t hgnn_ccn_small_workspace_bytes(const hgnn_ccn_config* cfg) {
+    if (!cs_ok(cfg)) return 0;
+    const int nf = cfg->f_in + cfg->layers * cfg->hidden;
+    return (4 * (size_t)cfg->bs * nf + 255) / 256 * 256 + (cfg->bs > 1 ? 4 * (size_t)cfg->bs * cs_ptot(cfg) : 0);
+}
+
+int hgnn_ccn_small_forward(const hgnn_ccn_config* cfg, const float* d_X, const float* d_adj,
+                           const int64_t* d_n_batch, const float* const* params, void* workspace, int32_t* d_err,
+                           int32_t tag, float* d_out, void* stream) {
+    if (!cs_ok(cfg)) return HGNN_ERR_UNSUPPORTED;
+    if (!d_X || !d_adj || !params || !workspace || !d_err || !d_out || tag <= 0 || tag >= (1 << 23))
+        return HGNN_ERR_ARG;
+    CsArgs a = cs_args(cfg, d_X, d_adj, d_n_batch, params, workspace);
+    a.out = d_out;
+    a.err = d_err;
+    a.tag = tag;
+    const size_t lds = cs_lds_bytes(a.rcap, a.f, a.h, a.L, false);
+    static bool attr = false;
+    cs_lds_attr(&k_ccn1_small_fwd<CS_CF>, attr);
+    hipLaunchKernelGGL(k_ccn1_small_fwd<CS_CF>, dim3(cfg->bs), dim3(CS_NT), lds, (hipStream_t)stream, a);
+    HGNN_LAUNCH_CHECK();
+    return HGNN_OK;
+}
+
+int hgnn_ccn_small_backward(const hgnn_ccn_config* cfg, const float* d_X, const float* d_adj,
+                            const int64_t* d_n_batch, const float* const* params, void* workspace,
+                            const float* d_dout, float* const* grads, float* d_dX, void* stream) {
+    if (!cs_ok(cfg)) return HGNN_ERR_UNSUPPORTED;
+    if (!d_X || !d_adj || !params || !workspace || !d_dout || !grads || !d_dX) return HGNN_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    CsArgs a = cs_args(cfg, d_X, d_adj, d_n_batch, params, workspace);
+    a.dout = d_dout;
+    a.dX = d_dX;
+    for (int l = 0; l < cfg->layers; ++l) {
+        a.gW[l] = grads[2 * l];
+        a.gB[l] = grads[2 * l + 1];
+    }
+    a.gfcw = grads[2 * cfg->layers];
+    a.gfcb = grads[2 * cfg->layers + 1];
+    const size_t lds = cs_lds_bytes(a.rcap, a.f, a.h, a.L, true);
+    if (cfg->hidden <= 2) {
+        static bool attr = false;
+        cs_lds_attr(&k_ccn1_small_bwd<CS_CF, 2>, attr);
+        hipLaunchKernelGGL((k_ccn1_small_bwd<CS_CF, 2>), dim3(cfg->bs), dim3(CS_NT), lds, s, a);
+    } else {
+        static bool attr = false;
+        cs_lds_attr(&k_ccn1_small_bwd<CS_CF, CS_CF>, attr);
+        hipLaunchKernelGGL((k_ccn1_small_bwd<CS_CF, CS_CF>), dim3(cfg->bs), dim3(CS_NT), lds, s, a);
+    }
+    HGNN_LAUNCH_CHECK();
+    if (cfg->bs > 1) {
+        const int nf = cfg->f_in + cfg->layers * cfg->hidden;
+        const int outs = (int)cs_ptot(cfg) + cfg->n_out * nf + cfg->n_out;
+        hipLaunchKernelGGL(k_ccn1_small_reduce, dim3((outs + 3) / 4), dim3(256), 0, s, a);
+        HGNN_LAUNCH_CHECK();
+    }
+    return HGNN_OK;
+}
+
+}  // extern "C"

@@ -104,6 +104,10 @@ SIGNATURES = {
                           ctypes.c_longlong, _VP, _VP, _VP], _I),
     "hgnn_ccn_backward": ([ctypes.POINTER(CcnConfig), ctypes.POINTER(ctypes.c_longlong), _VP, _VP,
                            ctypes.c_longlong, _VP, _VP, _VP, _VP, _VP], _I),
+    "hgnn_ccn_small_supported": ([ctypes.POINTER(CcnConfig)], _I),
+    "hgnn_ccn_small_workspace_bytes": ([ctypes.POINTER(CcnConfig)], ctypes.c_size_t),
+    "hgnn_ccn_small_forward": ([ctypes.POINTER(CcnConfig), _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _VP], _I),
+    "hgnn_ccn_small_backward": ([ctypes.POINTER(CcnConfig), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP], _I),
     "hgnn_collapse6to3": ([_VP, _VP, _I, _I, _VP], _I),
     "hgnn_collapse6to3_backward": ([_VP, _VP, _I, _I, _VP], _I),
     "hgnn_ccn_plan_offsets": ([ctypes.POINTER(CcnConfig), ctypes.c_longlong, ctypes.POINTER(ctypes.c_size_t)], _I),

@@ -19,11 +19,17 @@ reference's caller adds (scripts/train_ccn.py:36), n_batch (bs,) int64.
 """
 
 import ctypes
+import os
 
 import torch
 
 from . import _lib as L
 from .net import _require_cuda, _f32, _i64, _raise_bits, check_errors, watch_word
+
+# CCN_1D on graphs of <= 64 nodes through the one-workgroup-per-graph kernels (csrc/ccn_small.hip):
+# no plan, no workspace sizing, 1 + 1 dispatches per call for one graph.  HGNN_CCN_SMALL=0 (or setting
+# this to False) keeps every call on the general path.
+SMALL = os.environ.get("HGNN_CCN_SMALL", "1") != "0"
 
 CCN_MAX_DEGREE = {1: 1024, 2: 256}  # csrc/ccn.hip CCN1_MAXD, CCN_BIGD (by order)
 CCN2_MAX_CHANNELS = 16  # csrc/ccn.hip C2_CMAX_WIDE: CCN-2D f_in and hidden
@@ -39,6 +45,20 @@ class CcnSpec:
 
     def config(self, bs, nmax):
         return L.CcnConfig(self.order, bs, nmax, self.f_in, self.hidden, self.layers, self.n_out, 0)
+
+    def small(self, bs, nmax):
+        """(config, workspace bytes) of the small-graph path for this batch shape, or None."""
+        key = (bs, nmax)
+        c = self._small.get(key) if hasattr(self, "_small") else None
+        if c is None:
+            if not hasattr(self, "_small"):
+                self._small = {}
+            cfg = self.config(bs, nmax)
+            lib = L.lib()
+            c = (cfg, lib.hgnn_ccn_small_workspace_bytes(ctypes.byref(cfg))) \
+                if lib.hgnn_ccn_small_supported(ctypes.byref(cfg)) else False
+            self._small[key] = c
+        return c or None
 
     def param_shapes(self):
         m = 2 if self.order == 1 else 18
@@ -136,23 +156,93 @@ class _CcnFn(torch.autograd.Function):
         return (None, None, dX, None, None, *grads)
 
 
+class _TagWord:
+    """Per-device validation word of the small-graph kernels: each call passes a new tag and the
+    kernels leave atomicMax(word, tag * 256 + bits), so the word is never zeroed between calls."""
+
+    def __init__(self):
+        self.words = {}
+        self.tag = 0
+
+    def next(self, dev):
+        w = self.words.get(dev)
+        self.tag += 1
+        if w is None or self.tag >= (1 << 23):
+            if w is None:
+                w = torch.zeros(1, dtype=torch.int32, device=dev)
+                self.words[dev] = w
+            else:  # wrap: older tags must not outrank the new ones
+                w.zero_()
+            self.tag = 1 if self.tag >= (1 << 23) else self.tag
+        return w, self.tag
+
+
+_tags = _TagWord()
+
+
+class _CcnSmallFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec, small, X, adj, n_batch, *params):
+        lib = L.lib()
+        cfg, ws_bytes = small
+        bs = X.shape[0]
+        s = L.stream_handle(X.device)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=X.device)
+        out = torch.empty(bs, spec.n_out, dtype=torch.float32, device=X.device)
+        err, tag = _tags.next(X.device)
+        L.check(lib.hgnn_ccn_small_forward(ctypes.byref(cfg), L.ptr(X), L.ptr(adj), L.ptr(n_batch),
+                                           L.ptr_array(params), L.ptr(ws), L.ptr(err), tag, L.ptr(out), s),
+                "hgnn_ccn_small_forward")
+        watch_word(err, tag)
+        ctx.cfg, ctx.ws, ctx.X, ctx.adj, ctx.nb, ctx.params = cfg, ws, X, adj, n_batch, params
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = L.lib()
+        dout = dout.contiguous()
+        dev = dout.device
+        grads = [torch.empty_like(p) for p in ctx.params]
+        dX = torch.empty(ctx.X.shape, dtype=torch.float32, device=dev)
+        L.check(lib.hgnn_ccn_small_backward(ctypes.byref(ctx.cfg), L.ptr(ctx.X), L.ptr(ctx.adj), L.ptr(ctx.nb),
+                                            L.ptr_array(ctx.params), L.ptr(ctx.ws), L.ptr(dout), L.ptr_array(grads),
+                                            L.ptr(dX), L.stream_handle(dev)), "hgnn_ccn_small_backward")
+        return (None, None, dX, None, None, *grads)
+
+
 def run_ccn(spec, params, X, adj, n_batch, plan=None):
     """Batched CCN forward: X (bs,nmax,f), adj (bs,nmax,nmax), n_batch (bs,) -> (bs, n_out).
     plan: a CcnPlan of this adj / n_batch (else the plan is built here: without a host sync for
-    small shapes, ASYNC_PLAN_BOUND; with one otherwise)."""
+    small shapes, ASYNC_PLAN_BOUND; with one otherwise).  n_batch None: every graph has nmax nodes.
+    CCN_1D batches of <= 64-node graphs without a plan take the small-graph kernels (SMALL)."""
     check_errors(block=False)
+    if plan is None and SMALL and spec.order == 1 and X.dim() == 3:
+        small = spec.small(X.shape[0], X.shape[1])
+        if small is not None:
+            _require_cuda([X, adj, n_batch, *params], "CCN")
+            _check_shapes(spec, params, X, adj, n_batch)
+            return _CcnSmallFn.apply(spec, small, _f32(X), _f32(adj), None if n_batch is None else _i64(n_batch),
+                                     *[_f32(p) for p in params])
+    if n_batch is None:
+        n_batch = torch.full((X.shape[0],), X.shape[1], dtype=torch.int64, device=X.device)
     _require_cuda([X, adj, n_batch, *params], "CCN")
+    _check_shapes(spec, params, X, adj, n_batch)
+    return _CcnFn.apply(spec, plan, _f32(X), _f32(adj), _i64(n_batch), *[_f32(p) for p in params])
+
+
+def _check_shapes(spec, params, X, adj, n_batch):
     if X.dim() != 3 or adj.dim() != 3:
         raise RuntimeError(f"hgnn_amd: CCN expects X (bs,nmax,f) and adj (bs,nmax,nmax), got {tuple(X.shape)}, "
                            f"{tuple(adj.shape)}")
     bs, nmax, f = X.shape
-    if tuple(adj.shape) != (bs, nmax, nmax) or f != spec.f_in or n_batch.numel() != bs:
+    if tuple(adj.shape) != (bs, nmax, nmax) or f != spec.f_in or (n_batch is not None and n_batch.numel() != bs):
         raise RuntimeError(f"hgnn_amd: CCN shape mismatch: X {tuple(X.shape)}, adj {tuple(adj.shape)}, "
-                           f"n_batch {tuple(n_batch.shape)}, input_feats {spec.f_in}")
-    for p, shp in zip(params, spec.param_shapes()):
+                           f"n_batch {None if n_batch is None else tuple(n_batch.shape)}, input_feats {spec.f_in}")
+    if not hasattr(spec, "_shapes"):
+        spec._shapes = spec.param_shapes()
+    for p, shp in zip(params, spec._shapes):
         if tuple(p.shape) != shp:
             raise RuntimeError(f"hgnn_amd: CCN parameter shape {tuple(p.shape)} != {shp}")
-    return _CcnFn.apply(spec, plan, _f32(X), _f32(adj), _i64(n_batch), *[_f32(p) for p in params])
 
 
 def plan_maps(order, X, adj, n_batch):

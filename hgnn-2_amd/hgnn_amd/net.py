@@ -80,10 +80,10 @@ class _ErrorRing:
     def take(self):
         i = self.next
         self.next = (i + 1) % self.SLOTS
-        for k, (ev, slot) in enumerate(_pending):  # a slot still in flight: retire its check first
+        for k, (ev, slot, tag) in enumerate(_pending):  # a slot still in flight: retire its check first
             if slot == i:
                 ev.synchronize()
-                bits = int(self.host[slot])
+                bits = _word_bits(int(self.host[slot]), tag)
                 del _pending[k]
                 if bits:
                     _pending.clear()
@@ -95,19 +95,27 @@ class _ErrorRing:
 _ring = None
 
 
+def _word_bits(v, tag):
+    """Validation bits of a watched word: plain (tag None), or a tagged word tag * 256 + bits that
+    later calls overwrite by atomicMax (hgnn_ccn_small_forward): only this call's own tag counts."""
+    if tag is None:
+        return v
+    return v & 255 if (v >> 8) == tag else 0
+
+
 def check_errors(block=True):
     """Raise if any enqueued forward found an invalid input batch."""
     if _capturing():
         return
     keep = []
     bad = 0
-    for ev, slot in _pending:
+    for ev, slot, tag in _pending:
         if block:
             ev.synchronize()
         if block or ev.query():
-            bad |= int(_ring.host[slot])
+            bad |= _word_bits(int(_ring.host[slot]), tag)
         else:
-            keep.append((ev, slot))
+            keep.append((ev, slot, tag))
     _pending[:] = keep
     if bad:
         _pending.clear()
@@ -125,16 +133,17 @@ def _watch_error_word(cfg, ws):
     watch_word(ws[off:off + 4].view(torch.int32))
 
 
-def watch_word(err):
+def watch_word(err, tag=None):
     """Check a device error word (int32 view) without synchronising the stream: copied into a
-    pinned ring slot behind an event, read by a later check_errors() (HGNN_STRICT=1: at once)."""
+    pinned ring slot behind an event, read by a later check_errors() (HGNN_STRICT=1: at once).
+    tag: the word is tagged (see _word_bits)."""
     if _capturing():
         # inside a HIP graph capture (bench.py --graph): the batch was validated by the eager
         # warm-up steps; no host-visible check can be part of a replayed graph
         return
     global _ring
     if strict():
-        v = int(err.item())
+        v = _word_bits(int(err.item()), tag)
         if v:
             _raise_bits(v)
         return
@@ -144,7 +153,7 @@ def watch_word(err):
     _ring.host[slot:slot + 1].copy_(err, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record()
-    _pending.append((ev, slot))
+    _pending.append((ev, slot, tag))
 
 
 def _require_cuda(tensors, what):

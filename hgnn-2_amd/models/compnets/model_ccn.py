@@ -14,7 +14,6 @@ reference; forward_batch(X (bs, nmax, f), adj (bs, nmax, nmax), n_batch)
 (hgnn_amd.ccn -> hgnn_ccn_forward / hgnn_ccn_backward).
 """
 
-import torch
 import torch.nn as nn
 
 from functions.utils_ccn import CompnetUtils
@@ -32,7 +31,12 @@ class _CCN(nn.Module):
         return ps + [self.fc.weight, self.fc.bias]
 
     def _spec(self):
-        return CcnSpec(self.order, self.input_feats, self.w1.out_features, self.layers, self.n_outputs)
+        key = (self.order, self.input_feats, self.w1.out_features, self.layers, self.n_outputs)
+        sp = self.__dict__.get("_spec_cache")
+        if sp is None or sp[0] != key:  # kept: it caches the batch configurations of the native calls
+            sp = (key, CcnSpec(*key))
+            self.__dict__["_spec_cache"] = sp
+        return sp[1]
 
     def plan(self, adj, n_batch):
         """Index construction of a padded batch, reusable across forward_batch calls on it
@@ -46,9 +50,8 @@ class _CCN(nn.Module):
         if X.dim() != 2 or adj.dim() != 2:
             raise RuntimeError(f"hgnn_amd: CCN forward expects X (n, f) and adj (n, n), got {tuple(X.shape)}, "
                                f"{tuple(adj.shape)}")
-        n = X.shape[0]
-        nb = torch.full((1,), n, dtype=torch.int64, device=X.device)
-        return self.forward_batch(X.unsqueeze(0), adj.unsqueeze(0), nb).view(self.n_outputs)
+        # one graph of n = nmax nodes: no n_batch tensor (run_ccn makes one only for the general path)
+        return self.forward_batch(X.unsqueeze(0), adj.unsqueeze(0), None).view(self.n_outputs)
 
 
 class CCN_1D(_CCN):

@@ -318,6 +318,27 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                       void* plan_ws, long long max_sum_d2, void* workspace, const float* d_dout,
                       float* const* grads, float* d_dX, void* stream);
 
+/* CCN_1D on small graphs (nmax <= 64, f_in and hidden <= 8): one workgroup per graph builds the
+ * receptive fields, runs every level and the readout in LDS -- no plan, no host sync, one dispatch
+ * forward, one backward (+ one reduction over the graphs when bs > 1).  The per-graph drop-in call
+ * of scripts/train_ccn.py:31-73 (net(X, A + I) per graph) and QM9-size batches.  Same layouts and
+ * results as hgnn_ccn_forward / _backward (outputs and dX in the same fp32 order; weight gradients
+ * summed in a different order).  d_n_batch may be NULL (every graph has nmax nodes).
+ * supported: 1 if cfg fits (the LDS of the backward, 4 nmax^2 (hidden L + 2 max(f_in, hidden) +
+ * 2 hidden) + 8 KB, within 160 KB), else 0 (use the general path).
+ * Validation (self loops, symmetric pattern, 0 <= n_b <= nmax) is reported as
+ * atomicMax(*d_err, tag * 256 + bits) with 0 < tag < 2^23: a caller that increases tag per call reads
+ * its own call's bits as (word >> 8 == tag ? word & 255 : 0) without ever zeroing the word.
+ * The workspace holds the readout features between forward and backward. */
+int hgnn_ccn_small_supported(const hgnn_ccn_config* cfg);
+size_t hgnn_ccn_small_workspace_bytes(const hgnn_ccn_config* cfg);
+int hgnn_ccn_small_forward(const hgnn_ccn_config* cfg, const float* d_X, const float* d_adj,
+                           const int64_t* d_n_batch, const float* const* params, void* workspace,
+                           int32_t* d_err, int32_t tag, float* d_out, void* stream);
+int hgnn_ccn_small_backward(const hgnn_ccn_config* cfg, const float* d_X, const float* d_adj,
+                            const int64_t* d_n_batch, const float* const* params, void* workspace,
+                            const float* d_dout, float* const* grads, float* d_dX, void* stream);
+
 /* collapse6to3 (functions/contraction.py:106-121) on a general 6-D tensor
  * F (C, n, n, n, n, n) -> (n, n, 18 C); the 18 contractions of _c6to2_111 /
  * _c6to2_12 / _c6to2_3 with their diagonal filters. */

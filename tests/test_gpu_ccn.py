@@ -390,3 +390,96 @@ def test_ccn2_layer_counts_vs_closed_form_oracle(layers):
         _grad_close(Xr.grad[b, :x.shape[0]], xr.grad, f"L={layers} dX graph {b}")
     for n, p in net.named_parameters():
         _grad_close(p.grad, p64[n].grad, f"L={layers} grad {n}")
+
+
+def _run_path(small, net, X, A, nb, w):
+    """forward_batch + weighted-sum backward on one path (hgnn_amd.ccn.SMALL)"""
+    import hgnn_amd.ccn as HC
+    old = HC.SMALL
+    HC.SMALL = small
+    try:
+        net.zero_grad(set_to_none=True)
+        Xr = X.clone().requires_grad_(True)
+        out = net.forward_batch(Xr, A, nb)
+        (out * w).sum().backward()
+        torch.cuda.synchronize()
+        return out.detach().cpu(), Xr.grad.cpu(), {n: p.grad.detach().cpu().clone() for n, p in net.named_parameters()}
+    finally:
+        HC.SMALL = old
+
+
+@pytest.mark.parametrize("f,h,layers,bs", [(5, 2, 2, 1), (5, 2, 2, 64), (7, 5, 4, 16), (3, 8, 1, 5)])
+def test_ccn1_small_graph_path_equals_general_path(f, h, layers, bs):
+    """The one-workgroup-per-graph CCN-1D kernels (csrc/ccn_small.hip) against the general path on
+    the same batch: outputs and dX bit-identical (same fp32 order per level, same fp64 readout), weight
+    gradients on the gradient bound (different summation order), and against the fp64 oracle."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_1D
+    from oracle import ref_ccn as RC
+    graphs = [(X[:, :f] if X.shape[1] >= f else torch.cat([X, torch.rand(X.shape[0], f - X.shape[1])], 1),
+               A + torch.eye(A.shape[0]), t) for X, A, t in dg.qm9_shape_dataset(bs, seed=500 + bs)]
+    net = CCN_1D(f, 2, h, layers)
+    fu.det_init(net, 91 + layers)
+    p64 = {n: v.detach().double().clone().requires_grad_(True) for n, v in net.named_parameters()}
+    net = net.cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    assert net._spec().small(X.shape[0], X.shape[1]) is not None
+    w = torch.randn(bs, 2, generator=torch.Generator().manual_seed(bs)).cuda()
+    os_, dxs, gs = _run_path(True, net, X, A, nb, w)
+    og, dxg, gg = _run_path(False, net, X, A, nb, w)
+    assert torch.equal(os_, og), f"outputs differ: {(os_ - og).abs().max().item():.3g}"
+    assert torch.equal(dxs, dxg), f"dX differs: {(dxs - dxg).abs().max().item():.3g}"
+    for n in gg:
+        _grad_close(gs[n], gg[n], f"small vs general grad {n}")
+    for b, (x, a, _) in enumerate(graphs[:8]):
+        xr = x.double().requires_grad_(True)
+        ref = RC.ccn_forward(p64, xr, a.double(), 1, layers)
+        _close(os_[b], ref, f"small path graph {b}")
+        (ref * w[b].double().cpu()).sum().backward()
+        _grad_close(dxs[b, :x.shape[0]], xr.grad, f"small path dX graph {b}")
+        assert dxs[b, x.shape[0]:].abs().max().item() == 0.0 if x.shape[0] < X.shape[1] else True
+
+
+def test_ccn1_small_graph_path_per_graph_drop_in():
+    """net(X, A + I) per graph (n_batch None: the small path without any index tensor) equals the
+    batched general path row by row; the input gradient of the per-graph call as well."""
+    import hgnn_amd.ccn as HC
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_1D
+    graphs = [(X, A + torch.eye(A.shape[0]), t) for X, A, t in dg.qm9_shape_dataset(12, seed=515)]
+    net = CCN_1D(5, 1, 2, 2)
+    fu.det_init(net, 515)
+    net = net.cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    old = HC.SMALL
+    HC.SMALL = False
+    try:
+        ob = net.forward_batch(X, A, nb).detach().cpu()
+    finally:
+        HC.SMALL = old
+    for b, (x, a, _) in enumerate(graphs):
+        xr = x.cuda().requires_grad_(True)
+        o = net(xr, a.cuda())
+        assert torch.equal(o.detach().cpu(), ob[b]), f"graph {b}"
+        o.sum().backward()
+        assert torch.isfinite(xr.grad).all()
+
+
+def test_ccn1_small_graph_path_validation():
+    """The small path reports the general plan's validation bits: missing self loop, asymmetric
+    pattern, n_b > nmax -- raised by the next check (HGNN_STRICT semantics unchanged)."""
+    from hgnn_amd.net import check_errors
+    from models.compnets.model_ccn import CCN_1D
+    net = CCN_1D(5, 1, 2, 2).cuda()
+    A = torch.eye(4)
+    A[0, 1] = 1.0  # 1 does not list 0
+    with pytest.raises(RuntimeError, match="not symmetric"):
+        net(torch.randn(4, 5).cuda(), A.cuda())
+        check_errors()
+    A = torch.eye(4).unsqueeze(0)
+    with pytest.raises(RuntimeError, match="negative count"):
+        net.forward_batch(torch.randn(1, 4, 5).cuda(), A.cuda(), torch.tensor([5]).cuda())
+        check_errors()
+    # a clean call after the failures raises nothing (tags: older words do not count)
+    net(torch.randn(4, 5).cuda(), torch.eye(4).cuda())
+    check_errors()
