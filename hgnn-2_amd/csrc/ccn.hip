@@ -219,44 +219,48 @@ __global__ void __launch_bounds__(256) k_ccn1_fwd(CcnPlanView v, const int* tota
     const long long r0 = v.off1[i];
     const int k2 = 2 * cin;
     if (n <= 64 && cin <= C1F) {
-        // one chunk: lane x keeps its row sums and the column sum of neighbour a = x in registers, the
-        // four neighbours of a round load every channel at once (was one round trip per channel and a)
-        const int x = lane;
-        const bool vx = x < n;
+        // one chunk, no cross-lane reduction: lane l keeps the row sum of position x = l (a ascending) and
+        // the column sum of neighbour a = l (x ascending), four neighbours per round, every channel at once
+        const int l = lane;
+        const bool vl = l < n;
+        const int jl = ni[vl ? l : 0];
+        const float* fl = level0 ? X + (long long)jl * cin : fin + (long long)v.off1[jl] * cin;
         float rs[C1F], colv[C1F];
 #pragma unroll
         for (int c = 0; c < C1F; ++c) rs[c] = colv[c] = 0.f;
-        for (int a0 = 0; a0 < n; a0 += 4) {
-            float t[4][C1F];
+        for (int k0 = 0; k0 < n; k0 += 4) {
+            float t1[4][C1F], t2[4][C1F];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int a = min(a0 + u, n - 1);
-                const int j = ni[a];
-                const int p = vx ? pi[(long long)a * n + x] : -1;
-                const bool ok = p >= 0 && a0 + u < n;
-                const float* src = level0 ? X + (long long)j * cin : fin + ((long long)v.off1[j] + max(p, 0)) * cin;
-#pragma unroll
-                for (int c = 0; c < C1F; ++c) t[u][c] = (c < cin && ok) ? src[c] : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int a = a0 + u;
-                if (a >= n) break;
+            for (int q = 0; q < 4; ++q) {
+                const int k = min(k0 + q, n - 1);
+                const int j = ni[k];
+                const int p1 = vl ? pi[(long long)k * n + l] : -1;  // position x = l in N(j_k)
+                const int p2 = vl ? pi[(long long)l * n + k] : -1;  // position x = k in N(j_l)
+                const bool ok1 = p1 >= 0 && k0 + q < n, ok2 = p2 >= 0 && k0 + q < n;
+                const float* s1 = level0 ? X + (long long)j * cin : fin + ((long long)v.off1[j] + max(p1, 0)) * cin;
+                const float* s2 = level0 ? fl : fl + (long long)max(p2, 0) * cin;
 #pragma unroll
                 for (int c = 0; c < C1F; ++c) {
-                    if (c >= cin) break;
-                    rs[c] += t[u][c];
-                    const float cs = wave_total(t[u][c]);
-                    colv[c] = lane == a ? cs : colv[c];
-                    if (lane == 0) coll[(r0 + a) * k2 + cin + c] = cs;
+                    t1[q][c] = (c < cin && ok1) ? s1[c] : 0.f;
+                    t2[q][c] = (c < cin && ok2) ? s2[c] : 0.f;
                 }
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int c = 0; c < C1F; ++c) {
+                    rs[c] += t1[q][c];
+                    colv[c] += t2[q][c];
+                }
         }
-        if (vx) {
-            const long long row = r0 + x;
+        if (vl) {
+            const long long row = r0 + l;
 #pragma unroll
             for (int c = 0; c < C1F; ++c)
-                if (c < cin) coll[row * k2 + c] = rs[c];
+                if (c < cin) {
+                    coll[row * k2 + c] = rs[c];
+                    coll[row * k2 + cin + c] = colv[c];
+                }
             for (int o = 0; o < h; ++o) {
                 float s = bias[o];
 #pragma unroll

@@ -15,17 +15,24 @@
 // the same order, so forward values and input gradients are those of the general path; the weight
 // gradients are summed per lane over a wave's nodes, then over lanes and waves (fp32), where the general
 // path sums per node and then over nodes in fp64.
+#include <cstdio>
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace hgnn {
 namespace {
 
-constexpr int CS_NT = 256, CS_NW = CS_NT / 64;
+constexpr int CS_NT = 512, CS_NW = CS_NT / 64;   // 8 waves (~4 nodes of a QM9 graph each; 256 VGPRs a lane)
+constexpr int CS_RT = 256;                         // threads of the fp64 readout sums (the general path's order)
 constexpr int CS_CF = 8;                              // f_in and hidden bound
 constexpr int CS_LMAX = 15;
 constexpr int CS_NFMAX = CS_CF + CS_LMAX * CS_CF;     // readout width bound
 constexpr int CS_PMAX = CS_CF * 2 * CS_CF + CS_CF;    // one level's weight + bias entries
-constexpr size_t CS_FIXED = 512 + 256 + 272 + 4096 + 4 * CS_NW * CS_PMAX + 4 * CS_NFMAX + 8 * CS_NW * CS_CF;
+constexpr int CS_XMAX = 64 * CS_CF;                 // staged node features
+constexpr int CS_WMAX = CS_LMAX * CS_PMAX;            // staged level weights and biases
+constexpr size_t CS_FIXED = 512 + 256 + 272 + 4096 + 4 * CS_NW * CS_PMAX + 4 * CS_NFMAX + 8 * CS_NW * CS_CF +
+                            4 * CS_XMAX + 4 * CS_WMAX;
 constexpr size_t CS_LDS_MAX = 150 * 1024;  // dynamic LDS opt-in (the forward also has a static word)
 
 struct CsArgs {
@@ -39,7 +46,7 @@ struct CsArgs {
     const float* fcb;
     float* feat;             // [bs][nf] readout features (forward writes, backward reads)
     float* out;              // (bs, n_out)
-    int* err;                // forward: atomicMax(err, tag * 256 + bits)
+    int* err;                // forward: graphs with validation bits store tag * 256 + bits
     int tag;
     const float* dout;       // backward
     float* ppart;            // backward, bs > 1: [bs][ptot] level weight / bias partials, levels ascending
@@ -48,7 +55,14 @@ struct CsArgs {
     float* gfcw;
     float* gfcb;
     float* dX;               // (bs, nmax, f), padding rows zeroed
+    unsigned long long* prof;  // diagnostic phase stamps of graph 0 (HGNN_CCN_SMALL_PROF), or null
 };
+
+// phase stamp k of graph 0 (s_memtime core cycles), diagnostic builds of the timing only
+#define CS_STAMP(k)                                                          \
+    do {                                                                     \
+        if (a.prof && blockIdx.x == 0 && threadIdx.x == 0) a.prof[k] = clock64(); \
+    } while (0)
 
 struct CsLds {
     unsigned long long* bits;  // [64] row bit sets
@@ -58,6 +72,8 @@ struct CsLds {
     float* red;                // [CS_NW][CS_PMAX]
     float* vec;                // [CS_NFMAX] readout features (forward) / dsum (backward)
     double* dred;              // [CS_NW][CS_CF]
+    float* Xs;                 // [n][f] the graph's node features
+    float* Ws;                 // level l: W_l [h][2 cin] then b_l [h], levels ascending
     float* F;                  // forward: 2 levels (ping-pong); backward: all L levels, [rcap][h] each
     float* dcoll;              // backward: [rcap][2 cmax]
     float* dF0;                // backward: [rcap][h] x 2
@@ -86,6 +102,10 @@ __device__ inline CsLds cs_carve(char* base, const CsArgs& a, bool bwd) {
     o += 4 * CS_NFMAX;
     s.dred = reinterpret_cast<double*>(base + o);
     o += 8 * CS_NW * CS_CF;
+    s.Xs = reinterpret_cast<float*>(base + o);
+    o += 4 * CS_XMAX;
+    s.Ws = reinterpret_cast<float*>(base + o);
+    o += 4 * CS_WMAX;
     s.F = reinterpret_cast<float*>(base + o);
     o += 4 * (size_t)a.rcap * a.h * (bwd ? a.L : 2);
     s.dcoll = s.dF0 = s.dF1 = nullptr;
@@ -106,14 +126,57 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
     return v;
 }
 
-// Graph b's receptive fields: nbr, bits, deg, off1 in LDS.  Returns this lane's validation bits (self loop
-// missing, pattern not symmetric -- the general plan's ERR_CCN_SELFLOOP / ERR_CCN_ASYM).
-__device__ uint32_t cs_plan(const CsArgs& a, int b, int n, const CsLds& s) {
+// offset of level l's weights in Ws
+__device__ __forceinline__ int cs_woff(int l, int f, int h) {
+    return l == 0 ? 0 : (h * 2 * f + h) + (l - 1) * (h * 2 * h + h);
+}
+
+// One round of loads for the whole call: the graph's adjacency block (into As, stride n), its node
+// features and every level's weights; every later access is to LDS (the dependent global round trips
+// of a per-node walk were most of a QM9 graph's time).
+__device__ void cs_stage(const CsArgs& a, int b, int n, const CsLds& s, float* As) {
     const float* A = a.adj + (long long)b * a.nmax * a.nmax;
+    const float* Xg = a.X + (long long)b * a.nmax * a.f;
+    const int na = n * n, nx = n * a.f, nw = cs_woff(a.L, a.f, a.h);
+    const int total = na + nx + nw;
+    constexpr int U = 4;
+    for (int e0 = threadIdx.x; e0 < total; e0 += CS_NT * U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = e0 + u * CS_NT;
+            v[u] = 0.f;
+            if (e < na) {
+                const int r = e / n;
+                v[u] = A[(long long)r * a.nmax + (e - r * n)];
+            } else if (e < na + nx) {
+                v[u] = Xg[e - na];
+            } else if (e < total) {
+                int p = e - na - nx, l = 0;
+                while (l + 1 < a.L && p >= cs_woff(l + 1, a.f, a.h)) ++l;
+                const int q = p - cs_woff(l, a.f, a.h), hk = a.h * 2 * (l == 0 ? a.f : a.h);
+                v[u] = q < hk ? a.W[l][q] : a.B[l][q - hk];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = e0 + u * CS_NT;
+            if (e < na) As[e] = v[u];
+            else if (e < na + nx) s.Xs[e - na] = v[u];
+            else if (e < total) s.Ws[e - na - nx] = v[u];
+        }
+    }
+    __syncthreads();
+}
+
+// Graph b's receptive fields from the staged adjacency: nbr, bits, deg, off1 in LDS.  Returns this lane's
+// validation bits (self loop missing, pattern not symmetric -- the general plan's ERR_CCN_SELFLOOP /
+// ERR_CCN_ASYM).
+__device__ uint32_t cs_plan(int n, const CsLds& s, const float* As) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t bad = 0;
     for (int r = wv; r < n; r += CS_NW) {
-        const bool nz = lane < n && A[(long long)r * a.nmax + lane] > 0.f;  // utils_ccn.py:195 (A > 0)
+        const bool nz = lane < n && As[r * n + lane] > 0.f;  // utils_ccn.py:195 (A > 0)
         const unsigned long long m = __ballot(nz);
         if (nz) s.nbr[r * 64 + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned char)lane;
         if (lane == 0) {
@@ -133,6 +196,13 @@ __device__ uint32_t cs_plan(const CsArgs& a, int b, int n, const CsLds& s) {
         }
         s.off1[lane] = x - d;
         if (lane == 63) s.off1[64] = x;
+        // lanes per node of the level walks: the power of two >= the largest receptive field
+        int dm = d;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) dm = max(dm, __shfl_xor(dm, o, 64));
+        int g = 1;
+        while (g < dm) g <<= 1;
+        if (lane == 0) s.off1[66] = g;
     }
     // every neighbour j of r must list r (the backward gathers node j's readers from N(j))
     for (int r = wv; r < n; r += CS_NW) {
@@ -143,55 +213,85 @@ __device__ uint32_t cs_plan(const CsArgs& a, int b, int n, const CsLds& s) {
     return bad;
 }
 
-// Node i, lane x = receptive-field position: rs[c] = sum_a T[a][x][c] and colv[c] = the column sum of
-// neighbour a = x, T[a][x] = F_{j_a}[pos(nbr_i[x] in N(j_a))] (level 0: X[j_a] when present) -- the
-// order of k_ccn1_fwd's one-chunk path.
+// Level walks pack several nodes into a wave: G lanes per node (G = the power of two >= the graph's largest
+// receptive field, off1[66]), lane p of group g serves position / neighbour p of node i = base + wv * 64/G + g
+// (-1 past the graph).  A QM9 graph (d <= 5, G = 8) takes 8 nodes per wave: one pass of the 8 waves.
+struct CsSlot {
+    int i, p;
+};
+__device__ __forceinline__ CsSlot cs_slot(int base, int G, int n) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int i = base + wv * (64 / G) + lane / G;
+    return CsSlot{i < n ? i : -1, lane & (G - 1)};
+}
+
+// Node i, lane p < d_i (w = nbr_i[p]):  rs[c] = sum_a T[a][p][c] (p as the position x: w read from N(j_a), a
+// ascending) and colv[c] = sum_x T[p][x][c] (p as the neighbour a: every u_x read from N(w), x ascending),
+// T[a][x] = F_{j_a}[pos(u_x in N(j_a))] (level 0: X[j_a] when present).  Lane-local loops over the node's
+// neighbours -- no cross-lane reduction -- in the order of k_ccn1_fwd's one-chunk path.  Branch-free: the
+// four neighbours' ids, their rows and offsets, then every channel of both reads go out as one batch of LDS
+// loads each (reads past a row stay inside the LDS allocation and are discarded by the selects).
 template <int CF>
-__device__ __forceinline__ void cs_collect(const CsLds& s, int i, const float* __restrict__ Xg, const float* Fin,
-                                           int cin, float (&rs)[CF], float (&colv)[CF]) {
-    const int lane = threadIdx.x & 63;
-    const int d = s.deg[i];
-    const bool vx = lane < d;
-    const int u = vx ? s.nbr[i * 64 + lane] : 0;
-    const unsigned long long below = (1ull << u) - 1ull;
+__device__ __forceinline__ void cs_collect(const CsLds& s, CsSlot sl, int G, const float* __restrict__ Xg,
+                                           const float* Fin, int cin, float (&rs)[CF], float (&colv)[CF]) {
+    const int ib = (sl.i >= 0 ? sl.i : 0) * 64;
+    const int d = sl.i >= 0 ? s.deg[sl.i] : 0;
+    const bool v = sl.p < d;
+    const bool lv0 = Fin == nullptr;
+    const float* B = lv0 ? Xg : Fin;
+    const int wl = s.nbr[ib + (v ? sl.p : 0)];
+    const unsigned long long ml = s.bits[wl];
+    const unsigned long long bl = (1ull << wl) - 1ull;
+    const int ol = s.off1[wl];
+    const int dl = d > 0 ? d - 1 : 0;
 #pragma unroll
     for (int c = 0; c < CF; ++c) rs[c] = colv[c] = 0.f;
-    for (int a0 = 0; a0 < d; a0 += 4) {
-        float t[4][CF];
+    for (int k0 = 0; k0 < G; k0 += 4) {
+        int jk[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) jk[q] = s.nbr[ib + min(k0 + q, dl)];
+        unsigned long long mk[4];
+        int ok_[4], a1[4], a2[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int a = min(a0 + q, d - 1);
-            const int j = s.nbr[i * 64 + a];
-            const unsigned long long m = s.bits[j];
-            const bool ok = vx && ((m >> u) & 1ull) && a0 + q < d;
-            const float* src = Fin ? Fin + (s.off1[j] + __popcll(m & below)) * cin : Xg + j * cin;
-#pragma unroll
-            for (int c = 0; c < CF; ++c) t[q][c] = (c < cin && ok) ? src[c] : 0.f;
+            mk[q] = s.bits[jk[q]];
+            ok_[q] = s.off1[jk[q]];
         }
+        bool g1[4], g2[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int a = a0 + q;
-            if (a >= d) break;
+            const bool live = v && k0 + q < d;
+            g1[q] = live && ((mk[q] >> wl) & 1ull);
+            g2[q] = live && ((ml >> jk[q]) & 1ull);
+            a1[q] = lv0 ? jk[q] * cin : (ok_[q] + __popcll(mk[q] & bl)) * cin;
+            a2[q] = lv0 ? wl * cin : (ol + __popcll(ml & ((1ull << jk[q]) - 1ull))) * cin;
+        }
+        float t1[4][CF], t2[4][CF];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int c = 0; c < CF; ++c) {
-                if (c >= cin) break;
-                rs[c] += t[q][c];
-                const float cs = wave_total(t[q][c]);
-                colv[c] = lane == a ? cs : colv[c];
+                t1[q][c] = B[a1[q] + c];
+                t2[q][c] = B[a2[q] + c];
             }
-        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int c = 0; c < CF; ++c) {
+                rs[c] += (c < cin && g1[q]) ? t1[q][c] : 0.f;
+                colv[c] += (c < cin && g2[q]) ? t2[q][c] : 0.f;
+            }
     }
 }
 
 // F_l rows of node i: relu(b + W [rs | colv]) in k_ccn1_fwd's order
 template <int CF>
-__device__ __forceinline__ void cs_update(const CsLds& s, int i, const float (&rs)[CF], const float (&colv)[CF],
+__device__ __forceinline__ void cs_update(const CsLds& s, CsSlot sl, const float (&rs)[CF], const float (&colv)[CF],
                                           int cin, const float* __restrict__ W, const float* __restrict__ bias, int h,
                                           float* Fout) {
-    const int lane = threadIdx.x & 63;
-    if (lane >= s.deg[i]) return;
+    if (sl.i < 0 || sl.p >= s.deg[sl.i]) return;
     const int k2 = 2 * cin;
-    const int row = s.off1[i] + lane;
+    const int row = s.off1[sl.i] + sl.p;
     for (int o = 0; o < h; ++o) {
         float v = bias[o];
 #pragma unroll
@@ -205,17 +305,18 @@ __device__ __forceinline__ void cs_update(const CsLds& s, int i, const float (&r
 }
 
 // Readout column sums in fp64 (k_ccn_readout_part's order for a one-chunk graph): vec[col0 + c] =
-// sum over rows r of val(r, c), rows over the 256 threads, then the waves.
+// sum over rows r of val(r, c), rows over the first 256 threads, then their 4 waves.
 template <int CF, typename V>
 __device__ __forceinline__ void cs_colsum(const CsLds& s, int rows, int C, int col0, V val) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     double acc[CF];
 #pragma unroll
     for (int c = 0; c < CF; ++c) acc[c] = 0.0;
-    for (int r = threadIdx.x; r < rows; r += CS_NT)
+    if (threadIdx.x < CS_RT)
+        for (int r = threadIdx.x; r < rows; r += CS_RT)
 #pragma unroll
-        for (int c = 0; c < CF; ++c)
-            if (c < C) acc[c] += val(r, c);
+            for (int c = 0; c < CF; ++c)
+                if (c < C) acc[c] += val(r, c);
 #pragma unroll
     for (int c = 0; c < CF; ++c) {
         if (c >= C) break;
@@ -246,33 +347,44 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_fwd(CsArgs a) {
     const int b = blockIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const CsLds s = cs_carve(lds, a, false);
+    CS_STAMP(0);
     if (threadIdx.x == 0) sbad = 0;
     uint32_t bad = 0;
     const int n = cs_nodes(a, b, bad);
-    bad |= cs_plan(a, b, n, s);
-    const float* Xg = a.X + (long long)b * a.nmax * a.f;
+    cs_stage(a, b, n, s, s.F);
+    CS_STAMP(1);
+    bad |= cs_plan(n, s, s.F);
+    CS_STAMP(2);
+    const float* Xg = s.Xs;
     const int h = a.h, f = a.f, nf = f + a.L * h;
+    const int G = s.off1[66];
     // level 0 of the readout: sum_i d_i X[i]  (utils_ccn.py:212-216 tiles X[i] d_i times)
     cs_colsum<CF>(s, n, f, 0, [&](int r, int c) { return (double)s.deg[r] * (double)Xg[r * f + c]; });
+    CS_STAMP(3);
     const int rows = s.off1[n];
     const float* fin = nullptr;
     for (int l = 0; l < a.L; ++l) {
         const int cin = l == 0 ? f : h;
         float* fout = s.F + (size_t)(l & 1) * a.rcap * h;
-        for (int i = wv; i < n; i += CS_NW) {
+        for (int base = 0; base < n; base += CS_NW * (64 / G)) {
+            const CsSlot sl = cs_slot(base, G, n);
             float rs[CF], colv[CF];
-            cs_collect<CF>(s, i, Xg, fin, cin, rs, colv);
-            cs_update<CF>(s, i, rs, colv, cin, a.W[l], a.B[l], h, fout);
+            cs_collect<CF>(s, sl, G, Xg, fin, cin, rs, colv);
+            const float* Wl = s.Ws + cs_woff(l, f, h);
+            cs_update<CF>(s, sl, rs, colv, cin, Wl, Wl + h * 2 * cin, h, fout);
         }
         __syncthreads();
+        CS_STAMP(4 + 2 * l);
         cs_colsum<CF>(s, rows, h, f + l * h, [&](int r, int c) { return (double)fout[r * h + c]; });
+        CS_STAMP(5 + 2 * l);
         fin = fout;
     }
     for (int k = threadIdx.x; k < nf; k += CS_NT) a.feat[(long long)b * nf + k] = s.vec[k];
     // out = fc(feat) in fp64 (k_ccn_readout's order)
     for (int o = 0; o < a.n_out; ++o) {
         double acc = 0.0;
-        for (int k = threadIdx.x; k < nf; k += CS_NT) acc += (double)a.fcw[o * nf + k] * (double)s.vec[k];
+        if (threadIdx.x < CS_RT)
+            for (int k = threadIdx.x; k < nf; k += CS_RT) acc += (double)a.fcw[o * nf + k] * (double)s.vec[k];
         acc = wave_sum_d(acc);
         __syncthreads();
         if (lane == 0) s.dred[wv] = acc;
@@ -280,10 +392,12 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_fwd(CsArgs a) {
         if (threadIdx.x == 0)
             a.out[(long long)b * a.n_out + o] = (float)(s.dred[0] + s.dred[1] + s.dred[2] + s.dred[3] + (double)a.fcb[o]);
     }
+    CS_STAMP(30);
     bad = wave_or(bad);
     if (lane == 0 && bad) atomicOr(&sbad, bad);
     __syncthreads();
-    if (threadIdx.x == 0 && sbad) atomicMax(a.err, a.tag * 256 + (int)sbad);
+    if (threadIdx.x == 0 && sbad) a.err[0] = a.tag * 256 + (int)sbad;  // vector store (host-mapped word)
+    CS_STAMP(31);
 }
 
 template <int CF, int CH>
@@ -294,18 +408,22 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_bwd(CsArgs a) {
     const CsLds s = cs_carve(lds, a, true);
     uint32_t bad = 0;
     const int n = cs_nodes(a, b, bad);
-    (void)cs_plan(a, b, n, s);  // the forward reported the batch's validation bits
-    const float* Xg = a.X + (long long)b * a.nmax * a.f;
+    cs_stage(a, b, n, s, s.F);
+    (void)cs_plan(n, s, s.F);  // the forward reported the batch's validation bits
+    const float* Xg = s.Xs;
     const int h = a.h, f = a.f, L = a.L, nf = f + L * h;
+    const int G = s.off1[66];
     // the levels again, all kept
     for (int l = 0; l < L; ++l) {
         const int cin = l == 0 ? f : h;
         const float* fin = l == 0 ? nullptr : s.F + (size_t)(l - 1) * a.rcap * h;
         float* fout = s.F + (size_t)l * a.rcap * h;
-        for (int i = wv; i < n; i += CS_NW) {
+        for (int base = 0; base < n; base += CS_NW * (64 / G)) {
+            const CsSlot sl = cs_slot(base, G, n);
             float rs[CF], colv[CF];
-            cs_collect<CF>(s, i, Xg, fin, cin, rs, colv);
-            cs_update<CF>(s, i, rs, colv, cin, a.W[l], a.B[l], h, fout);
+            cs_collect<CF>(s, sl, G, Xg, fin, cin, rs, colv);
+            const float* Wl = s.Ws + cs_woff(l, f, h);
+            cs_update<CF>(s, sl, rs, colv, cin, Wl, Wl + h * 2 * cin, h, fout);
         }
         __syncthreads();
     }
@@ -327,7 +445,7 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_bwd(CsArgs a) {
     float* dFn = s.dF1;
     for (int l = L - 1; l >= 0; --l) {
         const int cin = l == 0 ? f : h, k2 = 2 * cin;
-        const float* W = a.W[l];
+        const float* W = s.Ws + cs_woff(l, f, h);
         const float* Fl = s.F + (size_t)l * a.rcap * h;
         const float* fin = l == 0 ? nullptr : s.F + (size_t)(l - 1) * a.rcap * h;
         const bool top = l == L - 1;
@@ -340,19 +458,18 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_bwd(CsArgs a) {
 #pragma unroll
             for (int c = 0; c < CF; ++c) aw[o][c] = ac[o][c] = 0.f;
         }
-        for (int i = wv; i < n; i += CS_NW) {
+        for (int base = 0; base < n; base += CS_NW * (64 / G)) {
+            const CsSlot sl = cs_slot(base, G, n);
             float rs[CF], colv[CF];
-            cs_collect<CF>(s, i, Xg, fin, cin, rs, colv);
-            const bool vx = lane < s.deg[i];
-            const int row = s.off1[i] + lane;
+            cs_collect<CF>(s, sl, G, Xg, fin, cin, rs, colv);
+            const int ii = sl.i >= 0 ? sl.i : 0;
+            const bool vx = sl.i >= 0 && sl.p < s.deg[ii];
+            const int row = s.off1[ii] + sl.p;
             float dp[CH];
 #pragma unroll
             for (int o = 0; o < CH; ++o) {
-                dp[o] = 0.f;
-                if (vx && o < h) {
-                    const float g = top ? dtop[o] : dFc[row * h + o];
-                    dp[o] = Fl[row * h + o] > 0.f ? g : 0.f;
-                }
+                const float g = top ? dtop[o] : dFc[row * h + o];  // unconditional LDS reads
+                dp[o] = (vx && o < h && Fl[row * h + o] > 0.f) ? g : 0.f;
                 ab[o] += dp[o];
 #pragma unroll
                 for (int c = 0; c < CF; ++c) {
@@ -389,7 +506,9 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_bwd(CsArgs a) {
         __syncthreads();
         const int P = h * k2 + h;
         for (int p = threadIdx.x; p < P; p += CS_NT) {
-            const float v = s.red[p] + s.red[CS_PMAX + p] + s.red[2 * CS_PMAX + p] + s.red[3 * CS_PMAX + p];
+            float v = s.red[p];
+#pragma unroll
+            for (int w = 1; w < CS_NW; ++w) v += s.red[w * CS_PMAX + p];
             if (a.bs == 1) {
                 if (p < h * k2) a.gW[l][p] = v;
                 else a.gB[l][p - h * k2] = v;
@@ -400,47 +519,60 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_bwd(CsArgs a) {
         }
         // gather: dF_{l-1}[j][u] = sum_{i in N(j)} [q valid] (drow_i[q] + dcol_i[pos of j]) + readout term;
         // level 0: dX[j] = the sum over u + d_j dsum  (k_ccn1_bwd_gather's order)
-        for (int j = wv; j < n; j += CS_NW) {
-            const int d = s.deg[j];
-            const bool vu = lane < d;
-            const int uu = vu ? s.nbr[j * 64 + lane] : 0;
+        for (int base = 0; base < n; base += CS_NW * (64 / G)) {
+            const CsSlot sl = cs_slot(base, G, n);
+            const int j = sl.i >= 0 ? sl.i : 0;
+            const int d = sl.i >= 0 ? s.deg[j] : 0;
+            const bool vu = sl.p < d;
+            const int uu = s.nbr[j * 64 + (vu ? sl.p : 0)];
             const unsigned long long bu = (1ull << uu) - 1ull, bj = (1ull << j) - 1ull;
+            const int dl = d > 0 ? d - 1 : 0;
             float acc[CF];
 #pragma unroll
             for (int c = 0; c < CF; ++c) acc[c] = 0.f;
-            for (int a0 = 0; a0 < d; a0 += 4) {
-                float t1[4][CF], t2[4][CF];
+            for (int a0 = 0; a0 < G; a0 += 4) {
+                int ik[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ik[q] = s.nbr[j * 64 + min(a0 + q, dl)];
+                unsigned long long m[4];
+                int ri[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const int ai = min(a0 + q, d - 1);
-                    const int i = s.nbr[j * 64 + ai];
-                    const unsigned long long m = s.bits[i];
-                    const bool ok = vu && ((m >> uu) & 1ull) && a0 + q < d;
-                    const int ri = s.off1[i];
-                    const float* s1 = s.dcoll + (ri + __popcll(m & bu)) * k2;
-                    const float* s2 = s.dcoll + (ri + __popcll(m & bj)) * k2 + cin;
+                    m[q] = s.bits[ik[q]];
+                    ri[q] = s.off1[ik[q]];
+                }
+                float t1[4][CF], t2[4][CF];
+                bool ok[4];
 #pragma unroll
-                    for (int c = 0; c < CF; ++c) {
-                        t1[q][c] = (c < cin && ok) ? s1[c] : 0.f;
-                        t2[q][c] = (c < cin && ok) ? s2[c] : 0.f;
+                for (int q = 0; q < 4; ++q) {
+                    ok[q] = vu && ((m[q] >> uu) & 1ull) && a0 + q < d;
+                    const float* s1 = s.dcoll + (ri[q] + __popcll(m[q] & bu)) * k2;
+                    const float* s2 = s.dcoll + (ri[q] + __popcll(m[q] & bj)) * k2 + cin;
+#pragma unroll
+                    for (int c = 0; c < CF; ++c) {  // unconditional LDS reads, discarded by the selects
+                        t1[q][c] = s1[c];
+                        t2[q][c] = s2[c];
                     }
                 }
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
 #pragma unroll
-                    for (int c = 0; c < CF; ++c) acc[c] += t1[q][c] + t2[q][c];
+                    for (int c = 0; c < CF; ++c)
+                        acc[c] += (c < cin && ok[q]) ? t1[q][c] + t2[q][c] : 0.f;
             }
             if (l > 0) {
                 if (vu)
 #pragma unroll
                     for (int c = 0; c < CF; ++c)
-                        if (c < cin) dFn[(s.off1[j] + lane) * cin + c] = acc[c] + s.vec[f + (l - 1) * h + c];
+                        if (c < cin) dFn[(s.off1[j] + sl.p) * cin + c] = acc[c] + s.vec[f + (l - 1) * h + c];
             } else {
+                // the node's G lanes summed by an xor tree: with zeros past d this is wave_total's association
 #pragma unroll
                 for (int c = 0; c < CF; ++c) {
                     if (c >= cin) break;
-                    const float tot = wave_total(vu ? acc[c] : 0.f);
-                    if (lane == 0) a.dX[((long long)b * a.nmax + j) * f + c] = tot + (float)d * s.vec[c];
+                    float tot = vu ? acc[c] : 0.f;
+                    for (int o = 1; o < G; o <<= 1) tot += __shfl_xor(tot, o, 64);
+                    if (sl.i >= 0 && sl.p == 0) a.dX[((long long)b * a.nmax + j) * f + c] = tot + (float)d * s.vec[c];
                 }
             }
         }
@@ -539,6 +671,21 @@ extern "C" {
 
 int hgnn_ccn_small_supported(const hgnn_ccn_config* cfg) { return cs_ok(cfg) ? 1 : 0; }
 
+int hgnn_host_word_alloc(void** host_ptr, void** dev_ptr) {
+    if (!host_ptr || !dev_ptr) return HGNN_ERR_ARG;
+    void* h = nullptr;
+    HGNN_HOST_CHECK(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipHostFree(h);
+        return HGNN_ERR_HIP;
+    }
+    static_cast<int32_t*>(h)[0] = 0;
+    *host_ptr = h;
+    *dev_ptr = d;
+    return HGNN_OK;
+}
+
 size_t hgnn_ccn_small_workspace_bytes(const hgnn_ccn_config* cfg) {
     if (!cs_ok(cfg)) return 0;
     const int nf = cfg->f_in + cfg->layers * cfg->hidden;
@@ -558,8 +705,24 @@ int hgnn_ccn_small_forward(const hgnn_ccn_config* cfg, const float* d_X, const f
     const size_t lds = cs_lds_bytes(a.rcap, a.f, a.h, a.L, false);
     static bool attr = false;
     cs_lds_attr(&k_ccn1_small_fwd<CS_CF>, attr);
+    static const bool prof = getenv("HGNN_CCN_SMALL_PROF") != nullptr;
+    static unsigned long long* dprof = nullptr;
+    if (prof) {
+        if (!dprof) HGNN_HOST_CHECK(hipMalloc(&dprof, 32 * 8));
+        HGNN_HOST_CHECK(hipMemsetAsync(dprof, 0, 32 * 8, (hipStream_t)stream));
+        a.prof = dprof;
+    }
     hipLaunchKernelGGL(k_ccn1_small_fwd<CS_CF>, dim3(cfg->bs), dim3(CS_NT), lds, (hipStream_t)stream, a);
     HGNN_LAUNCH_CHECK();
+    if (prof) {  // diagnostic: phase cycles of graph 0 (synchronises)
+        unsigned long long hp[32];
+        HGNN_HOST_CHECK(hipMemcpyAsync(hp, dprof, sizeof(hp), hipMemcpyDeviceToHost, (hipStream_t)stream));
+        HGNN_HOST_CHECK(hipStreamSynchronize((hipStream_t)stream));
+        fprintf(stderr, "ccn_small_fwd cycles:");
+        for (int k = 1; k < 32; ++k)
+            if (hp[k]) fprintf(stderr, " %d:%llu", k, hp[k] - hp[0]);
+        fprintf(stderr, "\n");
+    }
     return HGNN_OK;
 }
 

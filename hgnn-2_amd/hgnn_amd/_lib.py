@@ -105,6 +105,7 @@ SIGNATURES = {
     "hgnn_ccn_backward": ([ctypes.POINTER(CcnConfig), ctypes.POINTER(ctypes.c_longlong), _VP, _VP,
                            ctypes.c_longlong, _VP, _VP, _VP, _VP, _VP], _I),
     "hgnn_ccn_small_supported": ([ctypes.POINTER(CcnConfig)], _I),
+    "hgnn_host_word_alloc": ([ctypes.POINTER(_VP), ctypes.POINTER(_VP)], _I),
     "hgnn_ccn_small_workspace_bytes": ([ctypes.POINTER(CcnConfig)], ctypes.c_size_t),
     "hgnn_ccn_small_forward": ([ctypes.POINTER(CcnConfig), _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _VP], _I),
     "hgnn_ccn_small_backward": ([ctypes.POINTER(CcnConfig), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP], _I),

@@ -24,7 +24,7 @@ import os
 import torch
 
 from . import _lib as L
-from .net import _require_cuda, _f32, _i64, _raise_bits, check_errors, watch_word
+from .net import _require_cuda, _f32, _i64, _raise_bits, check_errors, register_check, strict, watch_word
 
 # CCN_1D on graphs of <= 64 nodes through the one-workgroup-per-graph kernels (csrc/ccn_small.hip):
 # no plan, no workspace sizing, 1 + 1 dispatches per call for one graph.  HGNN_CCN_SMALL=0 (or setting
@@ -156,28 +156,51 @@ class _CcnFn(torch.autograd.Function):
         return (None, None, dX, None, None, *grads)
 
 
-class _TagWord:
-    """Per-device validation word of the small-graph kernels: each call passes a new tag and the
-    kernels leave atomicMax(word, tag * 256 + bits), so the word is never zeroed between calls."""
+class _HostWord:
+    """Validation word of the small-graph kernels in host-mapped pinned memory (hgnn_host_word_alloc):
+    a call passes a new tag and a graph with validation bits stores tag * 256 + bits into it, so a
+    check is a host read -- no copy, no event, nothing enqueued per call.  A word whose tag is above the
+    last one reported is a new error (found by the first check after that kernel has run; HGNN_STRICT=1
+    or check_errors() synchronise first)."""
 
     def __init__(self):
-        self.words = {}
+        self.words = {}      # device index -> (ctypes int32 view of the host word, device pointer)
         self.tag = 0
+        self.reported = 0
 
     def next(self, dev):
-        w = self.words.get(dev)
+        w = self.words.get(dev.index)
+        if w is None:
+            h, d = ctypes.c_void_p(), ctypes.c_void_p()
+            with torch.cuda.device(dev):
+                L.check(L.lib().hgnn_host_word_alloc(ctypes.byref(h), ctypes.byref(d)), "hgnn_host_word_alloc")
+            w = (ctypes.c_int32.from_address(h.value), d)
+            self.words[dev.index] = w
         self.tag += 1
-        if w is None or self.tag >= (1 << 23):
-            if w is None:
-                w = torch.zeros(1, dtype=torch.int32, device=dev)
-                self.words[dev] = w
-            else:  # wrap: older tags must not outrank the new ones
-                w.zero_()
-            self.tag = 1 if self.tag >= (1 << 23) else self.tag
-        return w, self.tag
+        if self.tag >= (1 << 23):  # wrap: nothing in flight may carry an old tag
+            torch.cuda.synchronize()
+            for hw, _ in self.words.values():
+                hw.value = 0
+            self.tag, self.reported = 1, 0
+        return w[1], self.tag
+
+    def check(self, block):
+        if not self.words:
+            return
+        if block:
+            torch.cuda.synchronize()
+        bad = 0
+        for hw, _ in self.words.values():
+            v = hw.value
+            if (v >> 8) > self.reported and (v & 255):
+                self.reported = v >> 8
+                bad |= v & 255
+        if bad:
+            _raise_bits(bad)
 
 
-_tags = _TagWord()
+_word = _HostWord()
+register_check(_word.check)
 
 
 class _CcnSmallFn(torch.autograd.Function):
@@ -189,11 +212,12 @@ class _CcnSmallFn(torch.autograd.Function):
         s = L.stream_handle(X.device)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=X.device)
         out = torch.empty(bs, spec.n_out, dtype=torch.float32, device=X.device)
-        err, tag = _tags.next(X.device)
+        err, tag = _word.next(X.device)
         L.check(lib.hgnn_ccn_small_forward(ctypes.byref(cfg), L.ptr(X), L.ptr(adj), L.ptr(n_batch),
-                                           L.ptr_array(params), L.ptr(ws), L.ptr(err), tag, L.ptr(out), s),
+                                           L.ptr_array(params), L.ptr(ws), err, tag, L.ptr(out), s),
                 "hgnn_ccn_small_forward")
-        watch_word(err, tag)
+        if strict():
+            _word.check(True)
         ctx.cfg, ctx.ws, ctx.X, ctx.adj, ctx.nb, ctx.params = cfg, ws, X, adj, n_batch, params
         return out
 

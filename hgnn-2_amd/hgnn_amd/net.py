@@ -103,10 +103,19 @@ def _word_bits(v, tag):
     return v & 255 if (v >> 8) == tag else 0
 
 
+_checks = []  # further validation words with their own check(block) (hgnn_amd.ccn host-mapped word)
+
+
+def register_check(fn):
+    _checks.append(fn)
+
+
 def check_errors(block=True):
     """Raise if any enqueued forward found an invalid input batch."""
     if _capturing():
         return
+    for fn in _checks:
+        fn(block)
     keep = []
     bad = 0
     for ev, slot, tag in _pending:

@@ -326,11 +326,15 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
  * summed in a different order).  d_n_batch may be NULL (every graph has nmax nodes).
  * supported: 1 if cfg fits (the LDS of the backward, 4 nmax^2 (hidden L + 2 max(f_in, hidden) +
  * 2 hidden) + 8 KB, within 160 KB), else 0 (use the general path).
- * Validation (self loops, symmetric pattern, 0 <= n_b <= nmax) is reported as
- * atomicMax(*d_err, tag * 256 + bits) with 0 < tag < 2^23: a caller that increases tag per call reads
- * its own call's bits as (word >> 8 == tag ? word & 255 : 0) without ever zeroing the word.
+ * Validation (self loops, symmetric pattern, 0 <= n_b <= nmax): a graph with bits stores
+ * *d_err = tag * 256 + bits (0 < tag < 2^23; nothing is stored when the batch is valid), so a caller
+ * that increases tag per call never zeroes the word and reads a new error as a tag above the last one
+ * it reported.  d_err may be the device alias of a host-mapped word (hgnn_host_word_alloc): the
+ * check is then a host read, with no copy or event per call.
  * The workspace holds the readout features between forward and backward. */
 int hgnn_ccn_small_supported(const hgnn_ccn_config* cfg);
+/* A 64-byte host-mapped, coherent word block (zeroed): *host_ptr for the host, *dev_ptr for kernels. */
+int hgnn_host_word_alloc(void** host_ptr, void** dev_ptr);
 size_t hgnn_ccn_small_workspace_bytes(const hgnn_ccn_config* cfg);
 int hgnn_ccn_small_forward(const hgnn_ccn_config* cfg, const float* d_X, const float* d_adj,
                            const int64_t* d_n_batch, const float* const* params, void* workspace,
