@@ -306,6 +306,8 @@ int launch_agg_fwd(const AggFwdArgs& a, hipStream_t s) {
         case 3: return agg_fwd_cg<3>(a, g, s);
         case 4: return agg_fwd_cg<4>(a, g, s);
         case 5: return agg_fwd_cg<5>(a, g, s);
+        case 6: return agg_fwd_cg<6>(a, g, s);
+        case 7: return agg_fwd_cg<7>(a, g, s);
         default: return 2;
     }
 }
@@ -482,6 +484,8 @@ int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s) {
         case 3: return agg_bwd_c<3>(a, s);
         case 4: return agg_bwd_c<4>(a, s);
         case 5: return agg_bwd_c<5>(a, s);
+        case 6: return agg_bwd_c<6>(a, s);
+        case 7: return agg_bwd_c<7>(a, s);
         default: return 2;
     }
 }
@@ -521,6 +525,8 @@ int launch_agg_bwd_pair(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t 
         case 3: return agg_bwd_pair_j<3>(ga, pa, s);
         case 4: return agg_bwd_pair_j<4>(ga, pa, s);
         case 5: return agg_bwd_pair_j<5>(ga, pa, s);
+        case 6: return agg_bwd_pair_j<6>(ga, pa, s);
+        case 7: return agg_bwd_pair_j<7>(ga, pa, s);
         default: return 2;
     }
 }

@@ -271,7 +271,7 @@ int hgnn_graph_edge_slots(int n, const float* A) {
 }
 
 int hgnn_graph_operators(int n, const float* A, int J, int dual, float* W, int m, float* WL, float* Pm, float* Pd) {
-    if (n <= 0 || !A || !W || J < 1 || J > 3) return HGNN_ERR_ARG;
+    if (n <= 0 || !A || !W || J < 1 || J > 5) return HGNN_ERR_ARG;
     const int jt = J + 2;
     const Sp a = adjacency(n, A);
     const Ops w = slices(a, jt);
@@ -299,7 +299,7 @@ int hgnn_graph_operators(int n, const float* A, int J, int dual, float* W, int m
 // (the layout the caller sized the image with).
 static int csr_batch(int bs, const int* n_nodes, const float* const* A, const float* const* X, int f_in, int J,
                      int dual, const hgnn_csr_layout* expect, hgnn_csr_layout* lay, void* image) {
-    if (bs <= 0 || !n_nodes || !A || !lay || f_in <= 0 || J < 1 || J > 3) return HGNN_ERR_ARG;
+    if (bs <= 0 || !n_nodes || !A || !lay || f_in <= 0 || J < 1 || J > 5) return HGNN_ERR_ARG;
     const int jt = J + 2;
     const int sw = jt <= 3 ? 4 : 8;
     std::vector<GraphBuild> gs(bs);

@@ -74,7 +74,7 @@ bool valid_config(const hgnn_net_config* c) {
     if (c->bs <= 0 || c->nmax <= 0 || c->f_in <= 0 || c->d <= 0 || c->n_layers < 2) return false;
     if (c->dim_out <= 0) return false;
     if (c->kind == 1 && (c->emax < 0 || c->order < 1 || c->order > 3)) return false;
-    if (c->j_tot < 3 || c->j_tot > 5) return false;
+    if (c->j_tot < 3 || c->j_tot > 7) return false;  // entries of 8 floats: column + up to 7 slices
     if (2 * c->d > 512) return false;
     const long long capn = (long long)c->bs * c->nmax;
     const long long cape = (long long)c->bs * (c->kind == 1 ? c->emax : 0);
@@ -243,7 +243,7 @@ Program build_program(const hgnn_net_config* c) {
     }
     size_t max_da = 0, max_slab = 0;
     int max_cap = 0;
-    P.fused = P.c2 % 16 == 0 && P.c2 <= 256 && fused_enabled();
+    P.fused = P.c2 % 16 == 0 && P.c2 <= 256 && c->j_tot <= 5 && fused_enabled();
     P.fused_bwd = P.fused && env_flag("HGNN_FUSED_BWD", false);
     for (auto& h : P.halves) {
         const int cap = h.edge ? P.cap_e : P.cap_n;

@@ -504,6 +504,8 @@ static int extract_one(const ExtractArgs& a, dim3 grid, hipStream_t s) {
         case 3: hipLaunchKernelGGL(k_extract<3>, grid, dim3(X_THREADS), 0, s, a); break;
         case 4: hipLaunchKernelGGL(k_extract<4>, grid, dim3(X_THREADS), 0, s, a); break;
         case 5: hipLaunchKernelGGL(k_extract<5>, grid, dim3(X_THREADS), 0, s, a); break;
+        case 6: hipLaunchKernelGGL(k_extract<6>, grid, dim3(X_THREADS), 0, s, a); break;
+        case 7: hipLaunchKernelGGL(k_extract<7>, grid, dim3(X_THREADS), 0, s, a); break;
         default: return 2;
     }
     HGNN_LAUNCH_CHECK();
@@ -521,6 +523,8 @@ int launch_extract(const ExtractArgs& a, hipStream_t s) {
             case 3: extract_lds_launch<3>(a, lds, s); break;
             case 4: extract_lds_launch<4>(a, lds, s); break;
             case 5: extract_lds_launch<5>(a, lds, s); break;
+            case 6: extract_lds_launch<6>(a, lds, s); break;
+            case 7: extract_lds_launch<7>(a, lds, s); break;
             default: return 2;
         }
         HGNN_LAUNCH_CHECK();

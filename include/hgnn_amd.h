@@ -31,7 +31,7 @@
  * Size limits (a call outside them returns HGNN_ERR_UNSUPPORTED or HGNN_ERR_ARG before anything
  * is enqueued, or -- for data-dependent bounds -- sets a device error bit; the reference has no
  * such limits, the Python layer raises RuntimeError):
- *  - networks: J + 2 in [3, 5]; any d with 2d <= 512 (odd 2d runs the same MFMA GEMMs over a
+ *  - networks: J + 2 in [3, 7] (J <= 5; operator values exact below 2^24 as in the reference's fp32 powers); any d with 2d <= 512 (odd 2d runs the same MFMA GEMMs over a
  *    row stride padded to 4); the GEMMs address each operand through a 32-bit buffer resource,
  *    so every per-call operand must stay under 2 GB -- about 12 K QM9-shape graphs per call at
  *    d = 64 (the 640-wide edge aggregate is the largest; split larger batches); the dense

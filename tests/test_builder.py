@@ -41,11 +41,16 @@ def test_graph_operators_native_vs_loop_oracle():
     for X, A, _ in _graphs():
         if X.shape[0] == 1:
             continue  # the reference's torch.diag(d.squeeze()) raises on a 1-node graph
-        for J in (1, 2):
+        for J in (1, 2, 3, 4, 5):
             got = graph_operators([X, A], J, True)
             ref = R.graph_operators([X, A], J, True)
             for a, b in zip(got, ref):
-                assert a.shape == b.shape and torch.equal(a, b)
+                assert a.shape == b.shape
+                if J <= 3:
+                    assert torch.equal(a, b), J
+                else:  # A^8, A^16 of weighted adjacencies: the reference's fp32 matmul rounds per product
+                    # and sum, the builder squares in fp64 and rounds once (parity within fp32, unpinned bits)
+                    assert torch.allclose(a, b, rtol=2e-6, atol=0), J
 
 
 def test_graph_operators_native_speed():
