@@ -17,6 +17,7 @@ forward" roofline):
          MSE, backward, Adamax step per graph)
   cfg4   GNN_lg d=128 order 2 L=5, 512 QM9-shape graphs (one GPU's share of 4096)
   cfg5   CCN_2D(5, 1, 2, 2), 64 SBM N=200 graphs (A + I)
+  cfg5_pergraph  the same 64 graphs one at a time (forward, MSE, backward, Adamax step per graph)
 
 Prints one JSON line per configuration.  Usage:
   python tools/bench_configs.py [--only cfg3,cfg5] [--steps 20] [--warmup 5]
@@ -299,6 +300,10 @@ def main():
             "256 QM9-shape graphs", max(2, a.steps // 5), 1),
         "cfg4": lambda: run_lg("cfg4", "GNN_lg d=128 order 2 L=5 fwd+bwd, 512 QM9-shape (1 GPU of 4096)", 128, 2,
                                512, a.steps, a.warmup),
+        "cfg5_pergraph": lambda: run_ccn_pergraph(
+            "cfg5_pergraph", 2, dg.sbm_dataset(64, n=200, seed=0),
+            "CCN_2D(5,1,2,2) per graph as scripts/train_ccn.py: net(X, A+I), MSE, backward, Adamax step; "
+            "64 SBM N=200 graphs", 2, 1),
         "cfg5": lambda: run_ccn("cfg5", 2, dg.sbm_dataset(64, n=200, seed=0),
                                 "CCN_2D(5,1,2,2) fwd+bwd, 64 SBM N=200 graphs", max(3, a.steps // 4),
                                 max(1, a.warmup // 2)),
