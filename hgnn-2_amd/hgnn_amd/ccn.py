@@ -24,7 +24,8 @@ import os
 import torch
 
 from . import _lib as L
-from .net import _require_cuda, _f32, _i64, _raise_bits, check_errors, register_check, strict, watch_word
+from .net import (_capturing, _require_cuda, _f32, _i64, _raise_bits, check_errors, register_check, strict,
+                  watch_word)
 
 # CCN_1D on graphs of <= 64 nodes through the one-workgroup-per-graph kernels (csrc/ccn_small.hip):
 # no plan, no workspace sizing, 1 + 1 dispatches per call for one graph.  HGNN_CCN_SMALL=0 (or setting
@@ -216,7 +217,7 @@ class _CcnSmallFn(torch.autograd.Function):
         L.check(lib.hgnn_ccn_small_forward(ctypes.byref(cfg), L.ptr(X), L.ptr(adj), L.ptr(n_batch),
                                            L.ptr_array(params), L.ptr(ws), err, tag, L.ptr(out), s),
                 "hgnn_ccn_small_forward")
-        if strict():
+        if strict() and not _capturing():
             _word.check(True)
         ctx.cfg, ctx.ws, ctx.X, ctx.adj, ctx.nb, ctx.params = cfg, ws, X, adj, n_batch, params
         return out
@@ -238,9 +239,10 @@ def run_ccn(spec, params, X, adj, n_batch, plan=None):
     """Batched CCN forward: X (bs,nmax,f), adj (bs,nmax,nmax), n_batch (bs,) -> (bs, n_out).
     plan: a CcnPlan of this adj / n_batch (else the plan is built here: without a host sync for
     small shapes, ASYNC_PLAN_BOUND; with one otherwise).  n_batch None: every graph has nmax nodes.
-    CCN_1D batches of <= 64-node graphs without a plan take the small-graph kernels (SMALL)."""
+    CCN_1D batches of <= 64-node graphs take the small-graph kernels (SMALL; a plan is then unused)."""
     check_errors(block=False)
-    if plan is None and SMALL and spec.order == 1 and X.dim() == 3:
+    # the small-graph kernels need no plan: a batch planned for capture (CcnPlan) takes them too
+    if SMALL and spec.order == 1 and X.dim() == 3:
         small = spec.small(X.shape[0], X.shape[1])
         if small is not None:
             _require_cuda([X, adj, n_batch, *params], "CCN")

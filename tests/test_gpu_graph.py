@@ -79,9 +79,14 @@ def test_graph_replay_equals_eager_step(kind):
     assert torch.equal(X.grad, ref_dx)
 
 
-def test_ccn1_graph_replay_with_plan_equals_eager():
+@pytest.mark.parametrize("small", [False, True])
+def test_ccn1_graph_replay_with_plan_equals_eager(small, monkeypatch):
+    """Captured CCN-1D step (general path with a CcnPlan, or the small-graph kernels that need none)
+    replays bit-identically to the eager step."""
+    import hgnn_amd.ccn as HC
     import hgnn_amd.datagen as dg
     from models.compnets.model_ccn import CCN_1D
+    monkeypatch.setattr(HC, "SMALL", small)
     graphs = [(x, a + torch.eye(a.shape[0]), t) for x, a, t in dg.qm9_shape_dataset(32, seed=14)]
     bs, nmax = len(graphs), max(x.shape[0] for x, _, _ in graphs)
     X = torch.zeros(bs, nmax, 5)
