@@ -304,6 +304,18 @@ __device__ __forceinline__ void cs_update(const CsLds& s, CsSlot sl, const float
     }
 }
 
+// One level of the forward walk: F_l of every node (CF = the level's channel bound)
+template <int CF>
+__device__ __forceinline__ void cs_fwd_level(const CsLds& s, int n, int G, const float* Xg, const float* fin, int cin,
+                                             const float* Wl, int h, float* fout) {
+    for (int base = 0; base < n; base += CS_NW * (64 / G)) {
+        const CsSlot sl = cs_slot(base, G, n);
+        float rs[CF], colv[CF];
+        cs_collect<CF>(s, sl, G, Xg, fin, cin, rs, colv);
+        cs_update<CF>(s, sl, rs, colv, cin, Wl, Wl + h * 2 * cin, h, fout);
+    }
+}
+
 // Readout column sums in fp64 (k_ccn_readout_part's order for a one-chunk graph): vec[col0 + c] =
 // sum over rows r of val(r, c), rows over the first 256 threads, then their 4 waves.
 template <int CF, typename V>
@@ -366,13 +378,9 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_fwd(CsArgs a) {
     for (int l = 0; l < a.L; ++l) {
         const int cin = l == 0 ? f : h;
         float* fout = s.F + (size_t)(l & 1) * a.rcap * h;
-        for (int base = 0; base < n; base += CS_NW * (64 / G)) {
-            const CsSlot sl = cs_slot(base, G, n);
-            float rs[CF], colv[CF];
-            cs_collect<CF>(s, sl, G, Xg, fin, cin, rs, colv);
-            const float* Wl = s.Ws + cs_woff(l, f, h);
-            cs_update<CF>(s, sl, rs, colv, cin, Wl, Wl + h * 2 * cin, h, fout);
-        }
+        const float* Wl = s.Ws + cs_woff(l, f, h);
+        if (cin <= 2) cs_fwd_level<2>(s, n, G, Xg, fin, cin, Wl, h, fout);
+        else cs_fwd_level<CF>(s, n, G, Xg, fin, cin, Wl, h, fout);
         __syncthreads();
         CS_STAMP(4 + 2 * l);
         cs_colsum<CF>(s, rows, h, f + l * h, [&](int r, int c) { return (double)fout[r * h + c]; });
@@ -400,11 +408,155 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_fwd(CsArgs a) {
     CS_STAMP(31);
 }
 
+// One level of the backward walk (node pass, parameter gradients, gather), CF = this level's channel
+// bound (levels of hidden <= 2 take CF = 2: a quarter of the loads and selects of the 8-channel form).
+template <int CF, int CH>
+__device__ void cs_bwd_level(const CsArgs& a, const CsLds& s, int b, int l, int n, int G, const float* Xg,
+                             const float* dFc, float* dFn) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    (void)wv;
+    const int h = a.h, f = a.f, L = a.L;
+    (void)L;
+    const int p0 = h * 2 * f + h, p1 = h * 2 * h + h;
+    const int cin = l == 0 ? f : h, k2 = 2 * cin;
+    const float* W = s.Ws + cs_woff(l, f, h);
+    const float* Fl = s.F + (size_t)l * a.rcap * h;
+    const float* fin = l == 0 ? nullptr : s.F + (size_t)(l - 1) * a.rcap * h;
+    const bool top = l == L - 1;
+    const float* dtop = s.vec + f + (L - 1) * h;
+    // node pass: dpre = dF relu', per-lane parameter sums, dcoll = W^T dpre (k_ccn1_bwd_node's order)
+    float aw[CH][CF], ac[CH][CF], ab[CH];
+#pragma unroll
+    for (int o = 0; o < CH; ++o) {
+        ab[o] = 0.f;
+#pragma unroll
+        for (int c = 0; c < CF; ++c) aw[o][c] = ac[o][c] = 0.f;
+    }
+    for (int base = 0; base < n; base += CS_NW * (64 / G)) {
+        const CsSlot sl = cs_slot(base, G, n);
+        float rs[CF], colv[CF];
+        cs_collect<CF>(s, sl, G, Xg, fin, cin, rs, colv);
+        const int ii = sl.i >= 0 ? sl.i : 0;
+        const bool vx = sl.i >= 0 && sl.p < s.deg[ii];
+        const int row = s.off1[ii] + sl.p;
+        float dp[CH];
+#pragma unroll
+        for (int o = 0; o < CH; ++o) {
+            const float g = top ? dtop[o] : dFc[row * h + o];  // unconditional LDS reads
+            dp[o] = (vx && o < h && Fl[row * h + o] > 0.f) ? g : 0.f;
+            ab[o] += dp[o];
+#pragma unroll
+            for (int c = 0; c < CF; ++c) {
+                aw[o][c] = fmaf(dp[o], rs[c], aw[o][c]);
+                ac[o][c] = fmaf(dp[o], colv[c], ac[o][c]);
+            }
+        }
+        if (vx)
+            for (int k = 0; k < k2; ++k) {
+                float t = 0.f;
+#pragma unroll
+                for (int o = 0; o < CH; ++o)
+                    if (o < h) t = fmaf(W[o * k2 + k], dp[o], t);
+                s.dcoll[row * k2 + k] = t;
+            }
+    }
+    // level parameter gradients: lanes, then the waves in order
+#pragma unroll
+    for (int o = 0; o < CH; ++o) {
+        if (o >= h) break;
+#pragma unroll
+        for (int c = 0; c < CF; ++c) {
+            if (c >= cin) break;
+            const float tw = wave_total(aw[o][c]);
+            const float tc = wave_total(ac[o][c]);
+            if (lane == 0) {
+                s.red[wv * CS_PMAX + o * k2 + c] = tw;
+                s.red[wv * CS_PMAX + o * k2 + cin + c] = tc;
+            }
+        }
+        const float tb = wave_total(ab[o]);
+        if (lane == 0) s.red[wv * CS_PMAX + h * k2 + o] = tb;
+    }
+    __syncthreads();
+    const int P = h * k2 + h;
+    for (int p = threadIdx.x; p < P; p += CS_NT) {
+        float v = s.red[p];
+#pragma unroll
+        for (int w = 1; w < CS_NW; ++w) v += s.red[w * CS_PMAX + p];
+        if (a.bs == 1) {
+            if (p < h * k2) a.gW[l][p] = v;
+            else a.gB[l][p - h * k2] = v;
+        } else {
+            const int poff = l == 0 ? 0 : p0 + (l - 1) * p1;
+            a.ppart[(long long)b * (p0 + (L - 1) * p1) + poff + p] = v;
+        }
+    }
+    // gather: dF_{l-1}[j][u] = sum_{i in N(j)} [q valid] (drow_i[q] + dcol_i[pos of j]) + readout term;
+    // level 0: dX[j] = the sum over u + d_j dsum  (k_ccn1_bwd_gather's order)
+    for (int base = 0; base < n; base += CS_NW * (64 / G)) {
+        const CsSlot sl = cs_slot(base, G, n);
+        const int j = sl.i >= 0 ? sl.i : 0;
+        const int d = sl.i >= 0 ? s.deg[j] : 0;
+        const bool vu = sl.p < d;
+        const int uu = s.nbr[j * 64 + (vu ? sl.p : 0)];
+        const unsigned long long bu = (1ull << uu) - 1ull, bj = (1ull << j) - 1ull;
+        const int dl = d > 0 ? d - 1 : 0;
+        float acc[CF];
+#pragma unroll
+        for (int c = 0; c < CF; ++c) acc[c] = 0.f;
+        for (int a0 = 0; a0 < G; a0 += 4) {
+            int ik[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ik[q] = s.nbr[j * 64 + min(a0 + q, dl)];
+            unsigned long long m[4];
+            int ri[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                m[q] = s.bits[ik[q]];
+                ri[q] = s.off1[ik[q]];
+            }
+            float t1[4][CF], t2[4][CF];
+            bool ok[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                ok[q] = vu && ((m[q] >> uu) & 1ull) && a0 + q < d;
+                const float* s1 = s.dcoll + (ri[q] + __popcll(m[q] & bu)) * k2;
+                const float* s2 = s.dcoll + (ri[q] + __popcll(m[q] & bj)) * k2 + cin;
+#pragma unroll
+                for (int c = 0; c < CF; ++c) {  // unconditional LDS reads, discarded by the selects
+                    t1[q][c] = s1[c];
+                    t2[q][c] = s2[c];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int c = 0; c < CF; ++c)
+                    acc[c] += (c < cin && ok[q]) ? t1[q][c] + t2[q][c] : 0.f;
+        }
+        if (l > 0) {
+            if (vu)
+#pragma unroll
+                for (int c = 0; c < CF; ++c)
+                    if (c < cin) dFn[(s.off1[j] + sl.p) * cin + c] = acc[c] + s.vec[f + (l - 1) * h + c];
+        } else {
+            // the node's G lanes summed by an xor tree: with zeros past d this is wave_total's association
+#pragma unroll
+            for (int c = 0; c < CF; ++c) {
+                if (c >= cin) break;
+                float tot = vu ? acc[c] : 0.f;
+                for (int o = 1; o < G; o <<= 1) tot += __shfl_xor(tot, o, 64);
+                if (sl.i >= 0 && sl.p == 0) a.dX[((long long)b * a.nmax + j) * f + c] = tot + (float)d * s.vec[c];
+            }
+        }
+    }
+    __syncthreads();
+}
+
 template <int CF, int CH>
 __global__ void __launch_bounds__(CS_NT) k_ccn1_small_bwd(CsArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int b = blockIdx.x;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const CsLds s = cs_carve(lds, a, true);
     uint32_t bad = 0;
     const int n = cs_nodes(a, b, bad);
@@ -418,13 +570,9 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_bwd(CsArgs a) {
         const int cin = l == 0 ? f : h;
         const float* fin = l == 0 ? nullptr : s.F + (size_t)(l - 1) * a.rcap * h;
         float* fout = s.F + (size_t)l * a.rcap * h;
-        for (int base = 0; base < n; base += CS_NW * (64 / G)) {
-            const CsSlot sl = cs_slot(base, G, n);
-            float rs[CF], colv[CF];
-            cs_collect<CF>(s, sl, G, Xg, fin, cin, rs, colv);
-            const float* Wl = s.Ws + cs_woff(l, f, h);
-            cs_update<CF>(s, sl, rs, colv, cin, Wl, Wl + h * 2 * cin, h, fout);
-        }
+        const float* Wl = s.Ws + cs_woff(l, f, h);
+        if (cin <= 2) cs_fwd_level<2>(s, n, G, Xg, fin, cin, Wl, h, fout);
+        else cs_fwd_level<CF>(s, n, G, Xg, fin, cin, Wl, h, fout);
         __syncthreads();
     }
     // dsum[k] = sum_o dout[b][o] fcw[o][k] (k_ccn_readout_bwd's order); one graph: the fc gradients here
@@ -440,143 +588,11 @@ __global__ void __launch_bounds__(CS_NT) k_ccn1_small_bwd(CsArgs a) {
             else a.gfcb[w - a.n_out * nf] = (float)(double)dob[w - a.n_out * nf];
         }
     __syncthreads();
-    const int p0 = h * 2 * f + h, p1 = h * 2 * h + h;
     float* dFc = s.dF0;
     float* dFn = s.dF1;
     for (int l = L - 1; l >= 0; --l) {
-        const int cin = l == 0 ? f : h, k2 = 2 * cin;
-        const float* W = s.Ws + cs_woff(l, f, h);
-        const float* Fl = s.F + (size_t)l * a.rcap * h;
-        const float* fin = l == 0 ? nullptr : s.F + (size_t)(l - 1) * a.rcap * h;
-        const bool top = l == L - 1;
-        const float* dtop = s.vec + f + (L - 1) * h;
-        // node pass: dpre = dF relu', per-lane parameter sums, dcoll = W^T dpre (k_ccn1_bwd_node's order)
-        float aw[CH][CF], ac[CH][CF], ab[CH];
-#pragma unroll
-        for (int o = 0; o < CH; ++o) {
-            ab[o] = 0.f;
-#pragma unroll
-            for (int c = 0; c < CF; ++c) aw[o][c] = ac[o][c] = 0.f;
-        }
-        for (int base = 0; base < n; base += CS_NW * (64 / G)) {
-            const CsSlot sl = cs_slot(base, G, n);
-            float rs[CF], colv[CF];
-            cs_collect<CF>(s, sl, G, Xg, fin, cin, rs, colv);
-            const int ii = sl.i >= 0 ? sl.i : 0;
-            const bool vx = sl.i >= 0 && sl.p < s.deg[ii];
-            const int row = s.off1[ii] + sl.p;
-            float dp[CH];
-#pragma unroll
-            for (int o = 0; o < CH; ++o) {
-                const float g = top ? dtop[o] : dFc[row * h + o];  // unconditional LDS reads
-                dp[o] = (vx && o < h && Fl[row * h + o] > 0.f) ? g : 0.f;
-                ab[o] += dp[o];
-#pragma unroll
-                for (int c = 0; c < CF; ++c) {
-                    aw[o][c] = fmaf(dp[o], rs[c], aw[o][c]);
-                    ac[o][c] = fmaf(dp[o], colv[c], ac[o][c]);
-                }
-            }
-            if (vx)
-                for (int k = 0; k < k2; ++k) {
-                    float t = 0.f;
-#pragma unroll
-                    for (int o = 0; o < CH; ++o)
-                        if (o < h) t = fmaf(W[o * k2 + k], dp[o], t);
-                    s.dcoll[row * k2 + k] = t;
-                }
-        }
-        // level parameter gradients: lanes, then the waves in order
-#pragma unroll
-        for (int o = 0; o < CH; ++o) {
-            if (o >= h) break;
-#pragma unroll
-            for (int c = 0; c < CF; ++c) {
-                if (c >= cin) break;
-                const float tw = wave_total(aw[o][c]);
-                const float tc = wave_total(ac[o][c]);
-                if (lane == 0) {
-                    s.red[wv * CS_PMAX + o * k2 + c] = tw;
-                    s.red[wv * CS_PMAX + o * k2 + cin + c] = tc;
-                }
-            }
-            const float tb = wave_total(ab[o]);
-            if (lane == 0) s.red[wv * CS_PMAX + h * k2 + o] = tb;
-        }
-        __syncthreads();
-        const int P = h * k2 + h;
-        for (int p = threadIdx.x; p < P; p += CS_NT) {
-            float v = s.red[p];
-#pragma unroll
-            for (int w = 1; w < CS_NW; ++w) v += s.red[w * CS_PMAX + p];
-            if (a.bs == 1) {
-                if (p < h * k2) a.gW[l][p] = v;
-                else a.gB[l][p - h * k2] = v;
-            } else {
-                const int poff = l == 0 ? 0 : p0 + (l - 1) * p1;
-                a.ppart[(long long)b * (p0 + (L - 1) * p1) + poff + p] = v;
-            }
-        }
-        // gather: dF_{l-1}[j][u] = sum_{i in N(j)} [q valid] (drow_i[q] + dcol_i[pos of j]) + readout term;
-        // level 0: dX[j] = the sum over u + d_j dsum  (k_ccn1_bwd_gather's order)
-        for (int base = 0; base < n; base += CS_NW * (64 / G)) {
-            const CsSlot sl = cs_slot(base, G, n);
-            const int j = sl.i >= 0 ? sl.i : 0;
-            const int d = sl.i >= 0 ? s.deg[j] : 0;
-            const bool vu = sl.p < d;
-            const int uu = s.nbr[j * 64 + (vu ? sl.p : 0)];
-            const unsigned long long bu = (1ull << uu) - 1ull, bj = (1ull << j) - 1ull;
-            const int dl = d > 0 ? d - 1 : 0;
-            float acc[CF];
-#pragma unroll
-            for (int c = 0; c < CF; ++c) acc[c] = 0.f;
-            for (int a0 = 0; a0 < G; a0 += 4) {
-                int ik[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) ik[q] = s.nbr[j * 64 + min(a0 + q, dl)];
-                unsigned long long m[4];
-                int ri[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    m[q] = s.bits[ik[q]];
-                    ri[q] = s.off1[ik[q]];
-                }
-                float t1[4][CF], t2[4][CF];
-                bool ok[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    ok[q] = vu && ((m[q] >> uu) & 1ull) && a0 + q < d;
-                    const float* s1 = s.dcoll + (ri[q] + __popcll(m[q] & bu)) * k2;
-                    const float* s2 = s.dcoll + (ri[q] + __popcll(m[q] & bj)) * k2 + cin;
-#pragma unroll
-                    for (int c = 0; c < CF; ++c) {  // unconditional LDS reads, discarded by the selects
-                        t1[q][c] = s1[c];
-                        t2[q][c] = s2[c];
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-#pragma unroll
-                    for (int c = 0; c < CF; ++c)
-                        acc[c] += (c < cin && ok[q]) ? t1[q][c] + t2[q][c] : 0.f;
-            }
-            if (l > 0) {
-                if (vu)
-#pragma unroll
-                    for (int c = 0; c < CF; ++c)
-                        if (c < cin) dFn[(s.off1[j] + sl.p) * cin + c] = acc[c] + s.vec[f + (l - 1) * h + c];
-            } else {
-                // the node's G lanes summed by an xor tree: with zeros past d this is wave_total's association
-#pragma unroll
-                for (int c = 0; c < CF; ++c) {
-                    if (c >= cin) break;
-                    float tot = vu ? acc[c] : 0.f;
-                    for (int o = 1; o < G; o <<= 1) tot += __shfl_xor(tot, o, 64);
-                    if (sl.i >= 0 && sl.p == 0) a.dX[((long long)b * a.nmax + j) * f + c] = tot + (float)d * s.vec[c];
-                }
-            }
-        }
-        __syncthreads();
+        if ((l == 0 ? f : h) <= 2) cs_bwd_level<2, CH>(a, s, b, l, n, G, Xg, dFc, dFn);
+        else cs_bwd_level<CF, CH>(a, s, b, l, n, G, Xg, dFc, dFn);
         float* t = dFc;
         dFc = dFn;
         dFn = t;
