@@ -483,3 +483,32 @@ def test_ccn1_small_graph_path_validation():
     # a clean call after the failures raises nothing (tags: older words do not count)
     net(torch.randn(4, 5).cuda(), torch.eye(4).cuda())
     check_errors()
+
+
+def test_ccn1_small_graph_path_ragged_edge_cases():
+    """Ragged batch with a single-node graph, an empty slot (n_b = 0) and a QM9-shape graph: the small-graph
+    kernels equal the general path (outputs, dX, zeroed padding rows) and the empty slot reads fc.bias."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_1D
+    (xq, aq, _), = dg.qm9_shape_dataset(1, seed=9)
+    n = xq.shape[0]
+    X = torch.zeros(3, n, 5)
+    A = torch.zeros(3, n, n)
+    X[0, :1] = torch.randn(1, 5)
+    A[0, 0, 0] = 1.0
+    X[2, :n] = xq
+    A[2, :n, :n] = aq + torch.eye(n)
+    nb = torch.tensor([1, 0, n], dtype=torch.int64)
+    net = CCN_1D(5, 1, 2, 2)
+    fu.det_init(net, 909)
+    net = net.cuda()
+    X, A, nb = X.cuda(), A.cuda(), nb.cuda()
+    w = torch.ones(3, 1).cuda()
+    os_, dxs, gs = _run_path(True, net, X, A, nb, w)
+    og, dxg, gg = _run_path(False, net, X, A, nb, w)
+    assert torch.equal(os_, og)
+    assert torch.equal(dxs, dxg)
+    for k in gg:
+        _grad_close(gs[k], gg[k], f"ragged grad {k}")
+    assert torch.equal(os_[1], net.fc.bias.detach().cpu())
+    assert dxs[1].abs().max().item() == 0.0 and dxs[0, 1:].abs().max().item() == 0.0
