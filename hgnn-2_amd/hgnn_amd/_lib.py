@@ -170,5 +170,12 @@ def ptr_array(tensors):
     return arr
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_handle(device):
+    """The current HIP stream of `device` as a void* (torch's raw accessor: ~10 us less host time per call
+    than building a torch.cuda.Stream object; the per-graph CCN step makes two such calls)."""
+    if _raw_stream is not None:
+        return ctypes.c_void_p(_raw_stream(device.index if device.index is not None else torch.cuda.current_device()))
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
