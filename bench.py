@@ -11,8 +11,9 @@ graphs, hgnn_amd.dp.shard_graphs; per-layer gradient buckets are all-reduced on 
 communication stream while the earlier layers' backward still runs, and the BN
 running statistics are averaged, hgnn_amd.dp.LayerBucketAllReduce).
 
-Run:  python bench.py [--gpus N --steps K --warmup W]
+Run:  python bench.py [--gpus N --steps K --warmup W]   (N > 1: starts the N ranks itself)
       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+      (--gpus must equal the launcher's WORLD_SIZE)
 Prints ONE JSON line (rank 0) with the BASELINE metric, a live roofline of the
 dominant kernel class and HBM rooflines of the two aggregation classes (HIP
 events around their launches in a second and a third timed region of the same steps), a
@@ -159,8 +160,39 @@ def cpu_baseline(args, batch_cpu, model, gpu_res):
     return res, par
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start the N ranks as fresh child processes of
+    torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) before this process touches
+    the GPU, relay their output (rank 0's JSON line) and exit with their status.  A child, not an
+    exec: this process must never replace itself once anything could have initialised HIP."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    proc = subprocess.run(cmd, env=env)
+    if proc.returncode != 0:
+        sys.stderr.write(f"bench: the {n}-rank run failed (exit {proc.returncode})\n")
+    sys.exit(proc.returncode)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            launch_ranks(args.gpus)  # does not return
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench: --gpus {args.gpus} does not match WORLD_SIZE={os.environ['WORLD_SIZE']} "
+                 "from the launcher")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

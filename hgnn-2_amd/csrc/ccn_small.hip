@@ -80,9 +80,12 @@ struct CsLds {
     float* dF1;
 };
 
+// The level walks read CF channels of a row unconditionally and drop the ones past the row's width by
+// selects: up to CF - 1 floats past the last region (F's second ping-pong buffer forward, dF1 backward),
+// so the request carries CS_CF floats of padding and every such read stays inside the allocation.
 __host__ __device__ inline size_t cs_lds_bytes(int rcap, int f, int h, int L, bool bwd) {
     const int cmax = f > h ? f : h;
-    return CS_FIXED + 4 * (size_t)rcap * (bwd ? (size_t)h * L + 2 * cmax + 2 * h : 2 * (size_t)h);
+    return CS_FIXED + 4 * (size_t)rcap * (bwd ? (size_t)h * L + 2 * cmax + 2 * h : 2 * (size_t)h) + 4 * CS_CF;
 }
 
 __device__ inline CsLds cs_carve(char* base, const CsArgs& a, bool bwd) {
@@ -175,6 +178,9 @@ __device__ void cs_stage(const CsArgs& a, int b, int n, const CsLds& s, float* A
 __device__ uint32_t cs_plan(int n, const CsLds& s, const float* As) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t bad = 0;
+    // row 0's first entry is what an idle lane (past the graph) reads as its neighbour id: defined even
+    // for an empty slot (n = 0), so its bits / off1 reads stay inside the arrays
+    if (n == 0 && threadIdx.x == 0) s.nbr[0] = 0;
     for (int r = wv; r < n; r += CS_NW) {
         const bool nz = lane < n && As[r * n + lane] > 0.f;  // utils_ccn.py:195 (A > 0)
         const unsigned long long m = __ballot(nz);
@@ -230,7 +236,7 @@ __device__ __forceinline__ CsSlot cs_slot(int base, int G, int n) {
 // T[a][x] = F_{j_a}[pos(u_x in N(j_a))] (level 0: X[j_a] when present).  Lane-local loops over the node's
 // neighbours -- no cross-lane reduction -- in the order of k_ccn1_fwd's one-chunk path.  Branch-free: the
 // four neighbours' ids, their rows and offsets, then every channel of both reads go out as one batch of LDS
-// loads each (reads past a row stay inside the LDS allocation and are discarded by the selects).
+// loads each (reads past a row are discarded by the selects; cs_lds_bytes pads the allocation for them).
 template <int CF>
 __device__ __forceinline__ void cs_collect(const CsLds& s, CsSlot sl, int G, const float* __restrict__ Xg,
                                            const float* Fin, int cin, float (&rs)[CF], float (&colv)[CF]) {

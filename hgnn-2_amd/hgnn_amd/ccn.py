@@ -140,7 +140,7 @@ class _CcnFn(torch.autograd.Function):
         L.check(lib.hgnn_ccn_forward(ctypes.byref(cfg), sums, L.ptr(X), pa, L.ptr(plan), max_d2, L.ptr(ws),
                                      L.ptr(out), s), "hgnn_ccn_forward")
         ctx.cfg, ctx.sums, ctx.plan, ctx.ws, ctx.max_d2 = cfg, sums, plan, ws, max_d2
-        ctx.params = params
+        ctx.save_for_backward(*params)  # weights: an in-place change before backward raises
         ctx.x_shape = X.shape
         return out
 
@@ -149,25 +149,27 @@ class _CcnFn(torch.autograd.Function):
         lib = L.lib()
         dout = dout.contiguous()
         dev = dout.device
-        grads = [torch.empty_like(p) for p in ctx.params]
+        params = ctx.saved_tensors
+        grads = [torch.empty_like(p) for p in params]
         dX = torch.empty(ctx.x_shape, dtype=torch.float32, device=dev)
-        L.check(lib.hgnn_ccn_backward(ctypes.byref(ctx.cfg), ctx.sums, L.ptr_array(ctx.params), L.ptr(ctx.plan),
+        L.check(lib.hgnn_ccn_backward(ctypes.byref(ctx.cfg), ctx.sums, L.ptr_array(params), L.ptr(ctx.plan),
                                       ctx.max_d2, L.ptr(ctx.ws), L.ptr(dout), L.ptr_array(grads), L.ptr(dX),
                                       L.stream_handle(dev)), "hgnn_ccn_backward")
         return (None, None, dX, None, None, *grads)
 
 
 class _HostWord:
-    """Validation word of the small-graph kernels in host-mapped pinned memory (hgnn_host_word_alloc):
-    a call passes a new tag and a graph with validation bits stores tag * 256 + bits into it, so a
-    check is a host read -- no copy, no event, nothing enqueued per call.  A word whose tag is above the
-    last one reported is a new error (found by the first check after that kernel has run; HGNN_STRICT=1
-    or check_errors() synchronise first)."""
+    """Validation word of the small-graph kernels in host-mapped pinned memory (hgnn_host_word_alloc),
+    one per device: a graph with validation bits stores tag * 256 + bits into it (a plain store), so a
+    check is a host read -- no copy, no event, nothing enqueued per call.  A nonzero word is an error
+    not yet reported: the check reports it and clears the word from the host, so a HIP-graph replay
+    (whose captured tag never changes) reports each failing replay again.  Found by the first check
+    after that kernel has run (HGNN_STRICT=1 or check_errors() synchronise first); an error stored
+    between a check's read and its clear is lost (the check is a host read, not an exchange)."""
 
     def __init__(self):
         self.words = {}      # device index -> (ctypes int32 view of the host word, device pointer)
         self.tag = 0
-        self.reported = 0
 
     def next(self, dev):
         w = self.words.get(dev.index)
@@ -177,12 +179,8 @@ class _HostWord:
                 L.check(L.lib().hgnn_host_word_alloc(ctypes.byref(h), ctypes.byref(d)), "hgnn_host_word_alloc")
             w = (ctypes.c_int32.from_address(h.value), d)
             self.words[dev.index] = w
-        self.tag += 1
-        if self.tag >= (1 << 23):  # wrap: nothing in flight may carry an old tag
-            torch.cuda.synchronize()
-            for hw, _ in self.words.values():
-                hw.value = 0
-            self.tag, self.reported = 1, 0
+        # the tag only labels the store (a diagnostic): reporting goes by the word being nonzero
+        self.tag = self.tag % ((1 << 23) - 1) + 1
         return w[1], self.tag
 
     def check(self, block):
@@ -193,8 +191,8 @@ class _HostWord:
         bad = 0
         for hw, _ in self.words.values():
             v = hw.value
-            if (v >> 8) > self.reported and (v & 255):
-                self.reported = v >> 8
+            if v:
+                hw.value = 0
                 bad |= v & 255
         if bad:
             _raise_bits(bad)
@@ -219,18 +217,22 @@ class _CcnSmallFn(torch.autograd.Function):
                 "hgnn_ccn_small_forward")
         if strict() and not _capturing():
             _word.check(True)
-        ctx.cfg, ctx.ws, ctx.X, ctx.adj, ctx.nb, ctx.params = cfg, ws, X, adj, n_batch, params
+        # the backward rebuilds the levels from X, adj, n_batch and the weights: saved through autograd so
+        # an in-place change between forward and backward raises instead of giving wrong gradients
+        ctx.save_for_backward(X, adj, n_batch, *params)
+        ctx.cfg, ctx.ws = cfg, ws
         return out
 
     @staticmethod
     def backward(ctx, dout):
         lib = L.lib()
+        X, adj, nb, *params = ctx.saved_tensors
         dout = dout.contiguous()
         dev = dout.device
-        grads = [torch.empty_like(p) for p in ctx.params]
-        dX = torch.empty(ctx.X.shape, dtype=torch.float32, device=dev)
-        L.check(lib.hgnn_ccn_small_backward(ctypes.byref(ctx.cfg), L.ptr(ctx.X), L.ptr(ctx.adj), L.ptr(ctx.nb),
-                                            L.ptr_array(ctx.params), L.ptr(ctx.ws), L.ptr(dout), L.ptr_array(grads),
+        grads = [torch.empty_like(p) for p in params]
+        dX = torch.empty(X.shape, dtype=torch.float32, device=dev)
+        L.check(lib.hgnn_ccn_small_backward(ctypes.byref(ctx.cfg), L.ptr(X), L.ptr(adj), L.ptr(nb),
+                                            L.ptr_array(params), L.ptr(ctx.ws), L.ptr(dout), L.ptr_array(grads),
                                             L.ptr(dX), L.stream_handle(dev)), "hgnn_ccn_small_backward")
         return (None, None, dX, None, None, *grads)
 

@@ -80,10 +80,10 @@ class _ErrorRing:
     def take(self):
         i = self.next
         self.next = (i + 1) % self.SLOTS
-        for k, (ev, slot, tag) in enumerate(_pending):  # a slot still in flight: retire its check first
+        for k, (ev, slot) in enumerate(_pending):  # a slot still in flight: retire its check first
             if slot == i:
                 ev.synchronize()
-                bits = _word_bits(int(self.host[slot]), tag)
+                bits = int(self.host[slot])
                 del _pending[k]
                 if bits:
                     _pending.clear()
@@ -93,14 +93,6 @@ class _ErrorRing:
 
 
 _ring = None
-
-
-def _word_bits(v, tag):
-    """Validation bits of a watched word: plain (tag None), or a tagged word tag * 256 + bits that
-    later calls overwrite by atomicMax (hgnn_ccn_small_forward): only this call's own tag counts."""
-    if tag is None:
-        return v
-    return v & 255 if (v >> 8) == tag else 0
 
 
 _checks = []  # further validation words with their own check(block) (hgnn_amd.ccn host-mapped word)
@@ -118,13 +110,13 @@ def check_errors(block=True):
         fn(block)
     keep = []
     bad = 0
-    for ev, slot, tag in _pending:
+    for ev, slot in _pending:
         if block:
             ev.synchronize()
         if block or ev.query():
-            bad |= _word_bits(int(_ring.host[slot]), tag)
+            bad |= int(_ring.host[slot])
         else:
-            keep.append((ev, slot, tag))
+            keep.append((ev, slot))
     _pending[:] = keep
     if bad:
         _pending.clear()
@@ -142,17 +134,16 @@ def _watch_error_word(cfg, ws):
     watch_word(ws[off:off + 4].view(torch.int32))
 
 
-def watch_word(err, tag=None):
+def watch_word(err):
     """Check a device error word (int32 view) without synchronising the stream: copied into a
-    pinned ring slot behind an event, read by a later check_errors() (HGNN_STRICT=1: at once).
-    tag: the word is tagged (see _word_bits)."""
+    pinned ring slot behind an event, read by a later check_errors() (HGNN_STRICT=1: at once)."""
     if _capturing():
         # inside a HIP graph capture (bench.py --graph): the batch was validated by the eager
         # warm-up steps; no host-visible check can be part of a replayed graph
         return
     global _ring
     if strict():
-        v = _word_bits(int(err.item()), tag)
+        v = int(err.item())
         if v:
             _raise_bits(v)
         return
@@ -162,7 +153,7 @@ def watch_word(err, tag=None):
     _ring.host[slot:slot + 1].copy_(err, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record()
-    _pending.append((ev, slot, tag))
+    _pending.append((ev, slot))
 
 
 def _require_cuda(tensors, what):
@@ -278,25 +269,28 @@ class _NetFn(torch.autograd.Function):
         _watch_error_word(cfg, ws)
         ctx.cfg = cfg
         ctx.ws = ws
-        ctx.inp = inp
+        ctx.inp = inp  # device pointers of the inputs below, read again by the backward
         ctx.spec = spec
-        ctx.keep = (X, W, XL, WL, Pm, Pd, Nb, Eb, mask, mask_lg)
-        ctx.params = params
+        # saved through autograd: an in-place change of an input or a weight between forward and
+        # backward raises the usual version error instead of giving wrong gradients
+        ctx.save_for_backward(X, W, XL, WL, Pm, Pd, Nb, Eb, mask, mask_lg, *params)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         cfg = ctx.cfg
-        X = ctx.keep[0]
+        saved = ctx.saved_tensors
+        X, W = saved[0], saved[1]
+        params = saved[10:]
         dout = dout.contiguous().to(torch.float32)
-        grads, evs, nev = _grad_targets(ctx.spec, ctx.params)
+        grads, evs, nev = _grad_targets(ctx.spec, params)
         dX = torch.empty_like(X) if ctx.needs_input_grad[2] else None
-        dW = torch.empty_like(ctx.keep[1]) if ctx.needs_input_grad[3] else None
+        dW = torch.empty_like(W) if ctx.needs_input_grad[3] else None
         cfg.need_dx = 1 if dX is not None else 0
         cfg.need_dw = 1 if dW is not None else 0
         with torch.cuda.device(X.device):
             st = L.lib().hgnn_net_backward_ex(
-                ctypes.byref(cfg), ctypes.byref(ctx.inp), None, L.ptr_array(ctx.params),
+                ctypes.byref(cfg), ctypes.byref(ctx.inp), None, L.ptr_array(params),
                 ctypes.c_void_p(ctx.ws.data_ptr()), ctypes.c_void_p(dout.data_ptr()), L.ptr_array(grads), L.ptr(dX),
                 L.ptr(dW), L.stream_handle(X.device), ctypes.c_void_p(_timer.handle) if _timer is not None else None,
                 evs, nev)
@@ -418,7 +412,8 @@ class _NetCsrFn(torch.autograd.Function):
                                          L.ptr_array(spec.running), ctypes.c_void_p(ws.data_ptr()),
                                          ctypes.c_void_p(out.data_ptr()), L.stream_handle(dev)),
                 "network forward (csr)")
-        ctx.cfg, ctx.ws, ctx.batch, ctx.params, ctx.spec = cfg, ws, batch, params, spec
+        ctx.cfg, ctx.ws, ctx.batch, ctx.spec = cfg, ws, batch, spec
+        ctx.save_for_backward(*params)  # weights: an in-place change before backward raises
         return out
 
     @staticmethod
@@ -426,13 +421,14 @@ class _NetCsrFn(torch.autograd.Function):
         cfg = ctx.cfg
         batch = ctx.batch
         dout = dout.contiguous().to(torch.float32)
-        grads, evs, nev = _grad_targets(ctx.spec, ctx.params)
+        params = ctx.saved_tensors
+        grads, evs, nev = _grad_targets(ctx.spec, params)
         dX = torch.empty(batch.nodes, batch.f_in, dtype=torch.float32, device=batch.device) \
             if ctx.needs_input_grad[2] else None
         cfg.need_dx = 1 if dX is not None else 0
         cfg.need_dw = 0
         with torch.cuda.device(batch.device):
-            st = L.lib().hgnn_net_backward_ex(ctypes.byref(cfg), None, ctypes.byref(batch.view), L.ptr_array(ctx.params),
+            st = L.lib().hgnn_net_backward_ex(ctypes.byref(cfg), None, ctypes.byref(batch.view), L.ptr_array(params),
                                               ctypes.c_void_p(ctx.ws.data_ptr()), ctypes.c_void_p(dout.data_ptr()),
                                               L.ptr_array(grads), L.ptr(dX), None, L.stream_handle(batch.device),
                                               None, evs, nev)

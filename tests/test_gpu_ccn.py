@@ -512,3 +512,21 @@ def test_ccn1_small_graph_path_ragged_edge_cases():
         _grad_close(gs[k], gg[k], f"ragged grad {k}")
     assert torch.equal(os_[1], net.fc.bias.detach().cpu())
     assert dxs[1].abs().max().item() == 0.0 and dxs[0, 1:].abs().max().item() == 0.0
+
+
+def test_ccn1_small_graph_path_inplace_input_change_raises():
+    """The small path's backward rebuilds every level from X, adj and the weights (ccn_small.hip), so
+    they are saved through autograd: changing X in place between forward and backward raises the
+    version error instead of returning gradients of a different input."""
+    import hgnn_amd.datagen as dg
+    from models.compnets.model_ccn import CCN_1D
+    (x, a, _), = dg.qm9_shape_dataset(1, seed=21)
+    net = CCN_1D(5, 1, 2, 2).cuda()
+    X = x.cuda().requires_grad_(True)
+    Xi = X * 1.0  # a non-leaf the caller may reuse as a staging buffer
+    out = net(Xi, (a + torch.eye(a.shape[0])).cuda())
+    assert net._spec().small(1, x.shape[0]) is not None
+    with torch.no_grad():
+        Xi.add_(1.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        out.sum().backward()

@@ -37,11 +37,11 @@ def _free_port():
     return p
 
 
-def _shards(world):
+def _shards(world, ng=NG):
     _paths()
     import hgnn_amd.datagen as dg
     from hgnn_amd.dp import graph_cost, shard_graphs
-    graphs = dg.qm9_shape_dataset(NG, seed=909)
+    graphs = dg.qm9_shape_dataset(ng, seed=909)
     return graphs, shard_graphs([graph_cost(X, A) for X, A, _ in graphs], world)
 
 
@@ -52,7 +52,7 @@ def _batch(graphs):
     return list(prepare_batch(data, 0, 1))
 
 
-def _worker(rank, world, port, q, mode="none"):
+def _worker(rank, world, port, q, mode="none", shape=(D, L, NG, 2)):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ.setdefault("HGNN_STRICT", "1")
@@ -63,14 +63,15 @@ def _worker(rank, world, port, q, mode="none"):
         import fixture_util as fu
         from hgnn_amd.dp import LayerBucketAllReduce, running_stats
         from models.gnns.model_mnb import GNN_lg
+        d, nl, ng, steps = shape
         torch.cuda.set_device(0)
-        graphs, shards = _shards(world)
+        graphs, shards = _shards(world, ng)
         b = [t.cuda() for t in _batch([graphs[i] for i in shards[rank]])]
         X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = b
-        model = GNN_lg(0, D, L, 5, 1, 1, ORDER).cuda()
+        model = GNN_lg(0, d, nl, 5, 1, 1, ORDER).cuda()
         fu.det_init(model, WSEED)
         dp = LayerBucketAllReduce(model)
-        for step in range(2):  # twice: the flat buffer and the events are reused across steps
+        for step in range(steps):  # twice: the flat buffer and the events are reused across steps
             if mode == "none":
                 model.zero_grad(set_to_none=True)
             elif mode == "zero":
@@ -90,23 +91,23 @@ def _worker(rank, world, port, q, mode="none"):
         dist.destroy_process_group()
 
 
-def _oracle_shard(graphs, idx):
+def _oracle_shard(graphs, idx, d=D, nl=L, steps=2):
     _paths()
     import fixture_util as fu
     from models.gnns.model_mnb import GNN_lg
     from oracle import ref_mnb as R
     X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _batch([graphs[i] for i in idx])
-    m = GNN_lg(0, D, L, 5, 1, 1, ORDER)
+    m = GNN_lg(0, d, nl, 5, 1, 1, ORDER)
     fu.det_init(m, WSEED)
     dt = torch.float64
     p = {k: v.detach().to(dt).requires_grad_(True) for k, v in m.state_dict().items()}
-    st = R.bn_states(L, 2 * D, dtype=dt)
+    st = R.bn_states(nl, 2 * d, dtype=dt)
     runs = []
-    for _ in range(2):  # the ranks ran two steps: running stats advanced twice
+    for _ in range(steps):  # the ranks ran `steps` steps: running stats advanced that often
         for v in p.values():
             v.grad = None
         out = R.gnn_lg(p, [X.to(dt), XL.to(dt), W.to(dt), WL.to(dt), Pm.to(dt), Pd.to(dt)], Nb, mask.to(dt), Eb,
-                       mask_lg.to(dt), L, ORDER, st, True, fast=True)
+                       mask_lg.to(dt), nl, ORDER, st, True, fast=True)
         torch.nn.MSELoss()(out, T.to(dt)).backward()
         runs.append({k: v.grad.clone() for k, v in p.items()})
     return runs[-1], st
@@ -149,5 +150,44 @@ def test_world2_bucketed_allreduce_matches_shard_average(mode):
                     np.testing.assert_allclose(res["running"][i], want, rtol=1e-4, atol=1e-5)
                     i += 1
     # both ranks hold identical averaged gradients
+    for k in ref:
+        assert np.array_equal(got[0]["grad." + k], got[1]["grad." + k]), k
+
+
+def test_world2_config4_rank_shape_d128():
+    """Config 4's per-rank shape: GNN_lg d=128, 5 layers, 512 graphs per rank (a global batch of
+    1024 split in two Σ(N+M)-balanced shards), one step with the overlapped per-layer buckets;
+    the averaged gradients and running statistics against the fp64 oracle's two-shard average."""
+    import multiprocessing as mp
+    d, nl, ng = 128, 5, 1024
+    ctx = mp.get_context("forkserver")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, "none", (d, nl, ng, 1))) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=300) for _ in range(2))
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    graphs, shards = _shards(2, ng)
+    assert sorted(shards[0] + shards[1]) == list(range(ng))
+    assert abs(len(shards[0]) - len(shards[1])) <= 16
+    (g0, s0), (g1, s1) = (_oracle_shard(graphs, shards[r], d, nl, 1) for r in (0, 1))
+    ref = {k: (g0[k] + g1[k]) / 2 for k in g0}
+    gmax = max(v.abs().max().item() for v in ref.values())
+    for r in (0, 1):
+        res = got[r]
+        assert res["flat_is_grad"]
+        for k, v in ref.items():
+            g = torch.from_numpy(res["grad." + k]).double()
+            assert torch.all((g - v).abs() <= 1e-4 * gmax + 1e-5 * v.abs()), (r, k)
+        i = 0
+        for l in range(nl - 1):
+            for nm in ("bn1", "bn2"):
+                for key in ("running_mean", "running_std"):
+                    want = ((s0[f"layer{l}.{nm}"][key] + s1[f"layer{l}.{nm}"][key]) / 2).numpy()
+                    np.testing.assert_allclose(res["running"][i], want, rtol=1e-4, atol=1e-5)
+                    i += 1
     for k in ref:
         assert np.array_equal(got[0]["grad." + k], got[1]["grad." + k]), k

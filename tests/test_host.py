@@ -223,24 +223,26 @@ def test_ccn_cpu_tensors_raise():
         net(torch.zeros(3, 5), torch.eye(3))
 
 
-def test_small_ccn_validation_word_tags():
-    """Host side of the small-graph CCN validation word (hgnn_amd.ccn._HostWord): a word whose tag is
-    above the last reported one raises once with its bits; older tags and clean calls do not."""
+def test_small_ccn_validation_word_reported_and_cleared():
+    """Host side of the small-graph CCN validation word (hgnn_amd.ccn._HostWord): a nonzero word raises
+    once with its bits and is cleared by the check; the same word stored again (a HIP-graph replay
+    keeps its captured tag) raises again; clean checks do not raise; per-device words are independent."""
     import ctypes
 
     import hgnn_amd.ccn as HC
-    from hgnn_amd.net import _word_bits
     w = HC._HostWord()
-    word = ctypes.c_int32(0)
-    w.words = {0: (word, None)}
+    word, word1 = ctypes.c_int32(0), ctypes.c_int32(0)
+    w.words = {0: (word, None), 1: (word1, None)}
     w.check(False)
     word.value = (5 << 8) | 0x20
     with pytest.raises(RuntimeError, match="not symmetric"):
         w.check(False)
-    w.check(False)                  # reported already
-    word.value = (3 << 8) | 0x8     # an older call's word
-    w.check(False)
-    word.value = (7 << 8) | 0x8
+    assert word.value == 0
+    w.check(False)                  # reported and cleared
+    word.value = (5 << 8) | 0x20    # a replay of the same captured call fails again
+    with pytest.raises(RuntimeError, match="not symmetric"):
+        w.check(False)
+    word1.value = (2 << 8) | 0x8    # the other device's word
     with pytest.raises(RuntimeError, match="self loop"):
         w.check(False)
-    assert _word_bits((9 << 8) | 4, 9) == 4 and _word_bits((9 << 8) | 4, 8) == 0 and _word_bits(6, None) == 6
+    w.check(False)
