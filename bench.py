@@ -290,18 +290,14 @@ def main():
             per = cur if per is None else {k: min(per[k], cur[k]) for k in per}
         dominant = max(per, key=lambda k: per[k][0])
 
-    # the dominant class, plus the two aggregation classes: the north_star's HBM-roofline target is
-    # on the aggregation (sparse operator x feature gathers) of the forward
-    hbm_classes = [RF.K_AGG_FWD, RF.K_AGG_BWD] + ([RF.K_FUSED_FWD] if RF.fused_net(args.d) else []) + \
-        ([RF.K_FUSED_BWD] if RF.fused_bwd(args.d) else [])
-    # the dominant class gets a timed region of its own: events recorded between the main stream's
-    # kernels change what the side stream's dW blocks share the CUs with (51 vs 43 us per dW launch
-    # measured with all classes timed together against the rocprofv3 trace of the same command)
-    timed = [k for k in hbm_classes if k != dominant] if dominant is not None else []
-    n_dom = per[dominant][1] // prof_steps if dominant is not None else 0
-    n_rest = sum(per[k][1] for k in timed) // prof_steps if dominant is not None else 0
-    timer = KernelTimer(max(1, n_dom * args.steps + 8), [dominant]) if dominant is not None else None
-    timer2 = KernelTimer(max(1, n_rest * args.steps + 8), timed) if timed else None
+    # the dominant class, plus the two aggregation classes (the north_star's HBM-roofline target is on
+    # the aggregation): each class gets a timed region of its own -- a HIP event recorded between two
+    # kernels of the main stream also times the next dispatch's start-up and changes what the side
+    # stream's blocks share the CUs with, so events around one class only keep its per-launch time
+    # comparable with the rocprofv3 trace of the same command
+    hbm_classes = [RF.K_AGG_FWD, RF.K_AGG_BWD]
+    timed = ([dominant] + [k for k in hbm_classes if k != dominant]) if dominant is not None else []
+    timers = {k: KernelTimer(max(1, per[k][1] // prof_steps * args.steps + 8), [k]) for k in timed}
     graph = None
     if args.graph:
         # The step (~90 kernel launches + Python autograd) is captured once and replayed; every
@@ -359,50 +355,40 @@ def main():
                 comm["allreduce_span_ms_max_rank"] = round(float(c[0]), 4)
                 comm["allreduce_exposed_ms_max_rank"] = round(float(c[1]), 4)
 
-    if timer is not None:
-        # The dominant kernel class is timed with HIP events around each of its launches over a
-        # second timed region of the same steps: event records between kernels cost ~10 us each
-        # (1.90 vs 1.72 ms per step measured on one box), so `value` comes from a region without
-        # them.  (Events captured into a HIP graph give no elapsed times either.)
+    # every timed class over its own region of args.steps eager steps, after the `value` region (event
+    # records cost ~10 us each: 1.90 vs 1.72 ms per step measured on one box; events captured into a
+    # HIP graph give no elapsed times either)
+    timer_ms = {}
+    for k in timed:
         torch.cuda.synchronize()
-        with timer:
+        with timers[k]:
             for _ in range(args.steps):
                 step()
         torch.cuda.synchronize()
-        if timer2 is not None:  # third region: the aggregation (HBM) classes
-            with timer2:
-                for _ in range(args.steps):
-                    step()
-            torch.cuda.synchronize()
+        timer_ms[k] = timers[k].elapsed(k)
+        timers[k].close()
     roof = None
     roof_hbm = None
-    roof_fused = None
-    if timer is not None:
-        ms, n = timer.elapsed(dominant)
-        timer.close()
-        timer_ms = {dominant: (ms, n)}
-        if timer2 is not None:
-            timer_ms.update({k: timer2.elapsed(k) for k in timed})
-            timer2.close()
+    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    traffic_note = ("committed profile (profiles/pmc_traffic.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of an earlier "
+                    "run of this step), not measured in this run")
+    if timed:
         counts = RF.batch_counts(W.detach(), WL, Pm, Pd, Nb, Eb)
-        roof = RF.roofline_entry(dominant, ms, n, counts, args.order, 5, args.d, args.layers, args.steps,
-                                 pmc_path=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-        roof["timed_in"] = (f"second timed region: {args.steps} eager steps with HIP events around this "
-                            "class's launches only (the aggregation classes in a third region)")
+        ms, n = timer_ms[dominant]
+        roof = RF.roofline_entry(dominant, ms, n, counts, args.order, 5, args.d, args.layers, args.steps, pmc_path=pmc)
+        roof["traffic_source"] = traffic_note
+        roof["timed_in"] = (f"a region of its own: {args.steps} eager steps with HIP events around this class's "
+                            "launches only (each aggregation class in another such region)")
         roof["class_ms_per_step_profile"] = {RF.NAMES[k]: round(v[0] / prof_steps, 4) for k, v in per.items()}
         roof_hbm = {}
-        roof_fused = {}
         for k in hbm_classes:
             kms, kn = timer_ms[k]
-            e = RF.roofline_entry(k, kms, kn, counts, args.order, 5, args.d, args.layers, args.steps,
-                                  pmc_path=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-            ent = {x: e[x] for x in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                                     "algorithmic_bytes_per_launch", "launches_per_step", "avg_launch_us",
-                                     "requested_bytes_per_launch", "requested_gbs", "requested_frac") if x in e}
-            if e["bound"] == "hbm":
-                roof_hbm[RF.NAMES[k]] = ent
-            else:
-                roof_fused[RF.NAMES[k]] = ent
+            e = RF.roofline_entry(k, kms, kn, counts, args.order, 5, args.d, args.layers, args.steps, pmc_path=pmc)
+            roof_hbm[RF.NAMES[k]] = {x: e[x] for x in (
+                "bound", "achieved", "peak", "unit", "frac", "traffic", "algorithmic_bytes_per_launch",
+                "launches_per_step", "avg_launch_us", "requested_bytes_per_launch", "requested_gbs",
+                "requested_frac") if x in e}
+            roof_hbm[RF.NAMES[k]]["traffic_source"] = traffic_note
 
     # forward-only line (config "cfg2f"): the north star's HBM target is stated on the batched
     # LG-GNN forward.  Train-mode BN (batch statistics), no autograd graph kept.
@@ -421,12 +407,11 @@ def main():
             fwd()
         torch.cuda.synchronize()
         fms = (time.perf_counter() - t0) * 1e3 / args.steps
-        with KT(4096, [RF.K_AGG_FWD, RF.K_FUSED_FWD]) as tf:
+        with KT(4096, [RF.K_AGG_FWD]) as tf:
             for _ in range(args.steps):
                 fwd()
             torch.cuda.synchronize()
             ams, an = tf.elapsed(RF.K_AGG_FWD)
-            fms_f, fn_f = tf.elapsed(RF.K_FUSED_FWD)
         tf.close()
         counts_f = RF.batch_counts(W.detach(), WL, Pm, Pd, Nb, Eb)
         ffl, fby = RF.forward_work(counts_f, args.order, 5, args.d, args.layers)
@@ -440,9 +425,6 @@ def main():
                     "frac_hbm": round(fby / fms / 1e6 / RF.PEAK_HBM_GBS, 4),
                     "agg_fwd": {x: agg[x] for x in ("achieved", "unit", "frac", "launches_per_step", "avg_launch_us",
                                                     "requested_gbs", "requested_frac")}}
-        if fn_f:
-            fe = RF.roofline_entry(RF.K_FUSED_FWD, fms_f, fn_f, counts_f, args.order, 5, args.d, args.layers, args.steps)
-            roof_fwd["fused_fwd"] = {x: fe[x] for x in ("achieved", "unit", "frac", "launches_per_step", "avg_launch_us")}
 
     value = args.bs * world * args.steps / elapsed
     res = {
@@ -472,7 +454,6 @@ def main():
         "comm": comm,
         "roofline": roof,
         "roofline_hbm": roof_hbm,
-        "roofline_fused": roof_fused,
         "roofline_fwd": roof_fwd,
         "cpu_baseline": None,
         "parity": None,

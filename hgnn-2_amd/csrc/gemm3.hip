@@ -57,7 +57,7 @@ __device__ unsigned g_clock_n;
 
 namespace {
 
-enum { E3_FWD = 0, E3_STORE = 1, E3_DA_BN = 2 };
+enum { E3_FWD = 0, E3_STORE = 1 };
 
 struct G3 {
     const float* a;
@@ -73,18 +73,6 @@ struct G3 {
     const float* bias;
     int relu_from;
     float* bn_part;  // [ceil(m_cap / 64)][n][3] (count, mean, M2)
-    // E3_DA_BN: A = dY computed on load from (y, dz) and the BN statistics (a = y, lda = k)
-    const float* dz;
-    const float* mean;
-    const float* stdv;
-    const float* bn_w;
-    const float* sums;  // [k][4] from k_bn_bwd_fin
-    int bn_relu_from;
-    int training;
-    float* dy_out;      // [rows][k], written by the blockIdx.y == 0 column of tiles
-    float* dbpart;      // [tiles][k] column sums of dY
-    float* dw_s;        // BN scalar grads
-    float* db_s;
     int xcd;            // E3_FWD: the column tiles of a row tile on one XCD (gridDim.x % 8 == 0)
 };
 
@@ -111,7 +99,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
     }
     const int m0 = bx * BM, n0 = by * BN;
     const int Mv = p.m_valid ? *p.m_valid : p.m_cap;
-    if (m0 >= Mv && !(EPI == E3_DA_BN && blockIdx.x == 0 && blockIdx.y == 0)) return;
+    if (m0 >= Mv) return;
     const int K = p.k, N = p.n;
 
     // K % 4 == 0 (host-checked): a float4 is wholly inside or outside the k range, so the
@@ -120,60 +108,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
     // staging doubled the k-loop's instruction count (321 vs 204 per k-step) and cost ~5 us
     // per launch (round-1 GEMM lab).
     float4 ra[AF4], rb[BF4];
-    float4 rz[EPI == E3_DA_BN ? AF4 : 1];
-    // E3_DA_BN: per-channel affine form of the BN backward, dY = ca dz + cb (y - mu) + ce
-    // (train: ca = w / sd, cb = -m2 / sd^2, ce = -m1 / sd; eval: ca = w / sd), in LDS
-    constexpr int KB = EPI == E3_DA_BN ? 512 : 1;
-    __shared__ float colsum[KB], cA[KB], cB[KB], cE[KB], cMu[KB];
-    if constexpr (EPI == E3_DA_BN) {
-        const float inv_n = Mv > 0 ? 1.0f / (float)Mv : 0.f;
-        const float wv = *p.bn_w;
-        for (int ch = tid; ch < K; ch += NT) {
-            const float sd = p.stdv[ch];
-            colsum[ch] = 0.f;
-            cA[ch] = wv / sd;
-            cMu[ch] = p.mean[ch];
-            if (p.training) {
-                const float m1 = p.sums[ch * 4 + 0] * inv_n, m2 = p.sums[ch * 4 + 1] * inv_n;
-                cB[ch] = -m2 / (sd * sd);
-                cE[ch] = -m1 / sd;
-            } else {
-                cB[ch] = 0.f;
-                cE[ch] = 0.f;
-            }
-        }
-        if (blockIdx.x == 0 && blockIdx.y == 0 && (tid >> 6) == 0) {
-            // BN scalar grads: dw = sum_c sum_r dz h, db = sum_c sum_r dz (k_bn_bwd_apply formerly)
-            double t1 = 0.0, t2 = 0.0;
-            for (int ch = lane; ch < K; ch += 64) {
-                t1 += (double)p.sums[ch * 4 + 2];
-                t2 += (double)p.sums[ch * 4 + 3];
-            }
-            t1 = wave_sum_d(t1);
-            t2 = wave_sum_d(t2);
-            if (lane == 0) {
-                *p.dw_s = (float)t1;
-                *p.db_s = (float)t2;
-            }
-        }
-        if (m0 >= Mv) return;  // block (0, 0) of an empty batch: scalar grads only
-        __syncthreads();        // constants ready before the first staging
-    }
-    // dY for the staged float4 at (row gm, channels gk..gk+3); zero outside the matrix
-    auto bn_dy = [&](float4 yv, float4 dzv, int gm, int gk) {
-        const float yy[4] = {yv.x, yv.y, yv.z, yv.w}, zz[4] = {dzv.x, dzv.y, dzv.z, dzv.w};
-        float d[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int ch = gk + q;
-            d[q] = 0.f;
-            if (gm < Mv && ch < K) {
-                d[q] = fmaf(cA[ch], zz[q], fmaf(cB[ch], yy[q] - cMu[ch], cE[ch]));
-                if (ch >= p.bn_relu_from && !(yy[q] > 0.f)) d[q] = 0.f;
-            }
-        }
-        return make_float4(d[0], d[1], d[2], d[3]);
-    };
     // Loads are unconditional buffer loads: an out-of-range float4 gets an out-of-bounds offset
     // and reads 0 in hardware.  A conditional load made the compiler merge the loaded and the
     // zero value with register moves straight after the load, i.e. a vmcnt(0) in the middle of
@@ -183,8 +117,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
     constexpr unsigned OOB = 0x7ffffff0u;
     const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.a), 0, Mv * p.lda * 4, 0x00020000);
     const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.b), 0, N * p.ldb * 4, 0x00020000);
-    const auto rs_z = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(EPI == E3_DA_BN ? p.dz : p.a), 0,
-                                                        Mv * p.lda * 4, 0x00020000);
     auto ld4 = [](__amdgpu_buffer_rsrc_t r, unsigned off) {
         return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
     };
@@ -195,7 +127,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
             const int gm = m0 + row, gk = k0 + kq;
             const unsigned off = (gm < Mv && gk < K) ? (unsigned)(gm * p.lda + gk) * 4u : OOB;
             ra[i] = ld4(rs_a, off);
-            if constexpr (EPI == E3_DA_BN) rz[i] = ld4(rs_z, off);
         }
 #pragma unroll
         for (int i = 0; i < BF4; ++i) {
@@ -210,31 +141,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
 #pragma unroll
         for (int i = 0; i < AF4; ++i) {
             const int e = tid + i * NT, row = e / (BK / 4), kq = (e % (BK / 4)) * 4;
-            if constexpr (EPI == E3_DA_BN) {
-                const int gm = m0 + row, gk = k0 + kq;
-                const float4 d = bn_dy(ra[i], rz[i], gm, gk);
-                *reinterpret_cast<float4*>(&As[buf][row * LDK + kq]) = d;
-                if (blockIdx.y == 0) {
-                    if (gm < Mv && gk < K) *reinterpret_cast<float4*>(p.dy_out + (long long)gm * p.lda + gk) = d;
-                    // column sums: lanes with equal lane % (BK / 4) hold the same 4 columns
-                    float4 cs = d;
-#pragma unroll
-                    for (int off = BK / 4; off < 64; off <<= 1) {
-                        cs.x += __shfl_xor(cs.x, off, 64);
-                        cs.y += __shfl_xor(cs.y, off, 64);
-                        cs.z += __shfl_xor(cs.z, off, 64);
-                        cs.w += __shfl_xor(cs.w, off, 64);
-                    }
-                    if (lane < BK / 4 && gk < K) {
-                        atomicAdd(&colsum[gk], cs.x);
-                        atomicAdd(&colsum[gk + 1], cs.y);
-                        atomicAdd(&colsum[gk + 2], cs.z);
-                        atomicAdd(&colsum[gk + 3], cs.w);
-                    }
-                }
-            } else {
-                *reinterpret_cast<float4*>(&As[buf][row * LDK + kq]) = ra[i];
-            }
+            *reinterpret_cast<float4*>(&As[buf][row * LDK + kq]) = ra[i];
         }
 #pragma unroll
         for (int i = 0; i < BF4; ++i) {
@@ -395,10 +302,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3(G3 p) {
                     if (gm < Mv && gn < N) p.c[(long long)gm * p.ldc + gn] = acc[i][j][r];
                 }
             }
-        if constexpr (EPI == E3_DA_BN) {
-            if (blockIdx.y == 0)  // colsum complete: the main loop ended with a barrier
-                for (int i = tid; i < K; i += NT) p.dbpart[(long long)blockIdx.x * K + i] = colsum[i];
-        }
     }
 }
 
@@ -790,39 +693,6 @@ int dw3_chunks(int r_cap, int o, int k) {
 size_t dw3_slab_floats(int r_cap, int o, int k) { return (size_t)dw3_chunks(r_cap, o, k) * o * k; }
 
 // slabs[z][o][k] = sum_{r in chunk z} dY[r, o] A[r, k]
-int launch_gemm3_da_bn(const BnBwdArgs& bn, const int* m_valid, int m_cap, int o, const float* wt, int ldw, int kout,
-                       float* da, int ldda, hipStream_t s) {
-    if (m_cap <= 0) return 0;
-    if (o > 512 || o % 4 != 0 || bn.c != o) return HGNN_ERR_UNSUPPORTED;
-    if ((long long)m_cap * o * 4 >= (1ll << 31) || (long long)kout * ldw * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
-    G3 p{};
-    p.a = bn.y;
-    p.lda = o;
-    p.b = wt;
-    p.ldb = ldw;
-    p.m_cap = m_cap;
-    p.m_valid = m_valid;
-    p.k = o;
-    p.n = kout;
-    p.c = da;
-    p.ldc = ldda;
-    p.dz = bn.dz;
-    p.mean = bn.mean;
-    p.stdv = bn.std;
-    p.bn_w = bn.w;
-    p.sums = bn.sums;
-    p.bn_relu_from = bn.relu_from;
-    p.training = bn.training;
-    p.dy_out = bn.dy;
-    p.dbpart = bn.dbpart;
-    p.dw_s = bn.dw;
-    p.db_s = bn.db;
-    hipLaunchKernelGGL((k_gemm3<64, 128, 32, 2, 2, E3_DA_BN>), dim3(ceil_div(m_cap, 64), ceil_div(kout, 128)),
-                       dim3(256), 0, s, p);
-    HGNN_LAUNCH_CHECK();
-    return 0;
-}
-
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
                     int nz, float* slabs, hipStream_t s) {
     if (r_cap <= 0) return 0;
@@ -910,19 +780,12 @@ int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, in
     if (m_cap <= 0) return 0;
     if (o % 4 != 0) return HGNN_ERR_UNSUPPORTED;
     if ((long long)m_cap * lddy * 4 >= (1ll << 31) || (long long)kout * ldw * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
-    static const bool dma = [] {
-        const char* e = getenv("HGNN_GEMM_DMA");
-        return !(e && e[0] == '0');
-    }();
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    if (dma && lddy % 4 == 0 && ldw % 4 == 0 && al(dy) && al(wt)) {
-        static const bool xcd = [] {
-            const char* e = getenv("HGNN_DA_XCD");
-            return !e || e[0] != '0';
-        }();
-        const int gx = xcd ? ceil_div(ceil_div(m_cap, 64), 8) * 8 : ceil_div(m_cap, 64);
+    if (lddy % 4 == 0 && ldw % 4 == 0 && al(dy) && al(wt)) {
+        // the column tiles of a row tile on one XCD (k_gemm3's E3_FWD order)
+        const int gx = ceil_div(ceil_div(m_cap, 64), 8) * 8;
         hipLaunchKernelGGL((k_gemm5<64, 64, 2, 2>), dim3(gx, ceil_div(kout, 64)), dim3(256), 0, s,
-                           dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda, xcd ? 1 : 0);
+                           dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda, 1);
         HGNN_LAUNCH_CHECK();
         return 0;
     }

@@ -15,9 +15,9 @@ PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_FP32_MFMA_TFS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak
 
 (K_STRUCT, K_AGG_FWD, K_GEMM_FWD, K_BN_FWD, K_READOUT, K_BN_BWD, K_GEMM_DW, K_GEMM_DA, K_AGG_BWD, K_DW_DENSE,
- K_DW_REDUCE, K_FUSED_FWD, K_FUSED_BWD) = range(13)
+ K_DW_REDUCE) = range(11)
 NAMES = ["struct", "agg_fwd", "gemm_fwd", "bn_fwd", "readout", "bn_bwd", "gemm_dw", "gemm_da", "agg_bwd", "dw_dense",
-         "dw_reduce", "fused_fwd", "fused_bwd"]
+         "dw_reduce"]
 N_CLASSES = len(NAMES)
 
 
@@ -46,74 +46,48 @@ def lg_halves(order, f_in, d, n_layers, jt):
     return out, k_last
 
 
-def fused_net(d):
-    """Mirror of net.hip build_program's P.fused (fused aggregation + GEMM kernels in use)."""
-    import os
-    return (2 * d) % 16 == 0 and 2 * d <= 256 and os.environ.get("HGNN_FUSED", "0") not in ("", "0")
-
-
-def fused_bwd(d):
-    import os
-    return fused_net(d) and os.environ.get("HGNN_FUSED_BWD", "0") not in ("", "0")
-
-
-def fused_half(d, cg, cp):
-    return fused_net(d) and cg % 16 == 0 and cp % 16 == 0
-
-
 def class_work(kcls, counts, order, f_in, d, n_layers, jt=3):
     """(flops, bytes) of one training step for kernel class kcls (sum over its launches)."""
-    all_halves, k_last = lg_halves(order, f_in, d, n_layers, jt)
-    fnet = fused_bwd(d)
-    # forward: the fused halves run K_FUSED_FWD, the others the aggregation + GEMM pair;
-    # backward: with the fused kernels every half's dX is K_FUSED_BWD (no dA GEMM / gather)
-    halves = [h for h in all_halves if not fused_half(d, h[2], h[3])]
-    fhalves = [h for h in all_halves if fused_half(d, h[2], h[3])]
+    halves, k_last = lg_halves(order, f_in, d, n_layers, jt)
     c2 = 2 * d
     rows = lambda edge: counts["edges"] if edge else counts["nodes"]  # noqa: E731
     nnz_g = lambda edge: counts["nnz_wl"] if edge else counts["nnz_w"]  # noqa: E731
     fl = by = 0.0
-    if kcls == K_FUSED_FWD:
-        for edge, k, cg, cp in fhalves:
-            r, ro = rows(edge), rows(not edge)
-            fl += 2.0 * r * k * c2 + 2.0 * (nnz_g(edge) * jt * cg + 2 * counts["nnz_p"] * cp)
-            s_bytes = 8.0 * (r + r) + 16.0 * (nnz_g(edge) + counts["nnz_p"])
-            by += 4.0 * (r * cg + ro * cp + r * c2 + r * k + c2 * (k + 1)) + s_bytes
-    elif kcls == K_FUSED_BWD and fnet:
-        for edge, k, cg, cp in all_halves:
-            r, ro = rows(edge), rows(not edge)
-            fl += 2.0 * r * jt * c2 * cg + 2.0 * ro * 2 * c2 * cp
-            s_bytes = 8.0 * (r + ro) + 16.0 * (nnz_g(edge) + counts["nnz_p"])
-            by += 4.0 * (r * c2 + 2 * (r * cg + ro * cp) + c2 * k) + s_bytes
-    elif kcls == K_GEMM_FWD:
+    if kcls == K_GEMM_FWD:
         for edge, k, cg, cp in halves:
             r = rows(edge)
             fl += 2.0 * r * k * c2
             by += 4.0 * (r * k + r * c2 + c2 * (k + 1))
-    elif kcls == K_GEMM_DA and not fnet:
-        for edge, k, cg, cp in all_halves:
+    elif kcls == K_GEMM_DA:
+        for edge, k, cg, cp in halves:
             r = rows(edge)
             fl += 2.0 * r * c2 * k
             by += 4.0 * (r * c2 + r * k + c2 * k)
     elif kcls == K_GEMM_DW:
-        for edge, k, cg, cp in all_halves:
+        for edge, k, cg, cp in halves:
             r = rows(edge)
             fl += 2.0 * r * c2 * k
             by += 4.0 * (r * c2 + r * k + c2 * k)
     elif kcls in (K_AGG_FWD, K_AGG_BWD):
-        items = halves if kcls == K_AGG_FWD else ([] if fnet else all_halves)
-        items = [(e, k, cg, cp) for e, k, cg, cp in items] + [(False, k_last, c2, c2)]
+        items = [(e, k, cg, cp) for e, k, cg, cp in halves] + [(False, k_last, c2, c2)]
         for edge, k, cg, cp in items:
             r, ro = rows(edge), rows(not edge)
             s_bytes = 8.0 * (r + r) + 16.0 * (nnz_g(edge) + counts["nnz_p"])
             by += 4.0 * (r * k + r * cg + ro * cp) + s_bytes
             fl += 2.0 * (nnz_g(edge) * jt * cg + 2 * counts["nnz_p"] * cp)
+        if kcls == K_AGG_BWD:
+            # the gather that finalises a layer output's gradient applies its BN backward: reads the
+            # pre-BN row, writes dY
+            for edge, k, cg, cp in halves:
+                by += 4.0 * 2 * rows(edge) * c2
     elif kcls == K_BN_FWD:
-        for edge, k, cg, cp in all_halves:
+        for edge, k, cg, cp in halves:
             by += 4.0 * 2 * rows(edge) * c2
     elif kcls == K_BN_BWD:
-        for edge, k, cg, cp in all_halves:
-            by += 4.0 * 5 * rows(edge) * c2
+        # side pass: dz, y, dY read once (conv bias and BN scalar grads); the statistics come from
+        # the dA GEMMs' epilogues
+        for edge, k, cg, cp in halves:
+            by += 4.0 * 3 * rows(edge) * c2
     return fl, by
 
 
@@ -123,8 +97,7 @@ def agg_requested_bytes(kcls, counts, order, f_in, d, n_layers, jt=3):
     backward: one row slice per nonzero coefficient -- the diagonal entry's I and D slices, one
     A slice per other entry), every output row written once, the row lists read once.  The
     gap to class_work's compulsory bytes is what the L2 / MALL serve."""
-    all_halves, k_last = lg_halves(order, f_in, d, n_layers, jt)
-    halves = [h for h in all_halves if not fused_half(d, h[2], h[3])]
+    halves, k_last = lg_halves(order, f_in, d, n_layers, jt)
     c2 = 2 * d
     rows = lambda edge: counts["edges"] if edge else counts["nodes"]  # noqa: E731
     nnz_g = lambda edge: counts["nnz_wl"] if edge else counts["nnz_w"]  # noqa: E731
@@ -134,8 +107,8 @@ def agg_requested_bytes(kcls, counts, order, f_in, d, n_layers, jt=3):
             r = rows(edge)
             by += 4.0 * (nnz_g(edge) * cg + counts["nnz_p"] * cp + r * k) + 8.0 * 2 * r + 16.0 * (
                 nnz_g(edge) + counts["nnz_p"])
-    elif kcls == K_AGG_BWD and not fused_bwd(d):
-        for edge, k, cg, cp in all_halves + [(False, k_last, c2, c2)]:
+    elif kcls == K_AGG_BWD:
+        for edge, k, cg, cp in halves + [(False, k_last, c2, c2)]:
             r, ro = rows(edge), rows(not edge)
             by += 4.0 * ((nnz_g(edge) + r) * cg + 2 * counts["nnz_p"] * cp + r * cg + ro * cp) + 8.0 * (r + ro) + 16.0 * (
                 nnz_g(edge) + counts["nnz_p"])
@@ -160,7 +133,7 @@ def forward_work(counts, order, f_in, d, n_layers, jt=3):
     by += n_layers * S
     params = sum(c2 * (k + 1) for _, k, _, _ in halves) + k_last + 1
     by += 4.0 * params
-    fl = sum(class_work(k, counts, order, f_in, d, n_layers, jt)[0] for k in (K_GEMM_FWD, K_AGG_FWD, K_FUSED_FWD))
+    fl = sum(class_work(k, counts, order, f_in, d, n_layers, jt)[0] for k in (K_GEMM_FWD, K_AGG_FWD))
     fl += 2.0 * N * k_last
     return fl, by
 
@@ -172,14 +145,12 @@ CLASS_KERNELS = {
     K_GEMM_FWD: ("k_gemm3<", "k_gemm_fwd"),
     K_BN_FWD: ("k_bn_finalize", "k_bn_apply"),
     K_READOUT: ("k_readout",),
-    K_BN_BWD: ("k_bn_bwd",),
+    K_BN_BWD: ("k_bn_bwd", "k_bn_stat_fin", "k_bn_apply_bwd"),
     K_GEMM_DW: ("k_gemm3_tn", "k_gemm_dw"),
     K_GEMM_DA: ("k_gemm3<", "k_gemm_da"),
     K_AGG_BWD: ("k_agg_bwd",),
     K_DW_DENSE: ("k_dw_dense",),
     K_DW_REDUCE: ("k_dw_reduce",),
-    K_FUSED_FWD: ("k_fused<",),
-    K_FUSED_BWD: ("k_fused<",),
 }
 
 
@@ -189,9 +160,6 @@ def _in_class(kcls, name):
     if "k_gemm3<" in name:  # k_gemm3<BM, BN, BK, WGM, WGN, EPI>: EPI 0 = forward, 1 = dA
         epi = name.split(">")[0].rsplit(",", 1)[-1].strip()
         return (kcls == K_GEMM_FWD) == (epi == "0")
-    if "k_fused<" in name:  # k_fused<BN, NSM, EPI>: EPI 0 = forward, 1 = dX
-        epi = name.split(">")[0].rsplit(",", 1)[-1].strip()
-        return (kcls == K_FUSED_FWD) == (epi == "0")
     return True
 
 
@@ -216,7 +184,7 @@ def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, s
     """bench.py 'roofline' object for a kernel class measured over `steps` steps."""
     fl, by = class_work(kcls, counts, order, f_in, d, n_layers, jt)
     sec = max(ms_total / 1e3, 1e-12)
-    if kcls in (K_GEMM_FWD, K_GEMM_DA, K_GEMM_DW, K_FUSED_FWD, K_FUSED_BWD):
+    if kcls in (K_GEMM_FWD, K_GEMM_DA, K_GEMM_DW):
         achieved = fl * steps / sec / 1e12
         peak, unit, bound = PEAK_FP32_MFMA_TFS, "TFLOP/s", "mfma"
     else:

@@ -171,8 +171,6 @@ int hgnn_net_backward_ex(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
 #define HGNN_K_AGG_BWD 8
 #define HGNN_K_DW_DENSE 9  /* dense operator gradient dW (W.requires_grad) */
 #define HGNN_K_DW_REDUCE 10 /* dW slab + bias reductions                    */
-#define HGNN_K_FUSED_FWD 11 /* aggregation gathered into LDS + Conv1d pair GEMM (fused) */
-#define HGNN_K_FUSED_BWD 12 /* dX = (operator^T gather of dY) . Wcat, fused        */
 void* hgnn_timer_create(int max_launches, unsigned class_mask);
 void hgnn_timer_reset(void* timer);
 /* Waits for the recorded events; sums the durations of class `kernel_class`. */

@@ -80,13 +80,8 @@ def _check(model, b, L, order, kind="lg", dx_relax=False, factor=2.0):
     return o, gr
 
 
-@pytest.mark.parametrize("fused,fused_bwd", [("1", "0"), ("1", "1"), ("0", "0")])
-def test_config2_full_batch_512_vs_oracle(monkeypatch, fused, fused_bwd):
-    """The headline workload itself: 512 QM9-shape graphs, GNN_lg(0, 64, 5, 5, 1, 1, 2); with the
-    unfused kernels (default), the fused aggregation+GEMM forward (HGNN_FUSED=1) and in addition
-    the fused backward dX (HGNN_FUSED_BWD=1)."""
-    monkeypatch.setenv("HGNN_FUSED", fused)
-    monkeypatch.setenv("HGNN_FUSED_BWD", fused_bwd)
+def test_config2_full_batch_512_vs_oracle():
+    """The headline workload itself: 512 QM9-shape graphs, GNN_lg(0, 64, 5, 5, 1, 1, 2)."""
     import hgnn_amd.datagen as dg
     from models.gnns.model_mnb import GNN_lg
     b = _batch(dg.qm9_shape_dataset(512, seed=1000))
