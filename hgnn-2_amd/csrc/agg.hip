@@ -356,49 +356,14 @@ __device__ __forceinline__ void agg_bwd_g_chunk(const AggBwdArgs& a, float4 me, 
     }
 }
 
-// The gather that finalises a layer output's gradient (st.y) also sums, per channel, (dz, dz h) with
-// h = (y - mean) / std over its rows: the AGG_ST_ROWS rows of a block (each wave AGG_ST_ROWS / AGG_WV of
-// them, interleaved) in registers, then over the block's waves in a fixed order through LDS -- part[block][c].
-template <int C, bool V>
-__device__ __forceinline__ void row_stats(const AggBwdArgs& a, int r, int lane, const float (&acc)[C],
-                                          float2 (&sv)[C]) {
-    float yv[C];
-    load_row<C, V>(a.st.y + (long long)r * a.c, a.c, lane, yv);
-#pragma unroll
-    for (int i = 0; i < C; ++i) {
-        const int c = lane * C + i;
-        if (c < a.c) {
-            const float h = (yv[i] - a.st.mean[c]) * (1.0f / a.st.std[c]);
-            sv[i].x += acc[i];
-            sv[i].y = fmaf(acc[i], h, sv[i].y);
-        }
-    }
-}
-
-template <int C>
-__device__ __forceinline__ void block_stats(const AggBwdArgs& a, int blk, int lane, int wv, const float2 (&sv)[C]) {
-    __shared__ float2 red[AGG_WV][64 * C];
-#pragma unroll
-    for (int i = 0; i < C; ++i) red[wv][lane * C + i] = sv[i];
-    __syncthreads();
-    for (int t = threadIdx.x; t < a.c; t += AGG_NT) {
-        float2 q = red[0][t];
-#pragma unroll
-        for (int w = 1; w < AGG_WV; ++w) {
-            q.x += red[w][t].x;
-            q.y += red[w][t].y;
-        }
-        a.st.part[(long long)blk * a.c + t] = q;
-    }
-}
-
 // Long rows (the transposed line-graph lists hold rows of up to ~35 entries: 8 % of the rows,
 // 59 % of the entries at config 2) take 8 entries per round trip instead of 4 (serial trace:
 // 127.9 -> 122.6 us per step).
 constexpr int AGG_LONG = 8;
 
 template <int JT, int C, bool V>
-__device__ __forceinline__ void agg_bwd_g(const AggBwdArgs& a, int r, int lane, float (&acc)[C]) {
+__device__ __forceinline__ void agg_bwd_g(const AggBwdArgs& a, int r, int lane) {
+    float acc[C];
     float* o = a.out + (long long)r * a.ldo;
     if (a.accumulate) {
         load_row<C, V>(o, a.c, lane, acc);
@@ -425,7 +390,8 @@ __device__ __forceinline__ void agg_bwd_g(const AggBwdArgs& a, int r, int lane, 
 }
 
 template <int C, bool V>
-__device__ __forceinline__ void agg_bwd_p(const AggBwdArgs& a, int r, int lane, float (&acc)[C]) {
+__device__ __forceinline__ void agg_bwd_p(const AggBwdArgs& a, int r, int lane) {
+    float acc[C];
     float* o = a.out + (long long)r * a.ldo;
     if (a.accumulate) {
         load_row<C, V>(o, a.c, lane, acc);
@@ -459,48 +425,25 @@ __device__ __forceinline__ void agg_bwd_p(const AggBwdArgs& a, int r, int lane, 
     store_row<C, V>(o, a.c, lane, acc);
 }
 
-// MODE 1: G only (ga); 2: P only (pa); 3: blocks [0, gb) G on ga, the rest P on pa.  A block is AGG_WV waves
-// of one row each, or, in a part that emits BN statistics (st.y), AGG_ST_ROWS rows (ST: such a part exists).
-template <int JT, int C, bool V, bool G>
-__device__ __forceinline__ void bwd_part(const AggBwdArgs& a, int blk, int lane, int wv) {
-    const int total = *a.total_rows;
-    float acc[C];
-    if (!a.st.y) {
-        const int r = __builtin_amdgcn_readfirstlane(blk * AGG_WV + wv);
-        if (r >= total) return;
-        if constexpr (G) agg_bwd_g<JT, C, V>(a, r, lane, acc);
-        else agg_bwd_p<C, V>(a, r, lane, acc);
-        return;
-    }
-    const int r0 = blk * AGG_ST_ROWS;
-    if (r0 >= total) return;  // block-uniform
-    float2 sv[C];
-#pragma unroll
-    for (int i = 0; i < C; ++i) sv[i] = make_float2(0.f, 0.f);
-    for (int q = 0; q < AGG_ST_ROWS / AGG_WV; ++q) {
-        const int r = __builtin_amdgcn_readfirstlane(r0 + q * AGG_WV + wv);
-        if (r < total) {
-            if constexpr (G) agg_bwd_g<JT, C, V>(a, r, lane, acc);
-            else agg_bwd_p<C, V>(a, r, lane, acc);
-            row_stats<C, V>(a, r, lane, acc, sv);
-        }
-    }
-    block_stats<C>(a, blk, lane, wv, sv);
-}
-
+// MODE 1: G only (ga); 2: P only (pa); 3: blocks [0, gb) G on ga, the rest P on pa.
 template <int JT, int CG, int CP, bool V, int MODE>
 __global__ void __launch_bounds__(AGG_NT) k_agg_bwd(AggBwdArgs ga, AggBwdArgs pa, int gb) {
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     if (MODE == 1 || (MODE == 3 && (int)blockIdx.x < gb)) {
-        if constexpr (MODE != 2) bwd_part<JT, CG, V, true>(ga, blockIdx.x, lane, wv);
+        if constexpr (MODE != 2) {
+            const int r = __builtin_amdgcn_readfirstlane((int)blockIdx.x * AGG_WV + wv);
+            if (r >= *ga.total_rows) return;
+            agg_bwd_g<JT, CG, V>(ga, r, lane);
+        }
     } else {
-        if constexpr (MODE != 1) bwd_part<JT, CP, V, false>(pa, (int)blockIdx.x - (MODE == 3 ? gb : 0), lane, wv);
+        if constexpr (MODE != 1) {
+            const int r = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - (MODE == 3 ? gb : 0)) * AGG_WV + wv);
+            if (r >= *pa.total_rows) return;
+            agg_bwd_p<CP, V>(pa, r, lane);
+        }
     }
 }
-
-// blocks of a part: AGG_WV rows each, AGG_ST_ROWS with statistics
-static int part_blocks(const AggBwdArgs& a) { return ceil_div(a.cap_rows, a.st.y ? AGG_ST_ROWS : AGG_WV); }
 
 static bool bwd_vec_g(int cpl, const AggBwdArgs& a) {
     return vec_ok(cpl, a.c, a.ing, {a.ldg, a.gofs}) && vec_ok(cpl, a.c, a.out, {a.ldo});
@@ -511,7 +454,7 @@ static bool bwd_vec_p(int cpl, const AggBwdArgs& a) {
 
 template <int JT, int C>
 static int agg_bwd_single(const AggBwdArgs& a, hipStream_t s) {
-    const dim3 g(part_blocks(a));
+    const dim3 g(ceil_div(a.cap_rows, AGG_WV));
     if (a.ing) {
         if (bwd_vec_g(C, a)) hipLaunchKernelGGL((k_agg_bwd<JT, C, C, true, 1>), g, dim3(AGG_NT), 0, s, a, a, 0);
         else hipLaunchKernelGGL((k_agg_bwd<JT, C, C, false, 1>), g, dim3(AGG_NT), 0, s, a, a, 0);
@@ -549,7 +492,7 @@ int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s) {
 
 template <int JT, int C>
 static int agg_bwd_pair_c(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t s) {
-    const int gb = part_blocks(ga), pb = part_blocks(pa);
+    const int gb = ceil_div(ga.cap_rows, AGG_WV), pb = ceil_div(pa.cap_rows, AGG_WV);
     hipLaunchKernelGGL((k_agg_bwd<JT, C, C, true, 3>), dim3(gb + pb), dim3(AGG_NT), 0, s, ga, pa, gb);
     HGNN_LAUNCH_CHECK();
     return 0;

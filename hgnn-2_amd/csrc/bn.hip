@@ -1053,192 +1053,6 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     return 0;
 }
 
-// ---------------------------------------------------------------- BN backward of the executor (net.hip)
-// The statistics of a layer output's input gradient dz arrive as partials (sum dz, sum dz h) per block of
-// rows: from the gather that finalised dz (BnStatPart, 16 rows) or from launch_bn_stat_rows (64 rows).
-// One wave per channel sums them in fp64 (lane i takes tiles i, i + 64, ..., up to 32 loads of a round in
-// flight -- 1.5 K tiles at config 2's edge half in one round; no LDS, no barrier), then stores the apply
-// constants (mean, 1 / std, m1, m2) -- m1 = w S1 / n, m2 = w S2 / n are the means of g = w dz and g h of the
-// BN-backward formula (batch_normalization.py:65-77 through autograd) -- and S2, S1 for the BN scalar grads.
-__global__ void __launch_bounds__(64) k_bn_stat_fin(BnStatArgs a) {
-    const int c = blockIdx.x, lane = threadIdx.x;
-    double S1 = 0.0, S2 = 0.0;
-    const int n = *a.count;
-    if (a.training) {
-        const int tiles = ceil_div(n, a.rows_per_tile);
-        constexpr int U = 32;
-        for (int t0 = 0; t0 < tiles; t0 += 64 * U) {
-            float2 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int t = t0 + u * 64 + lane;
-                v[u] = t < tiles ? a.part[(long long)t * a.c + c] : make_float2(0.f, 0.f);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                S1 += (double)v[u].x;
-                S2 += (double)v[u].y;
-            }
-        }
-        S1 = wave_sum_d(S1);
-        S2 = wave_sum_d(S2);
-    }
-    if (lane == 0) {
-        const double w = (double)*a.w;
-        const float m1 = a.training && n > 0 ? (float)(w * S1 / n) : 0.f;
-        const float m2 = a.training && n > 0 ? (float)(w * S2 / n) : 0.f;
-        a.k[c] = make_float4(a.mean[c], 1.0f / a.std[c], m1, m2);
-        if (a.sums) {
-            a.sums[c] = (float)S2;
-            a.sums[a.c + c] = (float)S1;
-        }
-    }
-}
-
-int launch_bn_stat_fin(const BnStatArgs& a, hipStream_t s) {
-    if (a.c <= 0 || (a.training && (!a.part || a.rows_per_tile <= 0))) return HGNN_ERR_ARG;
-    hipLaunchKernelGGL(k_bn_stat_fin, dim3(a.c), dim3(64), 0, s, a);
-    HGNN_LAUNCH_CHECK();
-    return 0;
-}
-
-// (sum dz, sum dz h) per 64-row tile and channel: threads = channel x row group, the groups' sums in a
-// fixed order through LDS.
-__global__ void __launch_bounds__(256) k_bn_stat_rows(const float* __restrict__ dz, const float* __restrict__ y,
-                                                      const float* __restrict__ mean, const float* __restrict__ stdv,
-                                                      const int* total_rows, int c, float2* __restrict__ part) {
-    const int t = blockIdx.x, total = *total_rows;
-    const int r0 = t * 64;
-    if (r0 >= total) return;
-    const int r1 = min(total, r0 + 64);
-    __shared__ float2 red[256];
-    for (int c0 = 0; c0 < c; c0 += 256) {
-        const int cw = min(256, c - c0), nrg = 256 / cw;
-        const int rg = threadIdx.x / cw, ch = c0 + threadIdx.x % cw;
-        float2 v = make_float2(0.f, 0.f);
-        if (rg < nrg) {
-            const float mu = mean[ch], isd = 1.0f / stdv[ch];
-            for (int r = r0 + rg; r < r1; r += nrg) {
-                const float d = dz[(long long)r * c + ch];
-                v.x += d;
-                v.y += d * ((y[(long long)r * c + ch] - mu) * isd);
-            }
-        }
-        red[threadIdx.x] = v;
-        __syncthreads();
-        if ((int)threadIdx.x < cw) {
-            float2 q = red[threadIdx.x];
-            for (int g = 1; g < nrg; ++g) {
-                q.x += red[g * cw + threadIdx.x].x;
-                q.y += red[g * cw + threadIdx.x].y;
-            }
-            part[(long long)t * c + c0 + threadIdx.x] = q;
-        }
-        __syncthreads();
-    }
-}
-
-int launch_bn_stat_rows(const float* dz, const float* y, const float* mean, const float* std, const int* total_rows,
-                        int cap_rows, int c, float2* part, hipStream_t s) {
-    if (cap_rows <= 0) return 0;
-    if (c <= 0) return HGNN_ERR_ARG;
-    hipLaunchKernelGGL(k_bn_stat_rows, dim3(ceil_div(cap_rows, 64)), dim3(256), 0, s, dz, y, mean, std, total_rows, c,
-                       part);
-    HGNN_LAUNCH_CHECK();
-    return 0;
-}
-
-// dY of one 64-row tile per block and the tile's column sums (dbpart).  c % 4 == 0 and ldy == c: threads =
-// float4 channel group x row group (every load of a thread's rows in flight); otherwise one channel per
-// thread, the columns [c, ldy) written as zeros.
-template <bool V4>
-__global__ void __launch_bounds__(256) k_bn_apply_bwd(BnApplyArgs p, const int* total_rows, int c) {
-    const int t = blockIdx.x, total = *total_rows;
-    const int r0 = t * 64;
-    if (r0 >= total) return;
-    const int r1 = min(total, r0 + 64);
-    const float wv = *p.w;
-    const bool tr = p.training != 0;
-    __shared__ float4 red[256];
-    constexpr int W = V4 ? 4 : 1;
-    const int ld = V4 ? c : p.ldy;                // channels written per row (the padding too)
-    const int ngr = ceil_div(ld, W);
-    for (int g0 = 0; g0 < ngr; g0 += 256) {
-        const int gw = min(256, ngr - g0), nrg = 256 / gw;
-        const int rg = threadIdx.x / gw, gi = g0 + threadIdx.x % gw;
-        float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (rg < nrg) {
-            float4 k[W];
-            bool relu[W];
-#pragma unroll
-            for (int e = 0; e < W; ++e) {
-                const int ch = gi * W + e;
-                k[e] = ch < c ? p.k[ch] : make_float4(0.f, 0.f, 0.f, 0.f);
-                relu[e] = ch >= p.relu_from;
-            }
-            constexpr int U = 8;
-            for (int rb = r0 + rg; rb < r1; rb += U * nrg) {
-                float dv[U][W], yv[U][W];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const long long r = min(rb + u * nrg, r1 - 1);  // clamped: selected below
-                    if constexpr (V4) {
-                        const float4 a = *reinterpret_cast<const float4*>(p.dz + r * c + 4 * gi);
-                        const float4 b = *reinterpret_cast<const float4*>(p.y + r * c + 4 * gi);
-                        dv[u][0] = a.x; dv[u][1] = a.y; dv[u][2] = a.z; dv[u][3] = a.w;
-                        yv[u][0] = b.x; yv[u][1] = b.y; yv[u][2] = b.z; yv[u][3] = b.w;
-                    } else {
-                        dv[u][0] = gi < c ? p.dz[r * c + gi] : 0.f;
-                        yv[u][0] = gi < c ? p.y[r * c + gi] : 0.f;
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int r = rb + u * nrg;
-                    if (r >= r1) continue;
-                    float d[W];
-#pragma unroll
-                    for (int e = 0; e < W; ++e) {
-                        d[e] = gi * W + e < c ? bn_bwd_dy_inv(yv[u][e], dv[u][e], k[e].x, k[e].y, wv, k[e].z, k[e].w,
-                                                              tr, relu[e])
-                                              : 0.f;
-                        f4c(cs, e) += d[e];
-                    }
-                    if constexpr (V4)
-                        *reinterpret_cast<float4*>(p.dy + (long long)r * p.ldy + 4 * gi) = make_float4(d[0], d[1], d[2], d[3]);
-                    else
-                        p.dy[(long long)r * p.ldy + gi] = d[0];
-                }
-            }
-        }
-        red[threadIdx.x] = cs;
-        __syncthreads();
-        if ((int)threadIdx.x < gw && p.dbpart) {
-            float4 q = red[threadIdx.x];
-            for (int g = 1; g < nrg; ++g) {
-                const float4 x = red[g * gw + threadIdx.x];
-                q.x += x.x; q.y += x.y; q.z += x.z; q.w += x.w;
-            }
-#pragma unroll
-            for (int e = 0; e < W; ++e)
-                if (gi * W + e < c) p.dbpart[(long long)t * c + gi * W + e] = f4c(q, e);
-        }
-        __syncthreads();
-    }
-}
-
-int launch_bn_apply_bwd(const BnApplyArgs& ap, const int* total_rows, int cap_rows, int c, hipStream_t s) {
-    if (cap_rows <= 0) return 0;
-    if (!ap.dz || !ap.y || !ap.k || !ap.dy || ap.ldy < c || c <= 0) return HGNN_ERR_ARG;
-    const dim3 g(ceil_div(cap_rows, 64));
-    const bool v4 = c % 4 == 0 && ap.ldy == c && ((uintptr_t)ap.dz & 15) == 0 && ((uintptr_t)ap.y & 15) == 0 &&
-                    ((uintptr_t)ap.dy & 15) == 0;
-    if (v4) hipLaunchKernelGGL(k_bn_apply_bwd<true>, g, dim3(256), 0, s, ap, total_rows, c);
-    else hipLaunchKernelGGL(k_bn_apply_bwd<false>, g, dim3(256), 0, s, ap, total_rows, c);
-    HGNN_LAUNCH_CHECK();
-    return 0;
-}
-
 // ---------------------------------------------------------------- readout
 // y[b, o] = sum_{n < N_b} sum_k A[n, k] fcw[o, k] + Nmax * fcb[o]
 // The reference sums fc(x1) over all Nmax padded positions; padded positions

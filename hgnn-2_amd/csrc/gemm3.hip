@@ -780,12 +780,19 @@ int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, in
     if (m_cap <= 0) return 0;
     if (o % 4 != 0) return HGNN_ERR_UNSUPPORTED;
     if ((long long)m_cap * lddy * 4 >= (1ll << 31) || (long long)kout * ldw * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    static const bool dma = [] {
+        const char* e = getenv("HGNN_GEMM_DMA");
+        return !(e && e[0] == '0');
+    }();
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    if (lddy % 4 == 0 && ldw % 4 == 0 && al(dy) && al(wt)) {
-        // the column tiles of a row tile on one XCD (k_gemm3's E3_FWD order)
-        const int gx = ceil_div(ceil_div(m_cap, 64), 8) * 8;
+    if (dma && lddy % 4 == 0 && ldw % 4 == 0 && al(dy) && al(wt)) {
+        static const bool xcd = [] {
+            const char* e = getenv("HGNN_DA_XCD");
+            return !e || e[0] != '0';
+        }();
+        const int gx = xcd ? ceil_div(ceil_div(m_cap, 64), 8) * 8 : ceil_div(m_cap, 64);
         hipLaunchKernelGGL((k_gemm5<64, 64, 2, 2>), dim3(gx, ceil_div(kout, 64)), dim3(256), 0, s,
-                           dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda, 1);
+                           dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda, xcd ? 1 : 0);
         HGNN_LAUNCH_CHECK();
         return 0;
     }

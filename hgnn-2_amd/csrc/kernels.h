@@ -109,16 +109,6 @@ struct AggFwdArgs {
 };
 int launch_agg_fwd(const AggFwdArgs& a, hipStream_t s);
 
-// The gather that finalises a layer output's input gradient dz (its last writer) also emits the BN-backward
-// statistics of its rows: per block of AGG_ST_ROWS rows, part[block][c] = (sum dz, sum dz h),
-// h = (y - mean) / std -- the pass over dz and y a separate statistics kernel would make (net.hip).
-constexpr int AGG_ST_ROWS = 16;
-struct BnStatPart {
-    const float* y;        // pre-BN activations [rows][c]; null = no statistics
-    const float* mean;
-    const float* std;
-    float2* part;          // out [ceil(rows / AGG_ST_ROWS)][c]
-};
 struct AggBwdArgs {
     const int* total_rows;
     int cap_rows;
@@ -134,7 +124,6 @@ struct AggBwdArgs {
     float* out;
     int ldo;
     int accumulate;
-    BnStatPart st;          // st.y != null: out is final here -- also its BN-backward statistics
 };
 int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s);  // exactly one of ing / inp
 // the G gather of ga and the P gather of pa (different outputs) in one grid when they
@@ -229,12 +218,10 @@ size_t dw3_slab_floats(int r_cap, int o, int k);
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
                     int nz, float* slabs, hipStream_t s);
 // slabs [z][o][k] -> dW (rows [0, split) -> dw0, [split, o_real) -> dw1; rows >= o_real are the
-// zero padding of an odd 2d); bias grads from per-64-row-tile column sums of dY (dbpart
-// [tiles][o_real]); with bn_sums ([2][o_real]: per-channel sum dz h, sum dz from launch_bn_stat_fin)
-// also the BN scalar grads bn_dw = sum_c (sum dz h), bn_db = sum_c (sum dz)
+// zero padding of an odd 2d); bias grads from the BN-backward per-tile column sums of dY
+// (dbpart [tiles][o_real])
 int launch_dw_reduce2(const float* slabs, const int* r_valid, int nz, int o, int o_real, int k, int split,
-                      float* dw0, float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s,
-                      const float* bn_sums = nullptr, float* bn_dw = nullptr, float* bn_db = nullptr);
+                      float* dw0, float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s);
 
 // ---------------------------------------------------------------- BN
 struct BnFwdArgs {
@@ -275,43 +262,9 @@ struct BnBwdArgs {
     float* db;             // scalar out
     float* dbpart;         // optional out: per-64-row-tile column sums of dy [tiles][c]
 };
+// apply = 0: only the statistics (part + fin)
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply = 1);
 int bn_bwd_tiles(int cap_rows);
-
-// ---- BN backward of the network executor (net.hip)
-// Per channel: the statistics S1 = sum dz, S2 = sum dz h of the partials (BnStatPart / launch_bn_stat_rows),
-// and the apply constants k[c] = (mean, 1 / std, m1 = w S1 / n, m2 = w S2 / n); sums[c] = S2, sums[c + c] = S1
-// (the BN scalar grads, summed over the channels by launch_dw_reduce2).  Eval (training = 0): m1 = m2 = 0.
-struct BnStatArgs {
-    const float2* part;    // [tiles][c], tiles = ceil(*count / rows_per_tile)
-    int rows_per_tile;
-    const int* count;      // device: rows of the BN layer
-    int c;
-    const float* w;
-    const float* mean;     // the layer's BN statistics in use (batch; running in eval)
-    const float* std;
-    int training;
-    float4* k;
-    float* sums;
-};
-int launch_bn_stat_fin(const BnStatArgs& a, hipStream_t s);
-// the statistics partials straight from dz and y, per 64-row tile (a layer output whose gradient no gather
-// finalises: only the readout writes it)
-int launch_bn_stat_rows(const float* dz, const float* y, const float* mean, const float* std, const int* total_rows,
-                        int cap_rows, int c, float2* part, hipStream_t s);
-// dY = relu'(y) (w dz - m1 - h m2) / std (train; eval: w dz / std), columns [c, ldy) zero; and the conv bias
-// grads' partials dbpart[t][c] = sum of dY over the 64-row tile t
-struct BnApplyArgs {
-    const float* dz;
-    const float* y;
-    const float4* k;       // launch_bn_stat_fin
-    const float* w;
-    float* dy;
-    int ldy;
-    int relu_from, training;
-    float* dbpart;
-};
-int launch_bn_apply_bwd(const BnApplyArgs& ap, const int* total_rows, int cap_rows, int c, hipStream_t s);
 
 // dY of BN backward + ReLU for one element (batch_normalization.py:65-77 autograd):
 // g = w dz, h = (y - mean) / std, train: (g - m1 - h m2) / std with m1 = mean(g),

@@ -40,11 +40,6 @@ struct Half {
     int kp;  // row stride of the aggregate / dA buffers (k rounded up to 4: the GEMMs' float4 k)
     size_t a = 0, part = 0, mean = 0, stdv = 0;
     size_t wt = 0, wc = 0, bc = 0;  // repacked Conv1d-pair weights (repack.hip)
-    // backward, per half (every buffer written once per backward, so the side stream may read it late):
-    size_t stp = 0;   // BN statistics partials of the output's gradient [ceil(cap / 16)][c2] float2
-    size_t bst = 0;   // BN-backward constants [c2] float4 (mean, 1 / std, m1, m2), then [2][c2] sums
-    size_t dy = 0;    // dY of the Conv1d pair [cap][c2p]
-    size_t dbp = 0;   // per-64-row-tile column sums of dY [ceil(cap / 64)][c2] (conv bias grads)
 };
 
 struct Program {
@@ -58,7 +53,7 @@ struct Program {
     size_t node_off = 0, edge_off = 0, totals = 0, err = 0;
     size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
     int entry_stride_w = 4;
-    size_t da = 0, da2 = 0, slabs = 0, rb_scratch = 0;
+    size_t dy = 0, dy2 = 0, da = 0, da2 = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0, dbpart2 = 0;
     size_t bytes = 0;
 };
 
@@ -241,20 +236,22 @@ Program build_program(const hgnn_net_config* c) {
         h.wt = B.take((size_t)h.k * P.c2p * sizeof(float));
         h.wc = B.take((size_t)P.c2 * h.kp * sizeof(float));
         h.bc = B.take((size_t)P.c2 * sizeof(float));
-        h.stp = B.take((size_t)ceil_div(std::max(cap, 64), 16) * P.c2 * sizeof(float2));
-        h.bst = B.take((size_t)6 * P.c2 * sizeof(float));
-        h.dy = B.take((size_t)cap * P.c2p * sizeof(float));
-        h.dbp = B.take((size_t)ceil_div(std::max(cap, 1), 64) * P.c2 * sizeof(float));
         max_da = std::max(max_da, (size_t)cap * h.kp);
         max_slab = std::max(max_slab, dw3_slab_floats(cap, P.c2, h.k));
         max_cap = std::max(max_cap, cap);
     }
+    P.dbpart = B.take((size_t)bn_bwd_tiles(max_cap > 0 ? max_cap : 1) * P.c2 * sizeof(float));
+    P.dbpart2 = B.take((size_t)bn_bwd_tiles(max_cap > 0 ? max_cap : 1) * P.c2 * sizeof(float));
     P.a_last = B.take((size_t)P.cap_n * P.k_last * sizeof(float));
     P.colsum = B.take((size_t)c->bs * P.k_last * sizeof(float));
     max_da = std::max(max_da, (size_t)P.cap_n * P.k_last);
+    P.dy = B.take((size_t)max_cap * P.c2p * sizeof(float));
+    P.dy2 = B.take((size_t)max_cap * P.c2p * sizeof(float));
     P.da = B.take(max_da * sizeof(float));
-    P.da2 = B.take(max_da * sizeof(float));  // dA alternates: the side stream's dense dW reads it
+    P.da2 = B.take(max_da * sizeof(float));  // dA alternates like dY: the side stream's dense dW reads it
     P.slabs = B.take(max_slab * sizeof(float));
+    P.bnb_part = B.take((size_t)bn_bwd_tiles(max_cap) * P.c2 * 4 * sizeof(float));
+    P.bnb_sums = B.take((size_t)P.c2 * 4 * sizeof(float));
     P.rb_scratch = B.take(readout_bwd_scratch_bytes(c->dim_out, P.k_last));
     P.bytes = B.top;
     return P;
@@ -394,8 +391,7 @@ struct Timer {
         }                                                                               \
     } while (0)
 
-// Side stream.  Forward (line graph): the G part of a half's aggregation beside the main
-// stream's P part and GEMMs (net_forward).  Backward: the weight-gradient GEMM of a half (and its slab
+// Side stream.  Backward: the weight-gradient GEMM of a half (and its slab
 // reduction) only feeds the parameter grads, so it runs beside the dA -> dense dW
 // -> aggregation-backward chain of the same half.  Fork after the half's BN
 // backward, join before the next half's BN backward overwrites dY / the bias
@@ -575,14 +571,6 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
     return 0;
 }
 
-// Backward.  The BN backward of a layer output needs two statistics of its input gradient dz (S1 = sum dz,
-// S2 = sum dz h per channel, h = (y - mean) / std) before any row of dY exists.  dz is the sum of its
-// consumers' transposed gathers; the gather that runs last (the consumer half with the lowest program
-// index) emits the statistics partials of the rows it finalises (BnStatPart, 16 rows per block), so the
-// BN backward is one small reduction (launch_bn_stat_fin: the apply constants and the BN scalar grads'
-// sums) and one wide elementwise pass (launch_bn_apply_bwd: dY and the conv bias grads' tile sums) -- no
-// separate statistics pass over dz and y.  A layer output that only the readout reads gets its partials
-// from launch_bn_stat_rows.
 int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
                  const float* const* prm, void* ws, const float* dout, float* const* grads, float* dX, float* dW,
                  hipStream_t s, Timer* tm, void* const* ev = nullptr, int n_ev = 0) {
@@ -592,8 +580,6 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     BatchMeta m = src.m;
     const int* tot_n = m.totals;
     const int* tot_e = m.totals + 1;
-    const int H = (int)P.halves.size();
-    const bool train = c->training != 0;
     std::vector<char> init(P.feats.size(), 0);
     auto needs_grad = [&](int f) {
         if (f < 0) return false;
@@ -603,33 +589,6 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     };
     const bool need_dw = c->need_dw != 0;
     if (need_dw && (!dW || !in || !in->d_X || csr)) return HGNN_ERR_ARG;
-    // consumers of each layer output: the half reading it through its G part and through its P part
-    std::vector<int> cons_g(P.feats.size(), -1), cons_p(P.feats.size(), -1), prod(P.feats.size(), -1);
-    for (int hi = 0; hi < H; ++hi) {
-        const Half& h = P.halves[hi];
-        cons_g[h.gin] = hi;
-        if (h.pin >= 0) cons_p[h.pin] = hi;
-        prod[h.out] = hi;
-    }
-    // the gather that finalises a layer output's gradient: its consumer processed last, i.e. the one with
-    // the lowest program index (the readout's gathers run before every half)
-    auto last_part = [&](int f) -> int {  // 0: the readout only; 1: G part of cons_g; 2: P part of cons_p
-        const int g = cons_g[f], p = cons_p[f];
-        if (g < 0 && p < 0) return 0;
-        if (p < 0 || (g >= 0 && g < p)) return 1;
-        return 2;
-    };
-    auto is_bn_feat = [&](int f) { return f >= 0 && prod[f] >= 0; };
-    auto stat_part = [&](int f) -> BnStatPart {  // statistics partials of layer output f's gradient
-        const Half& hp = P.halves[prod[f]];
-        BnStatPart sp{};
-        if (!train) return sp;
-        sp.y = at<float>(ws, P.feats[f].y);
-        sp.mean = at<float>(ws, hp.mean);
-        sp.std = at<float>(ws, hp.stdv);
-        sp.part = at<float2>(ws, hp.stp);
-        return sp;
-    };
     // dense dW contribution of one graph_oper(W, X_l): G block of dA (node rows) x X_l
     auto dw_args = [&](int gin, const float* da, int lda, bool readout, int accumulate) -> DwDenseArgs {
         DwDenseArgs a{};
@@ -701,14 +660,15 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         if (lgr || lpr) TL(HGNN_K_AGG_BWD, launch_readout_agg_bwd(ra, s));
         if (lgr) init[P.last_gin] = 1;
         if (lpr) init[P.last_pin] = 1;
-    } else if (lgr || lpr || need_dw) {
+    } else if (needs_grad(P.last_gin) || needs_grad(P.last_pin) || need_dw) {
         float* da = at<float>(ws, P.da);
         TL(HGNN_K_READOUT, launch_readout_bwd_da(dout, m.node_off, c->bs, P.cap_n, tot_n, prm[P.p_fcw], c->dim_out, P.k_last,
                                   da, s));
         if (need_dw) TL(HGNN_K_DW_DENSE, dw_dense(P.last_gin, da, P.k_last, true, 0));
         const int cg = P.feats[P.last_gin].c;
+        const bool lg = needs_grad(P.last_gin), lp = needs_grad(P.last_pin);
         AggBwdArgs gab{}, pab{};
-        if (lgr) {
+        if (lg) {
             gab.total_rows = tot_n;
             gab.cap_rows = P.cap_n;
             gab.g = src.v[S_WT];
@@ -721,7 +681,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             gab.ldo = cg;
             gab.accumulate = init[P.last_gin];
         }
-        if (lpr) {
+        if (lp) {
             const int cp = P.feats[P.last_pin].c;
             pab.total_rows = tot_e;
             pab.cap_rows = P.cap_e;
@@ -736,11 +696,11 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             pab.ldo = cp;
             pab.accumulate = init[P.last_pin];
         }
-        if (lgr && lpr) TL(HGNN_K_AGG_BWD, launch_agg_bwd_pair(gab, pab, s));
-        else if (lgr) TL(HGNN_K_AGG_BWD, launch_agg_bwd(gab, s));
-        else if (lpr) TL(HGNN_K_AGG_BWD, launch_agg_bwd(pab, s));
-        if (lgr) init[P.last_gin] = 1;
-        if (lpr) init[P.last_pin] = 1;
+        if (lg && lp) TL(HGNN_K_AGG_BWD, launch_agg_bwd_pair(gab, pab, s));
+        else if (lg) TL(HGNN_K_AGG_BWD, launch_agg_bwd(gab, s));
+        else if (lp) TL(HGNN_K_AGG_BWD, launch_agg_bwd(pab, s));
+        if (lg) init[P.last_gin] = 1;
+        if (lp) init[P.last_pin] = 1;
     }
 
     SideStream* side = nullptr;
@@ -748,16 +708,17 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     // cross-stream event record / wait costs the main stream ~6-7 us of idle GPU per fork)
     static const bool use_side = env_flag("HGNN_SIDE", true);
     if (use_side) TRY(side_stream(s, &side));
-    // dA alternates between two buffers: the side stream's dense operator gradient (W.requires_grad) of
-    // half i may still read its buffer while the main stream runs half i - 1; every other buffer the side
-    // stream reads (a half's dY, bias-gradient partials and BN sums, the aggregate) is written once per
-    // backward.
+    // dY and the bias partials alternate between two buffers, so the side stream's
+    // dW of half i may still read its pair while the main stream runs half i+1.
     bool pending[2] = {false, false};
     int parity = 0;
-    // (Measured alternative, not kept: the gather half of the aggregation backward on a third stream,
-    // overlapping the next half -- 268K vs 286K graphs/s: the concurrent memory-bound kernels only
-    // slowed each other.)
-    auto fork_dw = [&](const Half& h, int cap, const int* tot, bool ndw_side, float* dab) -> int {
+    // The side stream also takes the dense operator gradient (W.requires_grad) of a node
+    // half: it only accumulates into dW, so it leaves the dA -> aggregation-backward chain.
+    // (Measured alternative, not kept: the gather half of the aggregation backward on a third
+    // stream, overlapping the next half -- 268K vs 286K graphs/s: the concurrent memory-bound
+    // kernels only slowed each other.)
+    auto fork_dw = [&](const Half& h, int cap, const int* tot, float* dyb, float* dbp, bool ndw_side,
+                       float* dab) -> int {
         const int nz = dw3_chunks(cap, P.c2, h.k);
         if (side) {
             HGNN_HOST_CHECK(hipEventRecord(side->fork[parity], s));
@@ -773,16 +734,15 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             if (ndw_side) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, dab, h.kp, false, 1));
             // dY rows have stride c2p; the dW GEMM's float4 loads along the 2d outputs read the zero
             // padding of an odd 2d and store only the 2d real rows of each slab
-            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(at<float>(ws, h.dy), P.c2p, at<float>(ws, h.a), h.kp, tot, cap, P.c2,
-                                               h.k, nz, at<float>(ws, P.slabs), s));
+            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(dyb, P.c2p, at<float>(ws, h.a), h.kp, tot, cap, P.c2, h.k, nz,
+                                               at<float>(ws, P.slabs), s));
             TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, nz, P.c2, P.c2, h.k, P.d,
-                                                   grads[h.pw_lin], grads[h.pw_relu], at<float>(ws, h.dbp),
-                                                   grads[h.pb_lin], grads[h.pb_relu], s,
-                                                   at<float>(ws, h.bst) + 4 * P.c2, grads[h.pbn_w], grads[h.pbn_b]));
+                                                   grads[h.pw_lin], grads[h.pw_relu], dbp, grads[h.pb_lin],
+                                                   grads[h.pb_relu], s));
             if (side) r = hipEventRecord(side->join[parity], s) == hipSuccess ? 0 : HGNN_ERR_HIP;
         } while (0);
         s = main_s;
-        pending[parity] = side != nullptr && ndw_side;
+        pending[parity] = side != nullptr;
         return r;
     };
     // per-layer completion events (hgnn_net_backward_ex): recorded once the first half (in program
@@ -800,58 +760,45 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         const Half& h = P.halves[hi];
         const int cap = h.edge ? P.cap_e : P.cap_n;
         const int* tot = h.edge ? tot_e : tot_n;
-        const int f = h.out;
-        // BN backward of this half's output: its gradient dz is final (every consumer has run)
-        if (!init[f]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[f].grad), 0,
-                                                     (size_t)cap * P.c2 * sizeof(float), s));
-        int rpt = AGG_ST_ROWS;
-        if (train && (!init[f] || last_part(f) == 0)) {  // no gather emitted the statistics partials
-            TL(HGNN_K_BN_BWD, launch_bn_stat_rows(at<float>(ws, P.feats[f].grad), at<float>(ws, P.feats[f].y),
-                                                  at<float>(ws, h.mean), at<float>(ws, h.stdv), tot, cap, P.c2,
-                                                  at<float2>(ws, h.stp), s));
-            rpt = 64;
-        }
-        BnStatArgs sa{};
-        sa.part = at<float2>(ws, h.stp);
-        sa.rows_per_tile = rpt;
-        sa.count = tot;
-        sa.c = P.c2;
-        sa.w = prm[h.pbn_w];
-        sa.mean = at<float>(ws, h.mean);
-        sa.std = at<float>(ws, h.stdv);
-        sa.training = c->training;
-        sa.k = at<float4>(ws, h.bst);
-        sa.sums = at<float>(ws, h.bst) + 4 * P.c2;
-        TL(HGNN_K_BN_BWD, launch_bn_stat_fin(sa, s));
-        BnApplyArgs ap{};
-        ap.dz = at<float>(ws, P.feats[f].grad);
-        ap.y = at<float>(ws, P.feats[f].y);
-        ap.k = at<float4>(ws, h.bst);
-        ap.w = prm[h.pbn_w];
-        ap.dy = at<float>(ws, h.dy);
-        ap.ldy = P.c2p;
-        ap.relu_from = h.relu_from;
-        ap.training = c->training;
-        ap.dbpart = at<float>(ws, h.dbp);
-        TL(HGNN_K_BN_BWD, launch_bn_apply_bwd(ap, tot, cap, P.c2, s));
-        init[f] = 1;
-
-        const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
-        const bool ndw = need_dw && !h.edge;
-        if (!ng && !np && !ndw) {
-            TRY(fork_dw(h, cap, tot, false, nullptr));
-            return 0;
-        }
-        float* da = at<float>(ws, parity ? P.da2 : P.da);
-        if (pending[parity]) {  // the dense dW two halves back still reads this dA buffer
+        float* dyb = at<float>(ws, parity ? P.dy2 : P.dy);
+        float* dbp = at<float>(ws, parity ? P.dbpart2 : P.dbpart);
+        if (pending[parity]) {  // the dW two halves back still reads this dY / bias-partial pair
             HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[parity], 0));
             pending[parity] = false;
         }
-        TL(HGNN_K_GEMM_DA, launch_gemm3_da(at<float>(ws, h.dy), P.c2p, tot, cap, P.c2p, at<float>(ws, h.wt), P.c2p,
-                                           h.k, da, h.kp, s));
+        if (!init[h.out]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[h.out].grad), 0,
+                                                          (size_t)cap * P.c2 * sizeof(float), s));
+        BnBwdArgs bb{};
+        bb.y = at<float>(ws, P.feats[h.out].y);
+        bb.dz = at<float>(ws, P.feats[h.out].grad);
+        bb.total_rows = tot;
+        bb.cap_rows = cap;
+        bb.c = P.c2;
+        bb.mean = at<float>(ws, h.mean);
+        bb.std = at<float>(ws, h.stdv);
+        bb.w = prm[h.pbn_w];
+        bb.relu_from = h.relu_from;
+        bb.training = c->training;
+        bb.part = at<float>(ws, P.bnb_part);
+        bb.sums = at<float>(ws, P.bnb_sums);
+        bb.dy = dyb;
+        bb.dw = grads[h.pbn_w];
+        bb.db = grads[h.pbn_b];
+        bb.dbpart = dbp;
+        bb.ldy = P.c2p;
+        const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
+        const bool ndw = need_dw && !h.edge;
+        TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s));
+
+        if (!ng && !np && !ndw) {
+            TRY(fork_dw(h, cap, tot, dyb, dbp, false, nullptr));
+            return 0;
+        }
+        float* da = at<float>(ws, parity ? P.da2 : P.da);
+        TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2p, tot, cap, P.c2p, at<float>(ws, h.wt), P.c2p, h.k, da, h.kp, s));
         // dW starts once dA is done: two MFMA GEMMs side by side only slow each other,
-        // dW beside the latency-bound aggregation-backward kernels does not
-        TRY(fork_dw(h, cap, tot, ndw, da));
+        // dW beside the latency-bound dense-dW / aggregation-backward kernels does not
+        TRY(fork_dw(h, cap, tot, dyb, dbp, ndw, da));
         AggBwdArgs gab{}, pab{};
         if (ng) {
             gab.total_rows = tot;
@@ -865,7 +812,6 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             gab.out = at<float>(ws, P.feats[h.gin].grad);
             gab.ldo = h.cg;
             gab.accumulate = init[h.gin];
-            if (is_bn_feat(h.gin) && last_part(h.gin) == 1 && cons_g[h.gin] == hi) gab.st = stat_part(h.gin);
         }
         if (np) {
             const bool other_edge = !h.edge;
@@ -881,7 +827,6 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             pab.out = at<float>(ws, P.feats[h.pin].grad);
             pab.ldo = h.cp;
             pab.accumulate = init[h.pin];
-            if (is_bn_feat(h.pin) && last_part(h.pin) == 2 && cons_p[h.pin] == hi) pab.st = stat_part(h.pin);
         }
         if (ng && np) TL(HGNN_K_AGG_BWD, launch_agg_bwd_pair(gab, pab, s));
         else if (ng) TL(HGNN_K_AGG_BWD, launch_agg_bwd(gab, s));
@@ -890,14 +835,12 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         if (np) init[h.pin] = 1;
         return 0;
     };
-    for (int hi = H - 1; hi >= 0; --hi, parity ^= 1) {
+    for (int hi = (int)P.halves.size() - 1; hi >= 0; --hi, parity ^= 1) {
         TRY(half_bwd(hi));
         TRY(mark(hi));
     }
-    if (side) {  // the weight gradients are complete when the call's stream has passed this point
-        HGNN_HOST_CHECK(hipEventRecord(side->join[parity], side->s));
-        HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[parity], 0));
-    }
+    for (int p = 0; p < 2; ++p)
+        if (pending[p]) HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[p], 0));
     if (c->need_dx) {
         if (!dX) return HGNN_ERR_ARG;
         if (!init[0]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[0].grad), 0,

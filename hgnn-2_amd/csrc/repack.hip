@@ -27,15 +27,18 @@ int launch_repack(const RepackTable& t, hipStream_t s) {
 
 // Slab sums: SG groups of slabs per output, each summed by one thread (4 accumulators), the SG
 // partials combined in order through LDS -- many slabs (the narrow-K layer-0 halves cut their rows
-// into ~374 chunks) no longer mean one long serial chain per output.
-// Trailing blocks of both reductions: block o < MR the bias gradient of output channel o (the tile
-// sums dbpart[t][o]); block MR the BN scalar grads from the per-channel sums of launch_bn_stat_fin
-// (bn_sums[c] = sum dz h, bn_sums[MR + c] = sum dz): summed over the channels in fp64.
-__device__ __forceinline__ void db_tail(int o, const int* r_valid, int MR, int split, const float* __restrict__ dbpart,
-                                        float* db0, float* db1, const float* __restrict__ bn_sums, float* bn_dw,
-                                        float* bn_db) {
-    __shared__ double red[4], red2[4];
-    if (o < MR) {
+// into ~374 chunks) no longer mean one long serial chain per output.  Trailing blocks: the bias
+// gradient of output channel o from the BN-backward tile sums (k_db_reduce's work, same order).
+template <int SG>
+__global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ slabs, const int* r_valid,
+                                                    int nz, int M, int MR, int N, int split, float* dw0,
+                                                    float* dw1, const float* __restrict__ dbpart, float* db0,
+                                                    float* db1) {
+    constexpr int OUT = 256 / SG;
+    const int nwb = (MR * N + OUT - 1) / OUT;
+    if ((int)blockIdx.x >= nwb) {
+        __shared__ double red[4];
+        const int o = blockIdx.x - nwb;
         const int tv = ceil_div(*r_valid, 64);
         double s = 0.0;
         for (int t = threadIdx.x; t < tv; t += 256) s += (double)dbpart[(long long)t * MR + o];
@@ -47,35 +50,6 @@ __device__ __forceinline__ void db_tail(int o, const int* r_valid, int MR, int s
             if (o < split) db0[o] = (float)t;
             else db1[o - split] = (float)t;
         }
-        return;
-    }
-    double sw = 0.0, sb = 0.0;
-    for (int c = threadIdx.x; c < MR; c += 256) {
-        sw += (double)bn_sums[c];
-        sb += (double)bn_sums[MR + c];
-    }
-    sw = wave_sum_d(sw);
-    sb = wave_sum_d(sb);
-    if ((threadIdx.x & 63) == 0) {
-        red[threadIdx.x >> 6] = sw;
-        red2[threadIdx.x >> 6] = sb;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        *bn_dw = (float)(((red[0] + red[1]) + red[2]) + red[3]);
-        *bn_db = (float)(((red2[0] + red2[1]) + red2[2]) + red2[3]);
-    }
-}
-
-template <int SG>
-__global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ slabs, const int* r_valid,
-                                                    int nz, int M, int MR, int N, int split, float* dw0,
-                                                    float* dw1, const float* __restrict__ dbpart, float* db0,
-                                                    float* db1, const float* bn_sums, float* bn_dw, float* bn_db) {
-    constexpr int OUT = 256 / SG;
-    const int nwb = (MR * N + OUT - 1) / OUT;
-    if ((int)blockIdx.x >= nwb) {
-        db_tail(blockIdx.x - nwb, r_valid, MR, split, dbpart, db0, db1, bn_sums, bn_dw, bn_db);
         return;
     }
     __shared__ float part[SG][OUT];
@@ -112,11 +86,22 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
 // are combined in order through LDS; the bias gradients as in k_dw_reduce2.
 __global__ void __launch_bounds__(256) k_dw_reduce4(const float* __restrict__ slabs, const int* r_valid, int nz, int M,
                                                     int MR, int N, int split, float* dw0, float* dw1,
-                                                    const float* __restrict__ dbpart, float* db0, float* db1,
-                                                    const float* bn_sums, float* bn_dw, float* bn_db) {
+                                                    const float* __restrict__ dbpart, float* db0, float* db1) {
     const int total = MR * N, nwb = (total + 255) / 256;
     if ((int)blockIdx.x >= nwb) {
-        db_tail(blockIdx.x - nwb, r_valid, MR, split, dbpart, db0, db1, bn_sums, bn_dw, bn_db);
+        __shared__ double red[4];
+        const int o = blockIdx.x - nwb;
+        const int tv = ceil_div(*r_valid, 64);
+        double s = 0.0;
+        for (int t = threadIdx.x; t < tv; t += 256) s += (double)dbpart[(long long)t * MR + o];
+        s = wave_sum_d(s);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const double t = red[0] + red[1] + red[2] + red[3];
+            if (o < split) db0[o] = (float)t;
+            else db1[o - split] = (float)t;
+        }
         return;
     }
     __shared__ float4 part[4][64];
@@ -159,23 +144,20 @@ __global__ void __launch_bounds__(256) k_dw_reduce4(const float* __restrict__ sl
 }
 
 int launch_dw_reduce2(const float* slabs, const int* r_valid, int nz, int o, int o_real, int k, int split,
-                      float* dw0, float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s,
-                      const float* bn_sums, float* bn_dw, float* bn_db) {
+                      float* dw0, float* dw1, const float* dbpart, float* db0, float* db1, hipStream_t s) {
     if (o_real <= 0 || o_real > o || nz <= 0) return HGNN_ERR_ARG;
-    if ((bn_sums != nullptr) != (bn_dw != nullptr) || (bn_dw != nullptr) != (bn_db != nullptr) || (bn_dw && !dbpart))
-        return HGNN_ERR_ARG;
     const int total = o_real * k;
     // slab groups by the slab count: more groups when there are many slabs per output
-    const int nb = dbpart ? o_real + (bn_dw ? 1 : 0) : 0;
+    const int nb = dbpart ? o_real : 0;
     if (total % 4 == 0 && ((long long)o * k) % 4 == 0 && ((uintptr_t)slabs & 15) == 0) {
         hipLaunchKernelGGL(k_dw_reduce4, dim3(ceil_div(total, 256) + nb), dim3(256), 0, s, slabs, r_valid, nz, o, o_real,
-                           k, split, dw0, dw1, dbpart, db0, db1, bn_sums, bn_dw, bn_db);
+                           k, split, dw0, dw1, dbpart, db0, db1);
     } else if (nz > 32) {
         hipLaunchKernelGGL(k_dw_reduce2<16>, dim3(ceil_div(total, 16) + nb), dim3(256), 0, s, slabs, r_valid, nz,
-                           o, o_real, k, split, dw0, dw1, dbpart, db0, db1, bn_sums, bn_dw, bn_db);
+                           o, o_real, k, split, dw0, dw1, dbpart, db0, db1);
     } else {
         hipLaunchKernelGGL(k_dw_reduce2<4>, dim3(ceil_div(total, 64) + nb), dim3(256), 0, s, slabs, r_valid, nz,
-                           o, o_real, k, split, dw0, dw1, dbpart, db0, db1, bn_sums, bn_dw, bn_db);
+                           o, o_real, k, split, dw0, dw1, dbpart, db0, db1);
     }
     HGNN_LAUNCH_CHECK();
     return 0;

@@ -75,19 +75,13 @@ def class_work(kcls, counts, order, f_in, d, n_layers, jt=3):
             s_bytes = 8.0 * (r + r) + 16.0 * (nnz_g(edge) + counts["nnz_p"])
             by += 4.0 * (r * k + r * cg + ro * cp) + s_bytes
             fl += 2.0 * (nnz_g(edge) * jt * cg + 2 * counts["nnz_p"] * cp)
-        if kcls == K_AGG_BWD:
-            # the gather that finalises a layer output's gradient applies its BN backward: reads the
-            # pre-BN row, writes dY
-            for edge, k, cg, cp in halves:
-                by += 4.0 * 2 * rows(edge) * c2
     elif kcls == K_BN_FWD:
         for edge, k, cg, cp in halves:
             by += 4.0 * 2 * rows(edge) * c2
     elif kcls == K_BN_BWD:
-        # side pass: dz, y, dY read once (conv bias and BN scalar grads); the statistics come from
-        # the dA GEMMs' epilogues
+        # statistics pass (dz, y read) and apply pass (dz, y read, dY written)
         for edge, k, cg, cp in halves:
-            by += 4.0 * 3 * rows(edge) * c2
+            by += 4.0 * 5 * rows(edge) * c2
     return fl, by
 
 
@@ -145,7 +139,7 @@ CLASS_KERNELS = {
     K_GEMM_FWD: ("k_gemm3<", "k_gemm_fwd"),
     K_BN_FWD: ("k_bn_finalize", "k_bn_apply"),
     K_READOUT: ("k_readout",),
-    K_BN_BWD: ("k_bn_bwd", "k_bn_stat_fin", "k_bn_apply_bwd"),
+    K_BN_BWD: ("k_bn_bwd",),
     K_GEMM_DW: ("k_gemm3_tn", "k_gemm_dw"),
     K_GEMM_DA: ("k_gemm3<", "k_gemm_da"),
     K_AGG_BWD: ("k_agg_bwd",),
