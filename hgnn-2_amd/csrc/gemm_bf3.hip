@@ -1,0 +1,193 @@
+// fp32 GEMM on bf16 MFMA through a three-way operand split (the forward Conv1d-pair GEMM).
+//
+// An fp32 operand x is used as three bf16 parts, x = x1 + x2 + x3 (split3: x1 = bf16(x), x2 = bf16(x - x1),
+// x3 = bf16(x - x1 - x2); the residual is below 2^-26 |x|).  A product is the six bf16 x bf16 terms with
+// i + j <= 4, each exact in fp32, accumulated in fp32 by v_mfma_f32_32x32x16_bf16; the three dropped
+// terms are below 2^-26 of the product, so the result carries the error of an fp32 GEMM (one rounding per
+// accumulation).  Six bf16 MFMAs (6 x 32 cycles per 32x32x16) replace eight fp32 ones (8 x 64 cycles per
+// 32x32x16 of v_mfma_f32_32x32x2_f32): 2.7x fewer MFMA cycles, which the forward GEMM (K = 640 at
+// config 2, bound by the fp32 MFMA issue rate) turns into time.
+//
+// Y[M][N] = A[M][K] . B[N][K]^T (+ bias, ReLU from column relu_from, BN partials per 64-row tile) with A
+// the fp32 aggregate (split at staging) and B the weights as three bf16 planes [3][N][ldb] (split once by
+// the repack, zero beyond K).  Block 64 x 64, 2 x 2 waves of 32 x 32, k stages of 32 staged global ->
+// registers -> LDS (double buffer); LDS plane rows of 64 B with the 16-B chunks XOR-swizzled by
+// (row >> 2) & 3, so the fragment reads (ds_read_b128: 8 k of one row per lane) are conflict-free.
+#include "kernels.h"
+
+namespace hgnn {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int G_BM = 64, G_BN = 64, G_BK = 32, G_NT = 256;
+constexpr int G_ROWB = G_BK * 2;                      // bytes of one plane row in a stage
+constexpr int G_PLANE = G_BM * G_ROWB;                // bytes of one plane of one operand (BM == BN)
+constexpr int G_STAGE = 6 * G_PLANE;                  // A planes, then B planes
+
+__device__ __forceinline__ int swz(int row, int ch) { return row * G_ROWB + 16 * (ch ^ ((row >> 2) & 3)); }
+
+__global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__ A, int lda,
+                                                       const __bf16* __restrict__ B, long long pb, int ldb,
+                                                       const int* __restrict__ m_valid, int m_cap, int N, int K,
+                                                       float* __restrict__ Y, int ldy, const float* __restrict__ bias,
+                                                       int relu_from, float* __restrict__ bn_part) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * G_STAGE];
+    const int M = m_valid ? *m_valid : m_cap;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv >> 1, wn = wv & 1;
+    // the column tiles of a row tile on one XCD (blocks b and b + 8 share an XCD's L2): gridDim.x % 8 == 0,
+    // so the row tile's aggregate rows come from HBM once
+    const int L = blockIdx.x + gridDim.x * blockIdx.y, jj = L >> 3;
+    const int by = jj % gridDim.y, bx = (L & 7) + 8 * (jj / gridDim.y);
+    const int m0 = bx * G_BM, n0 = by * G_BN;
+    if (m0 >= M) return;
+    // staging: A -- 64 rows x 4 chunks of 8 k, one chunk (two float4) per thread, split into the three
+    // planes; B -- 3 planes x 64 rows x 4 chunks of 16 B, three per thread
+    const int arow = tid >> 2, ach = tid & 3;
+    float4 ra[2];
+    u32x4 rb[3];
+    auto load = [&](int k0) {
+        const int k = k0 + 8 * ach, gm = m0 + arow;
+        const float* ap = A + (long long)gm * lda + k;
+        ra[0] = (gm < M && k < K) ? *reinterpret_cast<const float4*>(ap) : make_float4(0.f, 0.f, 0.f, 0.f);
+        ra[1] = (gm < M && k + 4 < K) ? *reinterpret_cast<const float4*>(ap + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int e = tid + G_NT * i, pl = e >> 8, row = (e & 255) >> 2, ch = e & 3;
+            const int kb = k0 + 8 * ch, gn = n0 + row;
+            rb[i] = (gn < N && kb < ldb) ? *reinterpret_cast<const u32x4*>(B + pl * pb + (long long)gn * ldb + kb)
+                                         : u32x4{0u, 0u, 0u, 0u};
+        }
+    };
+    auto store = [&](int buf) {
+        char* st = lds + buf * G_STAGE;
+        const float xv[8] = {ra[0].x, ra[0].y, ra[0].z, ra[0].w, ra[1].x, ra[1].y, ra[1].z, ra[1].w};
+        bf16x8 p0, p1, p2;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            __bf16 a, b, c;
+            split3(xv[e], a, b, c);
+            p0[e] = a;
+            p1[e] = b;
+            p2[e] = c;
+        }
+        *reinterpret_cast<bf16x8*>(st + swz(arow, ach)) = p0;
+        *reinterpret_cast<bf16x8*>(st + G_PLANE + swz(arow, ach)) = p1;
+        *reinterpret_cast<bf16x8*>(st + 2 * G_PLANE + swz(arow, ach)) = p2;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int e = tid + G_NT * i, pl = e >> 8, row = (e & 255) >> 2, ch = e & 3;
+            *reinterpret_cast<u32x4*>(st + (3 + pl) * G_PLANE + swz(row, ch)) = rb[i];
+        }
+    };
+    f32x16 acc, tacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int nt = (K + G_BK - 1) / G_BK;
+    const int r31 = lane & 31, h = lane >> 5;
+    const int frow = wm * 32 + r31, fcol = wn * 32 + r31;
+    load(0);
+    store(0);
+    __syncthreads();
+    if (nt > 1) load(G_BK);
+    for (int t = 0; t < nt; ++t) {
+        const char* st = lds + (t & 1) * G_STAGE;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tacc[r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < G_BK / 16; ++s) {
+            const int ch = 2 * s + h;
+            bf16x8 a[3], b[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                a[p] = *reinterpret_cast<const bf16x8*>(st + p * G_PLANE + swz(frow, ch));
+                b[p] = *reinterpret_cast<const bf16x8*>(st + (3 + p) * G_PLANE + swz(fcol, ch));
+            }
+            // the six terms with i + j <= 4, the small ones first
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], tacc, 0, 0, 0);
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], tacc, 0, 0, 0);
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], tacc, 0, 0, 0);
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], tacc, 0, 0, 0);
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], tacc, 0, 0, 0);
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], tacc, 0, 0, 0);
+        }
+        acc += tacc;  // per-stage partial sums added to acc (fma chains of G_BK terms, as the fp32 GEMMs)
+        if (t + 1 < nt) {
+            store((t + 1) & 1);
+            if (t + 2 < nt) load((t + 2) * G_BK);
+        }
+        __syncthreads();
+    }
+    // epilogue (k_gemm3 E3_FWD's): bias, ReLU, store, BN partials (count, mean, M2) per 64-row tile.
+    // C/D layout of the 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    float* red = reinterpret_cast<float*>(lds);  // free: the main loop ended with a barrier
+    const int col = wn * 32 + r31, gn = n0 + col;
+    const float bv = gn < N ? bias[gn] : 0.f;
+    const bool relu = gn >= relu_from;
+    float sm = 0.f;
+    int cnt = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int gm = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float v = acc[r] + bv;
+        if (relu) v = v < 0.f ? 0.f : v;
+        acc[r] = v;
+        if (gm < M) {
+            if (gn < N) Y[(long long)gm * ldy + gn] = v;
+            sm += v;
+            ++cnt;
+        }
+    }
+    if (!bn_part) return;
+    sm += __shfl_xor(sm, 32, 64);
+    cnt += __shfl_xor(cnt, 32, 64);
+    if (lane < 32) {
+        red[wm * G_BN + col] = sm;
+        red[2 * G_BN + wm * G_BN + col] = (float)cnt;
+    }
+    __syncthreads();
+    const float S = red[col] + red[G_BN + col];
+    const float Cn = red[2 * G_BN + col] + red[3 * G_BN + col];
+    const float mean = Cn > 0.f ? S / Cn : 0.f;
+    __syncthreads();
+    float q = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int gm = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (gm < M) {
+            const float dl = acc[r] - mean;
+            q = fmaf(dl, dl, q);
+        }
+    }
+    q += __shfl_xor(q, 32, 64);
+    if (lane < 32) red[wm * G_BN + col] = q;
+    __syncthreads();
+    if (wm == 0 && lane < 32 && gn < N) {
+        float* pp = bn_part + ((long long)bx * N + gn) * 3;
+        pp[0] = Cn;
+        pp[1] = mean;
+        pp[2] = red[col] + red[G_BN + col];
+    }
+}
+
+}  // namespace
+
+int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
+                        int ldb, int n, const float* bias, int relu_from, float* y, int ldy, float* bn_part,
+                        hipStream_t s) {
+    if (m_cap <= 0 || n <= 0) return 0;
+    if (lda % 4 || k % 4 || ldb % 8 || pb % 8 || k > lda || bf3_ld(k) > ldb || (reinterpret_cast<uintptr_t>(a) & 15) ||
+        (reinterpret_cast<uintptr_t>(b) & 15))
+        return HGNN_ERR_UNSUPPORTED;
+    if ((long long)m_cap * lda * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    const int gx = ceil_div(ceil_div(m_cap, G_BM), 8) * 8;
+    hipLaunchKernelGGL(k_gemm_bf3_fwd, dim3(gx, ceil_div(n, G_BN)), dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid,
+                       m_cap, n, k, y, ldy, bias, relu_from, bn_part);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // namespace hgnn

@@ -130,7 +130,23 @@ int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s);  // exactly one of ing /
 // share the lane layout, else two launches
 int launch_agg_bwd_pair(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t s);
 
-// ---------------------------------------------------------------- GEMM (gemm3.hip, repack.hip)
+// ---------------------------------------------------------------- GEMM (gemm3.hip, gemm_bf3.hip, repack.hip)
+// fp32 x as three bf16 parts x1 + x2 + x3 (residual below 2^-26 |x|): the operand form of the split-bf16
+// GEMM (gemm_bf3.hip)
+__device__ __forceinline__ void split3(float x, __bf16& a, __bf16& b, __bf16& c) {
+    a = (__bf16)x;
+    const float r = x - (float)a;
+    b = (__bf16)r;
+    c = (__bf16)(r - (float)b);
+}
+__host__ __device__ inline int bf3_ld(int k) { return (k + 15) / 16 * 16; }  // plane row length (bf16)
+// The forward Conv1d-pair GEMM on bf16 MFMA (three-way split, fp32 accuracy): Y = A . B^T + bias, ReLU
+// from column relu_from, BN partials per 64-row tile (as launch_gemm3_fwd); A fp32 [M][lda] (k < kp),
+// B three bf16 planes b + p pb [N][ldb] (ldb >= bf3_ld(k), zero beyond k)
+int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
+                        int ldb, int n, const float* bias, int relu_from, float* y, int ldy, float* bn_part,
+                        hipStream_t s);
+
 struct RepackItem {
     const float* wl;   // linear conv weight (d, K)
     const float* wr;   // ReLU conv weight (d, K)
@@ -140,6 +156,8 @@ struct RepackItem {
     float* wc;         // out: [2d][kp]
     float* bc;         // out: [2d]
     int k, kp, ldt;
+    __bf16* wc3;       // optional out: Wcat as three bf16 planes [3][2d][ldc3] (split3), zero beyond K
+    int ldc3;
 };
 constexpr int REPACK_MAX = 24;
 struct RepackTable {
@@ -181,6 +199,18 @@ __device__ __forceinline__ void repack_part(const RepackTable& t, int item, int 
             if (k < K && n < ldt) it.wt[(long long)k * ldt + n] = tile[tx][rr];
         }
         __syncthreads();
+    }
+    // WC as three bf16 planes (the split-bf16 forward GEMM's B operand), coalesced along k
+    if (it.wc3) {
+        const long long n3 = (long long)c2 * it.ldc3;
+        for (long long e = (long long)yb * 256 + threadIdx.x; e < n3; e += (long long)t.y * 256) {
+            const int n = (int)(e / it.ldc3), k = (int)(e % it.ldc3);
+            __bf16 a, b, c;
+            split3(k < K ? W(n, k) : 0.f, a, b, c);
+            it.wc3[e] = a;
+            it.wc3[n3 + e] = b;
+            it.wc3[2 * n3 + e] = c;
+        }
     }
     // WC (zero-padded to kp) and bc: coalesced along k
     const long long nc = (long long)c2 * kp;

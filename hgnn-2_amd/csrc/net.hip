@@ -40,6 +40,7 @@ struct Half {
     int kp;  // row stride of the aggregate / dA buffers (k rounded up to 4: the GEMMs' float4 k)
     size_t a = 0, part = 0, mean = 0, stdv = 0;
     size_t wt = 0, wc = 0, bc = 0;  // repacked Conv1d-pair weights (repack.hip)
+    size_t wc3 = 0;                 // Wcat as three bf16 planes [3][2d][bf3_ld(kp)] (split-bf16 forward GEMM)
 };
 
 struct Program {
@@ -236,6 +237,7 @@ Program build_program(const hgnn_net_config* c) {
         h.wt = B.take((size_t)h.k * P.c2p * sizeof(float));
         h.wc = B.take((size_t)P.c2 * h.kp * sizeof(float));
         h.bc = B.take((size_t)P.c2 * sizeof(float));
+        h.wc3 = B.take((size_t)3 * P.c2 * bf3_ld(h.kp) * 2);
         max_da = std::max(max_da, (size_t)cap * h.kp);
         max_slab = std::max(max_slab, dw3_slab_floats(cap, P.c2, h.k));
         max_cap = std::max(max_cap, cap);
@@ -433,6 +435,14 @@ static int side_stream(hipStream_t main_s, SideStream** out) {
     return 0;
 }
 
+// The forward Conv1d-pair GEMM on bf16 MFMA with three-way split operands (gemm_bf3.hip: fp32 accuracy,
+// 2.7x fewer MFMA cycles); HGNN_FWD_BF3=0: the fp32 MFMA kernels (launch_gemm3_fwd).  Line-graph networks
+// with 2d % 64 == 0 (the kernel's 64-column tiles).
+static bool fwd_bf3(const Program& P) {
+    static const bool on = env_flag("HGNN_FWD_BF3", true);
+    return on && P.c2 % 64 == 0;
+}
+
 int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
                 const float* const* prm, float* const* run, void* ws, float* out, hipStream_t s, Timer* tm) {
     const Program& P = program_of(c);
@@ -457,6 +467,10 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
             it.k = h.k;
             it.kp = h.kp;
             it.ldt = P.c2p;
+            if (fwd_bf3(P)) {
+                it.wc3 = at<__bf16>(ws, h.wc3);
+                it.ldc3 = bf3_ld(h.kp);
+            }
             if (rt.n == REPACK_MAX || hi + 1 == P.halves.size()) {
                 tables.push_back(rt);
                 rt.n = 0;
@@ -527,10 +541,16 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
         ag.ldo = h.kp;
         TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
 
-        TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<float>(ws, h.wc), h.kp,
-                                             P.c2, at<float>(ws, h.bc), h.relu_from,
-                                             at<float>(ws, P.feats[h.out].y), P.c2,
-                                             c->training ? at<float>(ws, h.part) : nullptr, s, lg ? 1 : 0));
+        if (fwd_bf3(P))
+            TL(HGNN_K_GEMM_FWD, launch_gemm_bf3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<__bf16>(ws, h.wc3),
+                                                    (long long)P.c2 * bf3_ld(h.kp), bf3_ld(h.kp), P.c2,
+                                                    at<float>(ws, h.bc), h.relu_from, at<float>(ws, P.feats[h.out].y),
+                                                    P.c2, c->training ? at<float>(ws, h.part) : nullptr, s));
+        else
+            TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<float>(ws, h.wc), h.kp,
+                                                 P.c2, at<float>(ws, h.bc), h.relu_from,
+                                                 at<float>(ws, P.feats[h.out].y), P.c2,
+                                                 c->training ? at<float>(ws, h.part) : nullptr, s, lg ? 1 : 0));
 
         BnFwdArgs bf{};
         bf.part = at<float>(ws, h.part);
