@@ -477,120 +477,6 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
     }
 }
 
-// The whole BN backward of a small input (c <= 16 channels, <= 64 row tiles: the GNN_simple
-// layers of config 1) in ONE block: statistics over all rows, then dY and the per-tile column sums
-// of dY, separated by the block's barriers -- one launch instead of part4 + fin + apply4.  The same
-// formulas as those three kernels; the statistics are summed per thread in fp32 (a few rows each)
-// and across threads in fp64.
-constexpr int BN_SMALL_THREADS = 1024, BN_SMALL_TILES = 64, BN_SMALL_C = 16;
-
-__global__ void __launch_bounds__(BN_SMALL_THREADS) k_bn_bwd_small(BnBwdArgs a) {
-    const int total = *a.total_rows;
-    const int L = a.c >> 2, RG = BN_SMALL_THREADS / L;
-    const int lane = threadIdx.x % L, rg = threadIdx.x / L;
-    const float wv = *a.w;
-    float mu[4], isd[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        mu[i] = a.mean[4 * lane + i];
-        isd[i] = 1.0f / a.std[4 * lane + i];
-    }
-    // pass 1: the four per-channel sums of k_bn_bwd_part4
-    float4 st[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) st[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r = rg; r < total; r += RG) {
-        const long long i = (long long)r * a.c + 4 * lane;
-        float4 dz = ld4(a.dz + i), yv = ld4(a.y + i);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float h = (f4c(yv, k) - mu[k]) * isd[k];
-            const float d = f4c(dz, k);
-            const float g = wv * d;
-            f4c(st[0], k) += g;
-            f4c(st[1], k) = fmaf(g, h, f4c(st[1], k));
-            f4c(st[2], k) = fmaf(d, h, f4c(st[2], k));
-            f4c(st[3], k) += d;
-        }
-    }
-    // fp64 reduction: over the lanes of a wave holding the same channels (threads t, t + L, ...),
-    // then over the 16 waves
-    __shared__ double wred[BN_SMALL_THREADS / 64][BN_SMALL_C][4];
-    const int w = threadIdx.x >> 6, wl = threadIdx.x & 63;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            double v = (double)f4c(st[j], k);
-            for (int o = 32; o >= L; o >>= 1) v += __shfl_xor(v, o, 64);
-            if (wl < L) wred[w][4 * wl + k][j] = v;
-        }
-    __syncthreads();
-    __shared__ float sums[BN_SMALL_C][4];
-    if (threadIdx.x < a.c * 4) {
-        const int ch = threadIdx.x >> 2, j = threadIdx.x & 3;
-        double t = 0.0;
-        for (int q = 0; q < BN_SMALL_THREADS / 64; ++q) t += wred[q][ch][j];
-        sums[ch][j] = (float)t;
-        a.sums[ch * 4 + j] = (float)t;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t1 = 0.0, t2 = 0.0;
-        for (int ch = 0; ch < a.c; ++ch) {
-            t1 += (double)sums[ch][2];
-            t2 += (double)sums[ch][3];
-        }
-        *a.dw = (float)t1;
-        *a.db = (float)t2;
-    }
-    // pass 2: dY (k_bn_bwd_apply4) and the per-64-row-tile column sums of dY; thread -> (tile slot,
-    // row of the tile, lane), 64 * L threads per tile
-    const float inv_n = total > 0 ? 1.0f / (float)total : 0.f;
-    float m1[4], m2[4];
-    bool relu[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int ch = 4 * lane + i;
-        m1[i] = sums[ch][0] * inv_n;
-        m2[i] = sums[ch][1] * inv_n;
-        relu[i] = ch >= a.relu_from;
-    }
-    const int per_tile = 64 * L, slots = BN_SMALL_THREADS / per_tile;
-    const int slot = threadIdx.x / per_tile, row = (threadIdx.x % per_tile) / L;
-    __shared__ float4 cred[BN_SMALL_THREADS];
-    const int tiles = ceil_div(total, 64);
-    for (int t0 = 0; t0 < tiles; t0 += slots) {
-        const int tile = t0 + slot, r = tile * 64 + row;
-        float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (tile < tiles && r < total) {
-            const long long i = (long long)r * a.c + 4 * lane;
-            float4 yv = ld4(a.y + i), dz = ld4(a.dz + i);
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                f4c(d, k) = bn_bwd_dy_inv(f4c(yv, k), f4c(dz, k), mu[k], isd[k], wv, m1[k], m2[k], a.training != 0,
-                                          relu[k]);
-            *reinterpret_cast<float4*>(a.dy + i) = d;
-        }
-        if (a.dbpart) {
-            cred[threadIdx.x] = d;
-            __syncthreads();
-            if (threadIdx.x < slots * a.c) {
-                const int sl = threadIdx.x / a.c, ch = threadIdx.x % a.c, tl = t0 + sl;
-                if (tl < tiles) {
-                    float acc = 0.f;
-                    for (int q = 0; q < 64; ++q) {
-                        float4 v = cred[sl * per_tile + q * L + (ch >> 2)];
-                        acc += f4c(v, ch & 3);
-                    }
-                    a.dbpart[(long long)tl * a.c + ch] = acc;
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
-
 // ---- Two-launch BN backward (c = 4L, L in {16, 32, 64}: 2d = 64 / 128 / 256).  The three-launch
 // form above spends ~6 us of a ~20 us half on k_bn_bwd_fin, a launch that only sums the tile
 // partials.  Here the statistics pass uses 256-row tiles (1024 threads, 8-16 rows in flight per
@@ -1011,24 +897,14 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     // a padded dY stride is written by the scalar apply only
     const bool v4 = bn_vec4(a) && (a.ldy == 0 || a.ldy == a.c);
     // (c / 4 a power of two: the per-wave shuffle reduction pairs the lanes of one channel group)
-    // HGNN_BN_SMALL=1: the single-block k_bn_bwd_small instead of the two-launch narrow form
-    static const bool one_block = [] {
-        const char* e = getenv("HGNN_BN_SMALL");
-        return e && e[0] == '1';
-    }();
     // the two-launch forms sum every statistics partial in each apply block's prologue (O(tiles^2 C)
     // L2 reads): only up to 192 row tiles of capacity (49 K rows; config 2's edge half is 140 with 91
     // live); larger inputs take part4 + fin + apply4
     const bool few = ceil_div(a.cap_rows, BN2_ROWS) <= 192;
-    if (apply && v4 && !one_block && bn2_enabled() && few && tiles > 0 && (a.c == 4 || a.c == 8 || a.c == 16)) {
+    if (apply && v4 && bn2_enabled() && few && tiles > 0 && (a.c == 4 || a.c == 8 || a.c == 16)) {
         if (a.c == 4) bn2s_launch<1>(a, s);
         else if (a.c == 8) bn2s_launch<2>(a, s);
         else bn2s_launch<4>(a, s);
-        HGNN_LAUNCH_CHECK();
-        return 0;
-    }
-    if (apply && v4 && (a.c == 4 || a.c == 8 || a.c == 16) && tiles <= BN_SMALL_TILES) {
-        hipLaunchKernelGGL(k_bn_bwd_small, dim3(1), dim3(BN_SMALL_THREADS), 0, s, a);
         HGNN_LAUNCH_CHECK();
         return 0;
     }

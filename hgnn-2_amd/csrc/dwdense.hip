@@ -115,16 +115,15 @@ __device__ __forceinline__ void dw_stage(const DwDenseArgs& a, int b, int off, i
 // MAXI = (n-tile, m-tile, slice) items per wave kept in registers: sized to the
 // graph so the accumulators do not cap occupancy (5 x 16 AGPRs at Nmax <= 32,
 // where only 3 items exist, left one wave per SIMD)
-// JSPLIT: one block per (graph, slice) -- blockIdx.y is the slice; the block stages only that
-// slice's G rows (half the LDS, a third of the loads per block, 3x the blocks).  One block per
-// graph left ~18 us per launch at config 2 for ~4 us of traffic: the per-block chain of staging,
-// MFMA and read-modify-write was the whole kernel.
-template <int FC, int MAXI, bool JSPLIT>
+// (A per-(graph, slice) block split -- a third of the loads per block, 3x the blocks -- was measured
+// at 350 K vs 366 K graphs/s: on the side stream the extra blocks crowd the main stream's backward
+// more than the shorter kernel saves; retired in round 4.)
+template <int FC, int MAXI>
 __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int b = blockIdx.x;
     const int nmax = a.nmax, F = a.f;
-    const int J = JSPLIT ? 1 : a.jt, j0 = JSPLIT ? (int)blockIdx.y : 0, JA = a.jt;
+    const int J = a.jt, j0 = 0, JA = a.jt;
     const int npad = (nmax + 31) / 32 * 32;
     const int tiles = npad / 32;
     const int nitems = tiles * tiles * J;
@@ -146,7 +145,7 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
 
     float* dWb = a.dW + (long long)b * nmax * nmax * JA;
     // block-uniform passes over the items; gridDim.y blocks of a graph share them
-    const int ystart = JSPLIT ? 0 : (int)blockIdx.y, ystep = JSPLIT ? 1 : (int)gridDim.y;
+    const int ystart = blockIdx.y, ystep = gridDim.y;
     for (int base = ystart * 4 * MAXI; base < nitems; base += ystep * 4 * MAXI) {
     f32x16 acc[MAXI];
 #pragma unroll
@@ -223,37 +222,26 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     }
 }
 
-template <int FC, int MAXI, bool JS>
+template <int FC, int MAXI>
 static void allow_lds(size_t lds) {
     // dynamic LDS beyond 64 KB must be allowed per kernel (gfx950: 160 KB per CU)
     // (the whole 160 KB once: a first call with a smaller size must not cap a later, larger one)
     static bool done = false;
     if (!done && lds > 64 * 1024) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_dense<FC, MAXI, JS>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_dense<FC, MAXI>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         done = true;
     }
 }
 
-template <int FC, bool JS>
+template <int FC>
 static void launch_fc(const DwDenseArgs& a, int maxi, int gy, size_t lds, hipStream_t s) {
-    allow_lds<FC, 1, JS>(lds);
-    allow_lds<FC, 3, JS>(lds);
-    allow_lds<FC, 5, JS>(lds);
-    if (maxi <= 1) hipLaunchKernelGGL((k_dw_dense<FC, 1, JS>), dim3(a.bs, gy), dim3(256), lds, s, a);
-    else if (maxi <= 3) hipLaunchKernelGGL((k_dw_dense<FC, 3, JS>), dim3(a.bs, gy), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL((k_dw_dense<FC, 5, JS>), dim3(a.bs, gy), dim3(256), lds, s, a);
-}
-
-// HGNN_DW_JSPLIT=1: one block per (graph, slice).  Measured on the box (alternating bench runs):
-// 350 K vs 366 K graphs/s with one block per graph -- this kernel runs on the side stream, and 3x
-// the blocks crowd the main stream's backward more than the shorter kernel saves.  Off by default.
-static bool jsplit_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("HGNN_DW_JSPLIT");
-        return e && e[0] == '1';
-    }();
-    return on;
+    allow_lds<FC, 1>(lds);
+    allow_lds<FC, 3>(lds);
+    allow_lds<FC, 5>(lds);
+    if (maxi <= 1) hipLaunchKernelGGL((k_dw_dense<FC, 1>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    else if (maxi <= 3) hipLaunchKernelGGL((k_dw_dense<FC, 3>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((k_dw_dense<FC, 5>), dim3(a.bs, gy), dim3(256), lds, s, a);
 }
 
 // Narrow inputs (F <= 16: layer 0's node features, the GNN_simple layers of config 1): the outer
@@ -317,10 +305,9 @@ int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
     // one F chunk when it fits (F = 2d = 128 at config 2): 19.1 -> 18.3 us per launch
     int fc = npad <= 32 ? (a.f > 64 ? 128 : 64) : (npad <= 64 ? 32 : 16);
     const int tiles = npad / 32;
-    // large batches: one block per (graph, slice); few graphs (cfg1: 32): the items' passes of a
-    // graph spread over blocks instead, so the grid is not a handful of long blocks
-    const bool js = jsplit_enabled() && a.bs >= 256;
-    const int J = js ? 1 : a.jt;
+    // few graphs (cfg1: 32): the items' passes of a graph spread over blocks, so the grid is not a
+    // handful of long blocks
+    const int J = a.jt;
     auto lds_of = [&](int c) {
         return sizeof(float) * ((size_t)npad * ((J * c + 1) + (c + 1)) + (size_t)J * c + 3 * c);
     };
@@ -330,23 +317,16 @@ int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
     const size_t lds = lds_of(fc);
     if (lds > 160 * 1024) return HGNN_ERR_UNSUPPORTED;
     const int nitems = tiles * tiles * J;
-    int maxi = ceil_div(nitems, 4), gy = js ? a.jt : 1;
-    if (!js && a.bs < 256 && nitems > 4) {
+    int maxi = ceil_div(nitems, 4), gy = 1;
+    if (a.bs < 256 && nitems > 4) {
         maxi = 1;
         gy = ceil_div(nitems, 4);
     }
-#define HGNN_DW_FC(JS)                                         \
-    if (fc == 128) launch_fc<128, JS>(a, maxi, gy, lds, s);    \
-    else if (fc == 64) launch_fc<64, JS>(a, maxi, gy, lds, s); \
-    else if (fc == 32) launch_fc<32, JS>(a, maxi, gy, lds, s); \
-    else if (fc == 16) launch_fc<16, JS>(a, maxi, gy, lds, s); \
-    else launch_fc<8, JS>(a, maxi, gy, lds, s);
-    if (js) {
-        HGNN_DW_FC(true)
-    } else {
-        HGNN_DW_FC(false)
-    }
-#undef HGNN_DW_FC
+    if (fc == 128) launch_fc<128>(a, maxi, gy, lds, s);
+    else if (fc == 64) launch_fc<64>(a, maxi, gy, lds, s);
+    else if (fc == 32) launch_fc<32>(a, maxi, gy, lds, s);
+    else if (fc == 16) launch_fc<16>(a, maxi, gy, lds, s);
+    else launch_fc<8>(a, maxi, gy, lds, s);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of an env switch on one box: alternating bench runs (no CPU baseline).
-# usage: VAR=HGNN_FUSED_DA A=0 B=1 REPS=3 bash tools/ab.sh
+# usage: VAR=HGNN_FWD_BF3 A=0 B=1 REPS=3 bash tools/ab.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
