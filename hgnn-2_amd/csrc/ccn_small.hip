@@ -691,7 +691,10 @@ using namespace hgnn;
 
 extern "C" {
 
-int hgnn_ccn_small_supported(const hgnn_ccn_config* cfg) { return cs_ok(cfg) ? 1 : 0; }
+int hgnn_ccn_small_supported(const hgnn_ccn_config* cfg) {
+    if (cfg && cfg->order == 2) return ccn2_small_ok(cfg) ? 1 : 0;
+    return cs_ok(cfg) ? 1 : 0;
+}
 
 int hgnn_host_word_alloc(void** host_ptr, void** dev_ptr) {
     if (!host_ptr || !dev_ptr) return HGNN_ERR_ARG;
@@ -709,6 +712,7 @@ int hgnn_host_word_alloc(void** host_ptr, void** dev_ptr) {
 }
 
 size_t hgnn_ccn_small_workspace_bytes(const hgnn_ccn_config* cfg) {
+    if (cfg && cfg->order == 2) return ccn2_small_workspace_bytes(cfg);
     if (!cs_ok(cfg)) return 0;
     const int nf = cfg->f_in + cfg->layers * cfg->hidden;
     return (4 * (size_t)cfg->bs * nf + 255) / 256 * 256 + (cfg->bs > 1 ? 4 * (size_t)cfg->bs * cs_ptot(cfg) : 0);
@@ -717,9 +721,13 @@ size_t hgnn_ccn_small_workspace_bytes(const hgnn_ccn_config* cfg) {
 int hgnn_ccn_small_forward(const hgnn_ccn_config* cfg, const float* d_X, const float* d_adj,
                            const int64_t* d_n_batch, const float* const* params, void* workspace, int32_t* d_err,
                            int32_t tag, float* d_out, void* stream) {
-    if (!cs_ok(cfg)) return HGNN_ERR_UNSUPPORTED;
+    const bool two = cfg && cfg->order == 2;
+    if (two ? !ccn2_small_ok(cfg) : !cs_ok(cfg)) return HGNN_ERR_UNSUPPORTED;
     if (!d_X || !d_adj || !params || !workspace || !d_err || !d_out || tag <= 0 || tag >= (1 << 23))
         return HGNN_ERR_ARG;
+    if (two)
+        return ccn2_small_forward(cfg, d_X, d_adj, d_n_batch, params, workspace, d_err, tag, d_out,
+                                  (hipStream_t)stream);
     CsArgs a = cs_args(cfg, d_X, d_adj, d_n_batch, params, workspace);
     a.out = d_out;
     a.err = d_err;
@@ -751,8 +759,12 @@ int hgnn_ccn_small_forward(const hgnn_ccn_config* cfg, const float* d_X, const f
 int hgnn_ccn_small_backward(const hgnn_ccn_config* cfg, const float* d_X, const float* d_adj,
                             const int64_t* d_n_batch, const float* const* params, void* workspace,
                             const float* d_dout, float* const* grads, float* d_dX, void* stream) {
-    if (!cs_ok(cfg)) return HGNN_ERR_UNSUPPORTED;
+    const bool two = cfg && cfg->order == 2;
+    if (two ? !ccn2_small_ok(cfg) : !cs_ok(cfg)) return HGNN_ERR_UNSUPPORTED;
     if (!d_X || !d_adj || !params || !workspace || !d_dout || !grads || !d_dX) return HGNN_ERR_ARG;
+    if (two)
+        return ccn2_small_backward(cfg, d_X, d_adj, d_n_batch, params, workspace, d_dout, grads, d_dX,
+                                   (hipStream_t)stream);
     hipStream_t s = (hipStream_t)stream;
     CsArgs a = cs_args(cfg, d_X, d_adj, d_n_batch, params, workspace);
     a.dout = d_dout;

@@ -388,4 +388,13 @@ bool readout_row_fits(const ReadoutAggArgs& ra, const DwDenseArgs* dw);
 // dW of the readout layer's graph_oper: dW[b, n, m, j] (+)= sum_f R_b[j F + f] X[m, f], every n
 int launch_dw_readout(const DwDenseArgs& a, hipStream_t s);
 
+// CCN-2D one-workgroup-per-graph path (ccn2_small.hip) behind hgnn_ccn_small_* for order 2
+bool ccn2_small_ok(const hgnn_ccn_config* c);
+size_t ccn2_small_workspace_bytes(const hgnn_ccn_config* c);
+int ccn2_small_forward(const hgnn_ccn_config* c, const float* X, const float* adj, const int64_t* nb,
+                       const float* const* params, void* ws, int32_t* err, int32_t tag, float* out, hipStream_t s);
+int ccn2_small_backward(const hgnn_ccn_config* c, const float* X, const float* adj, const int64_t* nb,
+                        const float* const* params, void* ws, const float* dout, float* const* grads, float* dX,
+                        hipStream_t s);
+
 }  // namespace hgnn

@@ -27,9 +27,9 @@ from . import _lib as L
 from .net import (_capturing, _require_cuda, _f32, _i64, _raise_bits, check_errors, register_check, strict,
                   watch_word)
 
-# CCN_1D on graphs of <= 64 nodes through the one-workgroup-per-graph kernels (csrc/ccn_small.hip):
-# no plan, no workspace sizing, 1 + 1 dispatches per call for one graph.  HGNN_CCN_SMALL=0 (or setting
-# this to False) keeps every call on the general path.
+# CCN_1D on graphs of <= 64 nodes and CCN_2D on graphs of <= 32 nodes through the one-workgroup-per-graph
+# kernels (csrc/ccn_small.hip, csrc/ccn2_small.hip): no plan, no workspace sizing, 1 + 1 dispatches per call
+# for one graph.  HGNN_CCN_SMALL=0 (or setting this to False) keeps every call on the general path.
 SMALL = os.environ.get("HGNN_CCN_SMALL", "1") != "0"
 
 CCN_MAX_DEGREE = {1: 1024, 2: 256}  # csrc/ccn.hip CCN1_MAXD, CCN_BIGD (by order)
@@ -241,10 +241,11 @@ def run_ccn(spec, params, X, adj, n_batch, plan=None):
     """Batched CCN forward: X (bs,nmax,f), adj (bs,nmax,nmax), n_batch (bs,) -> (bs, n_out).
     plan: a CcnPlan of this adj / n_batch (else the plan is built here: without a host sync for
     small shapes, ASYNC_PLAN_BOUND; with one otherwise).  n_batch None: every graph has nmax nodes.
-    CCN_1D batches of <= 64-node graphs take the small-graph kernels (SMALL; a plan is then unused)."""
+    CCN_1D batches of <= 64-node graphs and CCN_2D batches of <= 32-node graphs (f_in <= 8, hidden <= 2) take
+    the small-graph kernels (SMALL; a plan is then unused)."""
     check_errors(block=False)
     # the small-graph kernels need no plan: a batch planned for capture (CcnPlan) takes them too
-    if SMALL and spec.order == 1 and X.dim() == 3:
+    if SMALL and X.dim() == 3:
         small = spec.small(X.shape[0], X.shape[1])
         if small is not None:
             _require_cuda([X, adj, n_batch, *params], "CCN")

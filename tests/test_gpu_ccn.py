@@ -530,3 +530,164 @@ def test_ccn1_small_graph_path_inplace_input_change_raises():
         Xi.add_(1.0)
     with pytest.raises(RuntimeError, match="modified by an inplace operation"):
         out.sum().backward()
+
+
+def _qm9_2d(bs, seed, f=5):
+    import hgnn_amd.datagen as dg
+    return [(X[:, :f] if X.shape[1] >= f else torch.cat([X, torch.rand(X.shape[0], f - X.shape[1])], 1),
+             A + torch.eye(A.shape[0]), t) for X, A, t in dg.qm9_shape_dataset(bs, seed=seed)]
+
+
+@pytest.mark.parametrize("f,h,layers,bs", [(5, 2, 2, 1), (5, 2, 2, 64), (7, 1, 3, 16), (3, 2, 1, 5)])
+def test_ccn2_small_graph_path_equals_general_path(f, h, layers, bs):
+    """The one-workgroup-per-graph CCN-2D kernels (csrc/ccn2_small.hip) against the general path on the
+    same batch: outputs, dX and the weight gradients bit-identical (the general kernels' arithmetic in the
+    same order, the batch's parameter partials reduced in k_ccn_param_reduce's order), and against the
+    closed-form fp64 oracle (oracle/ref_ccn.py ccn2_forward_closed)."""
+    from models.compnets.model_ccn import CCN_2D
+    from oracle import ref_ccn as RC
+    graphs = _qm9_2d(bs, 700 + bs, f)
+    net = CCN_2D(f, 2, h, layers)
+    fu.det_init(net, 93 + layers)
+    p64 = {n: v.detach().double().clone().requires_grad_(True) for n, v in net.named_parameters()}
+    net = net.cuda()
+    X, A, nb = _pad(graphs, "cuda")
+    assert net._spec().small(X.shape[0], X.shape[1]) is not None
+    w = torch.randn(bs, 2, generator=torch.Generator().manual_seed(bs)).cuda()
+    os_, dxs, gs = _run_path(True, net, X, A, nb, w)
+    og, dxg, gg = _run_path(False, net, X, A, nb, w)
+    assert torch.equal(os_, og), f"outputs differ: {(os_ - og).abs().max().item():.3g}"
+    assert torch.equal(dxs, dxg), f"dX differs: {(dxs - dxg).abs().max().item():.3g}"
+    for n in gg:
+        assert torch.equal(gs[n], gg[n]), f"grad {n} differs: {(gs[n] - gg[n]).abs().max().item():.3g}"
+    for b, (x, a, _) in enumerate(graphs[:6]):
+        xr = x.double().requires_grad_(True)
+        ref = RC.ccn2_forward_closed(p64, xr, a.double(), layers)
+        _close(os_[b], ref, f"small path graph {b}")
+        (ref * w[b].double().cpu()).sum().backward()
+        _grad_close(dxs[b, :x.shape[0]], xr.grad, f"small path dX graph {b}")
+        assert dxs[b, x.shape[0]:].abs().max().item() == 0.0 if x.shape[0] < X.shape[1] else True
+
+
+def test_ccn2_small_graph_path_fixtures(golden):
+    """The reference's CCN_2D fixtures (tests/golden/ccn.npz, generated from the reference) through the
+    small path, per graph as scripts/train_ccn.py calls it, and bit-identical to the general path."""
+    import hgnn_amd.ccn as HC
+    z = golden("ccn")
+    seen = 0
+    for k, (X, adj, t) in enumerate(ccn_graphs(z)):
+        if f"2d_out_{k}" not in z:
+            continue
+        net, _ = ccn_params("2d", k)
+        net = net.cuda()
+        assert net._spec().small(1, X.shape[0]) is not None
+        res = {}
+        for small in (True, False):
+            old = HC.SMALL
+            HC.SMALL = small
+            try:
+                net.zero_grad(set_to_none=True)
+                Xr = X.cuda().requires_grad_(True)
+                out = net(Xr, adj.cuda())
+                torch.nn.MSELoss()(out, t[0].view(1).cuda()).backward()
+                res[small] = (out.detach().cpu(), Xr.grad.cpu(),
+                              {n: p.grad.detach().cpu().clone() for n, p in net.named_parameters()})
+            finally:
+                HC.SMALL = old
+        out, dx, gr = res[True]
+        _close(out, z[f"2d_out_{k}"], f"2d out {k}")
+        _grad_close(dx, z[f"2d_dX_{k}"], f"2d dX {k}")
+        for n, g in gr.items():
+            _grad_close(g, z[f"2d_grad_{k}.{n}"], f"2d grad {k} {n}")
+        assert torch.equal(out, res[False][0]) and torch.equal(dx, res[False][1]), k
+        for n in gr:
+            assert torch.equal(gr[n], res[False][2][n]), (k, n)
+        seen += 1
+    assert seen > 0
+
+
+def test_ccn2_small_graph_path_complete_graph_nmax32():
+    """The size bound of the small path: a complete 32-node graph (every receptive field of degree 32, the
+    position maps and P at their largest) equals the general path and the closed-form oracle."""
+    from models.compnets.model_ccn import CCN_2D
+    from oracle import ref_ccn as RC
+    n = 32
+    g = torch.Generator().manual_seed(32)
+    x = torch.rand(n, 5, generator=g)
+    a = torch.ones(n, n)
+    net = CCN_2D(5, 1, 2, 2)
+    fu.det_init(net, 32)
+    p64 = {k: v.detach().double().clone().requires_grad_(True) for k, v in net.named_parameters()}
+    net = net.cuda()
+    X, A, nb = x.view(1, n, 5).cuda(), a.view(1, n, n).cuda(), torch.tensor([n]).cuda()
+    assert net._spec().small(1, n) is not None
+    w = torch.ones(1, 1).cuda()
+    os_, dxs, gs = _run_path(True, net, X, A, nb, w)
+    og, dxg, gg = _run_path(False, net, X, A, nb, w)
+    assert torch.equal(os_, og) and torch.equal(dxs, dxg)
+    for k in gg:
+        assert torch.equal(gs[k], gg[k]), k
+    xr = x.double().requires_grad_(True)
+    ref = RC.ccn2_forward_closed(p64, xr, a.double(), 2)
+    _close(os_[0], ref, "complete graph")
+    ref.sum().backward()
+    _grad_close(dxs[0], xr.grad, "complete graph dX")
+
+
+def test_ccn2_small_graph_path_ragged_and_validation():
+    """Ragged batch (single node, empty slot, QM9 graph) equals the general path, the empty slot reads
+    fc.bias; the small path reports missing self loops / asymmetric patterns / n_b > nmax."""
+    from hgnn_amd.net import check_errors
+    from models.compnets.model_ccn import CCN_2D
+    (xq, aq, _), = _qm9_2d(1, 19)
+    n = xq.shape[0]
+    X = torch.zeros(3, n, 5)
+    A = torch.zeros(3, n, n)
+    X[0, :1] = torch.randn(1, 5)
+    A[0, 0, 0] = 1.0
+    X[2, :n] = xq
+    A[2, :n, :n] = aq
+    nb = torch.tensor([1, 0, n], dtype=torch.int64)
+    net = CCN_2D(5, 1, 2, 2)
+    fu.det_init(net, 919)
+    net = net.cuda()
+    X, A, nb = X.cuda(), A.cuda(), nb.cuda()
+    w = torch.ones(3, 1).cuda()
+    os_, dxs, gs = _run_path(True, net, X, A, nb, w)
+    og, dxg, gg = _run_path(False, net, X, A, nb, w)
+    assert torch.equal(os_, og) and torch.equal(dxs, dxg)
+    for k in gg:
+        assert torch.equal(gs[k], gg[k]), k
+    assert torch.equal(os_[1], net.fc.bias.detach().cpu())
+    assert dxs[1].abs().max().item() == 0.0 and dxs[0, 1:].abs().max().item() == 0.0
+    A1 = torch.eye(4)
+    A1[0, 1] = 1.0  # 1 does not list 0
+    with pytest.raises(RuntimeError, match="not symmetric"):
+        net(torch.randn(4, 5).cuda(), A1.cuda())
+        check_errors()
+    A2 = torch.ones(4, 4)
+    A2[2, 2] = 0.0
+    with pytest.raises(RuntimeError, match="self loop"):
+        net(torch.randn(4, 5).cuda(), A2.cuda())
+        check_errors()
+    with pytest.raises(RuntimeError, match="negative count"):
+        net.forward_batch(torch.randn(1, 4, 5).cuda(), torch.eye(4).unsqueeze(0).cuda(), torch.tensor([5]).cuda())
+        check_errors()
+    net(torch.randn(4, 5).cuda(), torch.eye(4).cuda())
+    check_errors()
+
+
+def test_ccn2_small_graph_path_inplace_input_change_raises():
+    """The small path's backward re-plans from adj and reads X: both saved through autograd, so an in-place
+    change between forward and backward raises the version error."""
+    from models.compnets.model_ccn import CCN_2D
+    (x, a, _), = _qm9_2d(1, 23)
+    net = CCN_2D(5, 1, 2, 2).cuda()
+    X = x.cuda().requires_grad_(True)
+    Xi = X * 1.0
+    out = net(Xi, a.cuda())
+    assert net._spec().small(1, x.shape[0]) is not None
+    with torch.no_grad():
+        Xi.add_(1.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        out.sum().backward()

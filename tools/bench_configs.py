@@ -18,6 +18,9 @@ forward" roofline):
   cfg4   GNN_lg d=128 order 2 L=5, 512 QM9-shape graphs (one GPU's share of 4096)
   cfg5   CCN_2D(5, 1, 2, 2), 64 SBM N=200 graphs (A + I)
   cfg5_pergraph  the same 64 graphs one at a time (forward, MSE, backward, Adamax step per graph)
+  cfg5q / cfg5qg  CCN_2D(5, 1, 2, 2), 256 QM9-shape graphs batched (eager / replayed from a HIP graph)
+  cfg5q_pergraph  the same 256 graphs one at a time (the reference driver's CCN_2D call pattern)
+  (HGNN_CCN_SMALL=0 puts the QM9-size CCN batches on the general path for an A/B)
 
 Prints one JSON line per configuration.  Usage:
   python tools/bench_configs.py [--only cfg3,cfg5] [--steps 20] [--warmup 5]
@@ -198,7 +201,7 @@ def run_ccn(name, order, graphs, desc, steps, warmup, graph=False):
     # graph mode: the batch is planned once, outside the capture -- unless the small-graph CCN-1D
     # kernels take it (QM9-size graphs), which need no plan
     import hgnn_amd.ccn as HC
-    small = order == 1 and HC.SMALL and net._spec().small(X.shape[0], X.shape[1]) is not None
+    small = HC.SMALL and net._spec().small(X.shape[0], X.shape[1]) is not None
     plan = net.plan(A, nb) if graph and not small else None
 
     def step():
@@ -309,6 +312,14 @@ def main():
             "cfg5_pergraph", 2, dg.sbm_dataset(64, n=200, seed=0),
             "CCN_2D(5,1,2,2) per graph as scripts/train_ccn.py: net(X, A+I), MSE, backward, Adamax step; "
             "64 SBM N=200 graphs", 2, 1),
+        "cfg5q_pergraph": lambda: run_ccn_pergraph(
+            "cfg5q_pergraph", 2, dg.qm9_shape_dataset(256, seed=0),
+            "CCN_2D(5,1,2,2) per graph as scripts/train_ccn.py: net(X, A+I), MSE, backward, Adamax step; "
+            "256 QM9-shape graphs", max(2, a.steps // 5), 1),
+        "cfg5q": lambda: run_ccn("cfg5q", 2, dg.qm9_shape_dataset(256, seed=0),
+                                 "CCN_2D(5,1,2,2) fwd+bwd, 256 QM9-shape graphs", a.steps, a.warmup),
+        "cfg5qg": lambda: run_ccn("cfg5q", 2, dg.qm9_shape_dataset(256, seed=0),
+                                  "CCN_2D(5,1,2,2) fwd+bwd, 256 QM9-shape graphs", a.steps, a.warmup, graph=True),
         "cfg5": lambda: run_ccn("cfg5", 2, dg.sbm_dataset(64, n=200, seed=0),
                                 "CCN_2D(5,1,2,2) fwd+bwd, 64 SBM N=200 graphs", max(3, a.steps // 4),
                                 max(1, a.warmup // 2)),
