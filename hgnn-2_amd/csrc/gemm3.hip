@@ -50,9 +50,42 @@ __device__ unsigned g_clock_n;
             g_clock[_i].kid = (KID_);                                       \
         }                                                                   \
     }
+// Phase stamps of the dW GEMM (same diagnostic build, tools/dw_phases.py): thread 0 of every block records
+// s_memrealtime (100 MHz, chip-wide) at entry, loop start, loop end and exit, plus the CU it ran on (HW_ID,
+// XCC_ID), so a launch's span splits into block start-up, main loop, epilogue and late (second-round or
+// CU-waiting) blocks.  Stored with vector stores from thread 0.
+constexpr unsigned PHASE_SLOTS = 1u << 17;
+struct PhaseStamp {
+    unsigned long long t[4];
+    unsigned hw, xcc, blk, rows;
+};
+__device__ PhaseStamp g_phase[PHASE_SLOTS];
+__device__ unsigned g_phase_n;
+#define PH_DECL() unsigned long long _ph[4] = {0ull, 0ull, 0ull, 0ull};
+#define PH_MARK(I_)                                                     \
+    if (threadIdx.x == 0) _ph[I_] = __builtin_amdgcn_s_memrealtime();
+#define PH_FLUSH(ROWS_)                                                                               \
+    if (threadIdx.x == 0) {                                                                           \
+        _ph[3] = __builtin_amdgcn_s_memrealtime();                                                    \
+        const unsigned _i = atomicAdd(&g_phase_n, 1u);                                                \
+        if (_i < PHASE_SLOTS) {                                                                       \
+            PhaseStamp& _s = g_phase[_i];                                                             \
+            _s.t[0] = _ph[0];                                                                         \
+            _s.t[1] = _ph[1];                                                                         \
+            _s.t[2] = _ph[2];                                                                         \
+            _s.t[3] = _ph[3];                                                                         \
+            _s.hw = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                              \
+            _s.xcc = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);                            \
+            _s.blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);                  \
+            _s.rows = (unsigned)(ROWS_);                                                              \
+        }                                                                                             \
+    }
 #else
 #define CLK_BEGIN()
 #define CLK_END(KID_)
+#define PH_DECL()
+#define PH_MARK(I_)
+#define PH_FLUSH(ROWS_)
 #endif
 
 namespace {
@@ -324,6 +357,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
     static_assert(AF4 * 4 * NT == BM * BK && BF4 * 4 * NT == BN * BK, "staging must cover the tile");
     __shared__ __attribute__((aligned(16))) float As[2][BK * PA];
     __shared__ __attribute__((aligned(16))) float Bs[2][BK * PB];
+    PH_DECL()
+    PH_MARK(0)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv / WGN, wn = wv % WGN;
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
@@ -342,7 +377,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
     const int R = *r_valid;
     const int kchunk = dw3_kc(R, nz);
     const int kbeg = bz * kchunk, kend = min(R, kbeg + kchunk);
-    if (kbeg >= kend) return;  // the reduce only sums the chunks that hold rows
+    if (kbeg >= kend) {  // the reduce only sums the chunks that hold rows
+        PH_FLUSH(0)
+        return;
+    }
     float4 ra[AF4], rb[BF4];
     auto load = [&](int k0) {
 #pragma unroll
@@ -384,6 +422,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
     const int nt = ceil_div(kend - kbeg, BK);
     const int h = lane >> 5, l31 = lane & 31;
     CLK_BEGIN()
+    PH_MARK(1)
     load(kbeg);
     store(0);
     __syncthreads();
@@ -419,6 +458,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
         __syncthreads();
     }
     CLK_END(2u)
+    PH_MARK(2)
     float* out = slabs + (long long)bz * M * N;
 #pragma unroll
     for (int i = 0; i < AM; ++i)
@@ -431,6 +471,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm3_tn(const float* __rest
                 if (gm < M && gn < N) out[(long long)gm * N + gn] = acc[i][j][r];
             }
         }
+    PH_FLUSH(kend - kbeg)
 }
 
 // ---- dA on v_mfma_f32_16x16x4_f32 with LDS-DMA staging (tools/gemm4_lab.hip, "g5")
@@ -827,6 +868,21 @@ extern "C" int hgnn_diag_clock_read(void* out, int max_n, int reset) {
     if (reset) {
         const unsigned z = 0;
         if (hipMemcpyToSymbol(HIP_SYMBOL(hgnn::g_clock_n), &z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return (int)k;
+}
+
+// Diagnostic build: the dW GEMM's phase stamps (48 B each), as above.
+extern "C" int hgnn_diag_phase_read(void* out, int max_n, int reset) {
+    unsigned n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(hgnn::g_phase_n), sizeof(n)) != hipSuccess) return -1;
+    if (n > hgnn::PHASE_SLOTS) n = hgnn::PHASE_SLOTS;
+    const unsigned k = n < (unsigned)max_n ? n : (unsigned)max_n;
+    if (k && hipMemcpyFromSymbol(out, HIP_SYMBOL(hgnn::g_phase), k * sizeof(hgnn::PhaseStamp)) != hipSuccess)
+        return -1;
+    if (reset) {
+        const unsigned z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hgnn::g_phase_n), &z, sizeof(z)) != hipSuccess) return -1;
     }
     return (int)k;
 }

@@ -316,14 +316,17 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                       void* plan_ws, long long max_sum_d2, void* workspace, const float* d_dout,
                       float* const* grads, float* d_dX, void* stream);
 
-/* CCN_1D on small graphs (nmax <= 64, f_in and hidden <= 8): one workgroup per graph builds the
- * receptive fields, runs every level and the readout in LDS -- no plan, no host sync, one dispatch
- * forward, one backward (+ one reduction over the graphs when bs > 1).  The per-graph drop-in call
- * of scripts/train_ccn.py:31-73 (net(X, A + I) per graph) and QM9-size batches.  Same layouts and
- * results as hgnn_ccn_forward / _backward (outputs and dX in the same fp32 order; weight gradients
- * summed in a different order).  d_n_batch may be NULL (every graph has nmax nodes).
- * supported: 1 if cfg fits (the LDS of the backward, 4 nmax^2 (hidden L + 2 max(f_in, hidden) +
- * 2 hidden) + 8 KB, within 160 KB), else 0 (use the general path).
+/* CCN on small graphs -- order 1 (CCN_1D): nmax <= 64, f_in and hidden <= 8; order 2 (CCN_2D):
+ * nmax <= 32, f_in <= 8, hidden <= 2 (the reference's CCN_2D hidden size).  One workgroup per graph
+ * builds the receptive fields, runs every level and the readout -- no plan, no host sync, one
+ * dispatch forward, one backward (+ one reduction over the graphs when bs > 1).  The per-graph
+ * drop-in call of scripts/train_ccn.py:31-73 (net(X, A + I) per graph) and QM9-size batches.  Same
+ * layouts and results as hgnn_ccn_forward / _backward: outputs and dX in the same fp32 order (order 2:
+ * the weight gradients too; order 1 sums them in a different order).  d_n_batch may be NULL (every
+ * graph has nmax nodes).
+ * supported: 1 if cfg fits (order 1: the LDS of the backward, 4 nmax^2 (hidden L + 2 max(f_in, hidden)
+ * + 2 hidden) + 8 KB, within 160 KB; order 2: 8 waves x (6.5 KB + 10 nmax^2 B) + 8 KB), else 0 (use
+ * the general path).  Order 2's workspace holds each graph's levels (nmax^3 rows per level bound).
  * Validation (self loops, symmetric pattern, 0 <= n_b <= nmax): a graph with bits stores
  * *d_err = tag * 256 + bits (0 < tag < 2^23; nothing is stored when the batch is valid), so a caller
  * that increases tag per call never zeroes the word and reads a new error as a tag above the last one
