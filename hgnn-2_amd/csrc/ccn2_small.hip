@@ -45,7 +45,6 @@ struct QArgs {
     int bs, nmax, f, h, L, n_out;
     long long r1, r2;          // per-graph row bounds: sum d <= nmax^2, sum d^2 <= nmax^3
     long long gstride;         // floats of one graph's workspace region
-    int lds_dyn;               // dynamic LDS of the launch: past the per-wave scratch, the graph's level arena
     const float* W[Q_LMAX];
     const float* B[Q_LMAX];
     const float* fcw;
@@ -102,7 +101,6 @@ __host__ __device__ inline size_t q_wave_bytes(int nmax) {
 }
 __host__ __device__ inline size_t q_lds_bytes(int nmax) { return q_al16(sizeof(QGraph)) + Q_NW * q_wave_bytes(nmax); }
 constexpr size_t Q_LDS_MAX = 160 * 1024;
-constexpr size_t Q_LDS_DYN = Q_LDS_MAX - 512;  // every launch's dynamic LDS (the kernels' static words aside)
 
 // LDS accesses of one wave's lanes to each other's entries: the LDS executes a wave's operations in order,
 // so a compiler barrier is all that is needed between a store and another lane's load
@@ -209,7 +207,7 @@ __device__ __forceinline__ void q_prologue(const QGraph& g, QWave& w, short* sp,
 // One node of a forward level: k_c2_fwd's arithmetic (one output pass: h <= HC)
 template <int CM, int NB, bool L0>
 __device__ void q_node_fwd(const QArgs& a, QGraph& g, QWave& w, short* sp, float* P, int i, int l, const float* fin,
-                           int cin, float* fout, float* fout_g) {
+                           int cin, float* fout) {
     constexpr int HC = Q_HC;
     const int lane = threadIdx.x & 63;
     const int h = a.h, hc = h, o0 = 0;
@@ -411,7 +409,6 @@ __device__ void q_node_fwd(const QArgs& a, QGraph& g, QWave& w, short* sp, float
                 if (x == y) s += w.s_diag[o];
                 s = s < 0.f ? 0.f : s;
                 fout[(o2 + e) * h + o0 + o] = s;
-                if (fout_g != fout) fout_g[(o2 + e) * h + o0 + o] = s;  // the backward's copy
                 ns[o] += s;
             }
         }
@@ -469,14 +466,6 @@ __global__ void __launch_bounds__(Q_NT) k_ccn2_small_fwd(QArgs a) {
     bad |= q_plan(a, b, n, g);
     const int f = a.f, h = a.h, nf = f + a.L * h;
     float* G = a.gws + (long long)b * a.gstride;
-    // the levels in the LDS arena when the graph's rows fit (QM9: a few hundred rows of 2 channels), written
-    // through to the workspace for the backward; the row walks then wait on LDS, not on L2
-    const long long rows2 = g.off2[n];
-    const size_t arena = (size_t)a.lds_dyn - q_lds_bytes(a.nmax);
-    const bool in_lds = (size_t)(4 * rows2 * h) * a.L <= arena;
-    float* A0 = reinterpret_cast<float*>(lds + q_lds_bytes(a.nmax));
-    const long long lstride = in_lds ? rows2 * h : a.r2 * h;
-    float* Fl0 = in_lds ? A0 : G;
     // level 0 of the readout: sum_i d_i^2 X[i] (utils_ccn.py:167-172 tile X[i] d_i x d_i times)
     q_colsum(g, n, f, 0, [&](int r, int c, double& acc) {
         const double d = g.deg[r];
@@ -485,15 +474,14 @@ __global__ void __launch_bounds__(Q_NT) k_ccn2_small_fwd(QArgs a) {
     });
     for (int l = 0; l < a.L; ++l) {
         const int cin = l == 0 ? f : h;
-        float* fout = Fl0 + l * lstride;
-        float* fout_g = G + (long long)l * a.r2 * h;
-        const float* fin = l == 0 ? nullptr : Fl0 + (l - 1) * lstride;
+        float* fout = G + (long long)l * a.r2 * h;
+        const float* fin = l == 0 ? nullptr : G + (long long)(l - 1) * a.r2 * h;
         if (l == 0) c2_weights<Q_HC, CF>(reinterpret_cast<float(*)[Q_HC][CF]>(g.wc), a.W[l], cin, 0, h);
         else c2_weights<Q_HC, Q_HC>(reinterpret_cast<float(*)[Q_HC][Q_HC]>(g.wc), a.W[l], cin, 0, h);
         __syncthreads();
         for (int i = wv; i < n; i += Q_NW) {
-            if (l == 0) q_node_fwd<CF, 1, true>(a, g, w, sp, P, i, l, fin, cin, fout, fout_g);
-            else q_node_fwd<Q_HC, 8, false>(a, g, w, sp, P, i, l, fin, cin, fout, fout_g);
+            if (l == 0) q_node_fwd<CF, 1, true>(a, g, w, sp, P, i, l, fin, cin, fout);
+            else q_node_fwd<Q_HC, 8, false>(a, g, w, sp, P, i, l, fin, cin, fout);
         }
         __syncthreads();
         q_colsum(g, n, h, f + l * h, [&](int r, int c, double& acc) { acc += (double)g.nsum[l][r][c]; });
@@ -918,39 +906,11 @@ __global__ void __launch_bounds__(Q_NT) k_ccn2_small_bwd(QArgs a) {
     (void)q_plan(a, b, n, g);  // the forward reported the batch's validation bits
     const int f = a.f, h = a.h, L = a.L, nf = f + L * h;
     float* G = a.gws + (long long)b * a.gstride;
-    // the levels, the dp format and the level-0 terms in the LDS arena when they fit (the forward's levels
-    // copied in first), else in the graph's workspace region
-    const long long rows2 = g.off2[n], rows1 = g.off1[n];
-    const size_t arena = (size_t)a.lds_dyn - q_lds_bytes(a.nmax);
-    const size_t need = 4 * (size_t)((L + 2) * rows2 * h + rows1 * h + (long long)n * h + rows1 * f) + 16 * 6;
-    const bool in_lds = need <= arena;
-    float *Fl0, *dA, *dB, *rdp, *trd, *g0;
-    long long lstride;
-    if (in_lds) {
-        char* ar = lds + q_lds_bytes(a.nmax);
-        auto take = [&](long long nfl) {
-            float* p = reinterpret_cast<float*>(ar);
-            ar += (4 * nfl + 15) / 16 * 16;
-            return p;
-        };
-        lstride = rows2 * h;
-        Fl0 = take(L * lstride);
-        dA = take(rows2 * h);
-        dB = take(rows2 * h);
-        rdp = take(rows1 * h);
-        trd = take((long long)n * h);
-        g0 = take(rows1 * f);
-        for (int l = 0; l < L; ++l)
-            for (long long e = threadIdx.x; e < lstride; e += Q_NT) Fl0[l * lstride + e] = G[l * a.r2 * h + e];
-    } else {
-        lstride = a.r2 * h;
-        Fl0 = G;
-        dA = G + (long long)L * a.r2 * h;
-        dB = dA + a.r2 * h;
-        rdp = dB + a.r2 * h;
-        trd = rdp + a.r1 * h;
-        g0 = trd + (long long)a.nmax * h;
-    }
+    float* dA = G + (long long)L * a.r2 * h;
+    float* dB = dA + a.r2 * h;
+    float* rdp = dB + a.r2 * h;
+    float* trd = rdp + a.r1 * h;
+    float* g0 = trd + (long long)a.nmax * h;
     // dsum[k] = sum_o dout[b][o] fcw[o][k] (k_ccn_readout_bwd's order)
     const float* dob = a.dout + (long long)b * a.n_out;
     for (int k = threadIdx.x; k < nf; k += Q_NT) {
@@ -980,8 +940,8 @@ __global__ void __launch_bounds__(Q_NT) k_ccn2_small_bwd(QArgs a) {
         const int cin = l == 0 ? f : h;
         const int K = 18 * cin, stride = h * K + h;
         float* pl = a.ppart[l];
-        const float* Fl = Fl0 + l * lstride;
-        const float* fin = l == 0 ? nullptr : Fl0 + (l - 1) * lstride;
+        const float* Fl = G + (long long)l * a.r2 * h;
+        const float* fin = l == 0 ? nullptr : G + (long long)(l - 1) * a.r2 * h;
         const float* dtop = l == L - 1 ? g.vec + f + (L - 1) * h : nullptr;
         if (l == 0) c2_weights<Q_HC, CF>(reinterpret_cast<float(*)[Q_HC][CF]>(g.wc), a.W[l], cin, 0, h);
         else c2_weights<Q_HC, Q_HC>(reinterpret_cast<float(*)[Q_HC][Q_HC]>(g.wc), a.W[l], cin, 0, h);
@@ -1146,7 +1106,7 @@ template <typename K>
 void q_lds_attr(K kernel, bool& done) {
     if (!done) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)Q_LDS_DYN);
+                                  (int)Q_LDS_MAX);
         (void)hipGetLastError();  // a refused opt-in shows at the launch, not here
         done = true;
     }
@@ -1157,7 +1117,7 @@ void q_lds_attr(K kernel, bool& done) {
 bool ccn2_small_ok(const hgnn_ccn_config* c) {
     return c && c->order == 2 && c->bs > 0 && c->nmax > 0 && c->nmax <= Q_N && c->f_in > 0 && c->f_in <= Q_CF &&
            c->hidden > 0 && c->hidden <= Q_H && c->layers >= 1 && c->layers <= Q_LMAX && c->n_out > 0 &&
-           q_nf(c) <= Q_NF && q_lds_bytes(c->nmax) <= Q_LDS_DYN;
+           q_nf(c) <= Q_NF && q_lds_bytes(c->nmax) <= Q_LDS_MAX;
 }
 
 size_t ccn2_small_workspace_bytes(const hgnn_ccn_config* c) {
@@ -1175,8 +1135,7 @@ int ccn2_small_forward(const hgnn_ccn_config* c, const float* X, const float* ad
     a.tag = tag;
     static bool attr = false;
     q_lds_attr(&k_ccn2_small_fwd<Q_CF>, attr);
-    a.lds_dyn = (int)Q_LDS_DYN;
-    hipLaunchKernelGGL(k_ccn2_small_fwd<Q_CF>, dim3(c->bs), dim3(Q_NT), Q_LDS_DYN, s, a);
+    hipLaunchKernelGGL(k_ccn2_small_fwd<Q_CF>, dim3(c->bs), dim3(Q_NT), q_lds_bytes(c->nmax), s, a);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
 }
@@ -1195,8 +1154,7 @@ int ccn2_small_backward(const hgnn_ccn_config* c, const float* X, const float* a
     a.gfcb = grads[2 * c->layers + 1];
     static bool attr = false;
     q_lds_attr(&k_ccn2_small_bwd<Q_CF>, attr);
-    a.lds_dyn = (int)Q_LDS_DYN;
-    hipLaunchKernelGGL(k_ccn2_small_bwd<Q_CF>, dim3(c->bs), dim3(Q_NT), Q_LDS_DYN, s, a);
+    hipLaunchKernelGGL(k_ccn2_small_bwd<Q_CF>, dim3(c->bs), dim3(Q_NT), q_lds_bytes(c->nmax), s, a);
     HGNN_LAUNCH_CHECK();
     if (c->bs > 1) {
         int np = 0;
