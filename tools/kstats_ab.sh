@@ -1,5 +1,5 @@
 #!/bin/bash
-# Kernel stats of the default bench under two settings of one switch: VAR=HGNN_X bash tools/r04_kstats_ab.sh
+# Kernel stats of the default bench under two settings of one switch: VAR=HGNN_X bash tools/kstats_ab.sh
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd /tmp && export TMPDIR=/tmp
