@@ -742,6 +742,11 @@ int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const in
         const char* e = getenv("HGNN_DW_XCD");
         return !e || e[0] != '0';
     }();
+    static const bool bf3 = [] {
+        const char* e = getenv("HGNN_DW_BF3");
+        return !e || e[0] != '0';
+    }();
+    if (bf3) return launch_gemm_bf3_dw(dy, lddy, a, lda, r_valid, r_cap, o, k, nz, slabs, xcd, s);
     hipLaunchKernelGGL((k_gemm3_tn<128, 128, 32, 4, 2>), dim3(ceil_div(o, 128), ceil_div(k, 128), nz), dim3(512), 0, s,
                        dy, lddy, a, lda, slabs, o, k, r_valid, nz, xcd && nz % 8 == 0 ? 1 : 0);
     HGNN_LAUNCH_CHECK();

@@ -173,7 +173,151 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
     }
 }
 
+// ---- dW on bf16 MFMA: slabs[z][m][n] = sum_{r in chunk z} A[r][m] B[r][n] (k_gemm3_tn's contract: A = dY
+// [R][lda], m < M = 2d; B = the saved aggregate [R][ldb], n < N = kp; chunk z of dw3_kc(R, nz) rows), each
+// operand split into three bf16 planes at staging and the six products with i + j <= 4 summed on
+// v_mfma_f32_32x32x16_bf16 -- the fp32 version is bound by its MFMA issue (8 x 64 cycles per 32x32x16 step
+// of a wave against 6 x 32 here).  Block 128 x 128, 8 waves of 32 x 64; stages of 16 rows.  The reduction
+// index is the row r, so the LDS planes hold the transposed image [m][16 r] (32 B per m, the two 16-B halves
+// swapped by bit 3 of m: conflict-free ds_read_b128 fragments); a thread stages one column and four rows of
+// each operand (scalar loads, 256 B per wave instruction).  A stage is short (12 MFMAs per wave), so the
+// global loads run DW_PD stages ahead in a register ring.
+constexpr int D_BK = 16, D_NT = 512, D_ROWB = D_BK * 2, D_PLANE = 128 * D_ROWB, D_STAGE = 6 * D_PLANE;
+
+__device__ __forceinline__ int dswz(int m, int ch) { return m * D_ROWB + 16 * (ch ^ ((m >> 3) & 1)); }
+
+template <int PD>
+__global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn(const float* __restrict__ A, int lda,
+                                                      const float* __restrict__ B, int ldb,
+                                                      float* __restrict__ slabs, int M, int N,
+                                                      const int* __restrict__ r_valid, int nz, int xcd_remap) {
+    static_assert(PD >= 2, "a ring of at least two stages");
+    __shared__ __attribute__((aligned(16))) char lds[2 * D_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv >> 1, wn = wv & 1;
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (xcd_remap) {  // k_gemm3_tn's order: the output tiles of one row chunk on one XCD
+        const int T = gridDim.x * gridDim.y;
+        const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int j = L >> 3, t = j % T;
+        bz = (L & 7) + 8 * (j / T);
+        bx = t % gridDim.x;
+        by = t / gridDim.x;
+    }
+    const int m0 = bx * 128, n0 = by * 128;
+    const int R = *r_valid;
+    const int kchunk = dw3_kc(R, nz);
+    const int kbeg = bz * kchunk, kend = min(R, kbeg + kchunk);
+    if (kbeg >= kend) return;  // the reduce only sums the chunks that hold rows
+    const int col = tid & 127, rq = tid >> 7;
+    const bool am = m0 + col < M, bn = n0 + col < N;
+    const float* ap = A + m0 + col;
+    const float* bp = B + n0 + col;
+    float ra[PD][4], rb[PD][4];
+    auto load = [&](float (&xa)[4], float (&xb)[4], int k0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int gk = k0 + 4 * rq + i;
+            xa[i] = (gk < kend && am) ? ap[(long long)gk * lda] : 0.f;
+            xb[i] = (gk < kend && bn) ? bp[(long long)gk * ldb] : 0.f;
+        }
+    };
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    auto store = [&](const float (&xa)[4], const float (&xb)[4], int buf) {
+        char* st = lds + buf * D_STAGE;
+        const int off = dswz(col, rq >> 1) + (rq & 1) * 8;
+        bf16x4 p[3], q[3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __bf16 x, y, z;
+            split3(xa[i], x, y, z);
+            p[0][i] = x;
+            p[1][i] = y;
+            p[2][i] = z;
+            split3(xb[i], x, y, z);
+            q[0][i] = x;
+            q[1][i] = y;
+            q[2][i] = z;
+        }
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+            *reinterpret_cast<bf16x4*>(st + pl * D_PLANE + off) = p[pl];
+            *reinterpret_cast<bf16x4*>(st + (3 + pl) * D_PLANE + off) = q[pl];
+        }
+    };
+    f32x16 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const int nt = (kend - kbeg + D_BK - 1) / D_BK;
+    const int r31 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int u = 0; u < PD; ++u) load(ra[u], rb[u], kbeg + u * D_BK);
+    store(ra[0], rb[0], 0);
+    __syncthreads();
+    for (int t0 = 0; t0 < nt; t0 += PD) {
+#pragma unroll
+        for (int u = 0; u < PD; ++u) {
+            const int t = t0 + u;
+            if (t >= nt) break;
+            const char* st = lds + (t & 1) * D_STAGE;
+            bf16x8 a[3], b[2][3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                a[pl] = *reinterpret_cast<const bf16x8*>(st + pl * D_PLANE + dswz(wm * 32 + r31, h));
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    b[j][pl] = *reinterpret_cast<const bf16x8*>(st + (3 + pl) * D_PLANE + dswz(wn * 64 + j * 32 + r31, h));
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {  // the six terms with i + j <= 4, the small ones first
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[j][1], acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][2], acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[j][0], acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][1], acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[j][0], acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][0], acc[j], 0, 0, 0);
+            }
+            if (t + 1 < nt) {
+                const int un = (u + 1) % PD;  // the slot holding stage t + 1
+                store(ra[un], rb[un], (t + 1) & 1);
+                load(ra[u], rb[u], kbeg + (t + PD) * D_BK);  // slot u (stage t, staged) takes stage t + PD
+            }
+            __syncthreads();
+        }
+    }
+    float* out = slabs + (long long)bz * M * N;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int gn = n0 + wn * 64 + j * 32 + r31;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int gm = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (gm < M && gn < N) out[(long long)gm * N + gn] = acc[j][r];
+        }
+    }
+}
+
 }  // namespace
+
+int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o,
+                       int k, int nz, float* slabs, int xcd, hipStream_t s) {
+    if (r_cap <= 0) return 0;
+    if (nz <= 0) return HGNN_ERR_ARG;
+    if ((long long)r_cap * (lda > lddy ? lda : lddy) >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    static const int pd = [] {
+        const char* e = getenv("HGNN_DW_PD");
+        return e ? atoi(e) : 2;
+    }();
+    const dim3 g(ceil_div(o, 128), ceil_div(k, 128), nz);
+    const int xr = xcd && nz % 8 == 0 ? 1 : 0;
+    if (pd == 2) hipLaunchKernelGGL(k_gemm_bf3_tn<2>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr);
+    else if (pd == 6) hipLaunchKernelGGL(k_gemm_bf3_tn<6>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr);
+    else hipLaunchKernelGGL(k_gemm_bf3_tn<4>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr);
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
 
 int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
                         int ldb, int n, const float* bias, int relu_from, float* y, int ldy, float* bn_part,

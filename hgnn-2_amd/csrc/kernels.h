@@ -146,6 +146,9 @@ __host__ __device__ inline int bf3_ld(int k) { return (k + 15) / 16 * 16; }  // 
 int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
                         int ldb, int n, const float* bias, int relu_from, float* y, int ldy, float* bn_part,
                         hipStream_t s);
+// The dW GEMM (launch_gemm3_dw's contract) on bf16 MFMA through the same three-way split
+int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o,
+                       int k, int nz, float* slabs, int xcd, hipStream_t s);
 
 struct RepackItem {
     const float* wl;   // linear conv weight (d, K)
