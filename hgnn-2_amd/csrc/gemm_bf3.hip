@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
 // index is the row r, so the LDS planes hold the transposed image [m][16 r] (32 B per m, the two 16-B halves
 // swapped by bit 3 of m: conflict-free ds_read_b128 fragments); a thread stages one column and four rows of
 // each operand (scalar loads, 256 B per wave instruction).  A stage is short (12 MFMAs per wave), so the
-// global loads run DW_PD stages ahead in a register ring.
+// global loads run PD - 1 stages ahead in a register ring.
 constexpr int D_BK = 16, D_NT = 512, D_ROWB = D_BK * 2, D_PLANE = 128 * D_ROWB, D_STAGE = 6 * D_PLANE;
 
 __device__ __forceinline__ int dswz(int m, int ch) { return m * D_ROWB + 16 * (ch ^ ((m >> 3) & 1)); }
@@ -306,15 +306,9 @@ int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const
     if (r_cap <= 0) return 0;
     if (nz <= 0) return HGNN_ERR_ARG;
     if ((long long)r_cap * (lda > lddy ? lda : lddy) >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
-    static const int pd = [] {
-        const char* e = getenv("HGNN_DW_PD");
-        return e ? atoi(e) : 2;
-    }();
-    const dim3 g(ceil_div(o, 128), ceil_div(k, 128), nz);
-    const int xr = xcd && nz % 8 == 0 ? 1 : 0;
-    if (pd == 2) hipLaunchKernelGGL(k_gemm_bf3_tn<2>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr);
-    else if (pd == 6) hipLaunchKernelGGL(k_gemm_bf3_tn<6>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr);
-    else hipLaunchKernelGGL(k_gemm_bf3_tn<4>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr);
+    // ring depth 2: step times 1.300-1.302 ms against 1.306-1.314 (4) and 1.313-1.323 (6), alternating runs
+    hipLaunchKernelGGL(k_gemm_bf3_tn<2>, dim3(ceil_div(o, 128), ceil_div(k, 128), nz), dim3(D_NT), 0, s, dy, lddy, a, lda,
+                       slabs, o, k, r_valid, nz, xcd && nz % 8 == 0 ? 1 : 0);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
