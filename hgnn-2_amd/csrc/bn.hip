@@ -881,6 +881,18 @@ static bool bn2_enabled() {
     return on;
 }
 
+// The wide two-launch form (c = 64 / 128 / 256) is off by default since round 4: with the dW GEMM on bf16 MFMA
+// beside it, the three-launch form's 64-row tiles (many 256-thread blocks instead of ~91 of 1024 threads)
+// measured 1.254-1.265 vs 1.282-1.313 ms per step in five alternating pairs (config 2); HGNN_BN_BWD2=1
+// turns it back on
+static bool bn2_wide_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("HGNN_BN_BWD2");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 template <int L>
 static void bn2_launch(const BnBwdArgs& a, hipStream_t s) {
     const int t2 = ceil_div(a.cap_rows, BN2_ROWS);
@@ -908,7 +920,7 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
         HGNN_LAUNCH_CHECK();
         return 0;
     }
-    if (apply && v4 && tiles > 0 && bn2_enabled() && few && (a.c == 64 || a.c == 128 || a.c == 256)) {
+    if (apply && v4 && tiles > 0 && bn2_wide_enabled() && few && (a.c == 64 || a.c == 128 || a.c == 256)) {
         if (a.c == 64) bn2_launch<16>(a, s);
         else if (a.c == 128) bn2_launch<32>(a, s);
         else bn2_launch<64>(a, s);
