@@ -13,6 +13,10 @@ from .net import expected_k
 
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_FP32_MFMA_TFS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak
+PEAK_BF16_MFMA_TFS = 16 * PEAK_FP32_MFMA_TFS  # dense bf16 MFMA: 16x the fp32 rate per clock (MI355X_MICROARCH.md)
+# the split-bf16 GEMMs (k_gemm_bf3_fwd, k_gemm_bf3_tn) run six bf16 products per fp32 product: their fp32
+# algorithmic FLOPs are priced against a sixth of the bf16 peak
+PEAK_SPLIT_BF16_TFS = PEAK_BF16_MFMA_TFS / 6
 
 (K_STRUCT, K_AGG_FWD, K_GEMM_FWD, K_BN_FWD, K_READOUT, K_BN_BWD, K_GEMM_DW, K_GEMM_DA, K_AGG_BWD, K_DW_DENSE,
  K_DW_REDUCE) = range(11)
@@ -136,12 +140,12 @@ def forward_work(counts, order, f_in, d, n_layers, jt=3):
 CLASS_KERNELS = {
     K_STRUCT: ("k_plan", "k_extract", "k_pack_nodes", "k_pack_edges", "k_repack", "k_unpack_nodes"),
     K_AGG_FWD: ("k_agg_fwd",),
-    K_GEMM_FWD: ("k_gemm3<", "k_gemm_fwd"),
+    K_GEMM_FWD: ("k_gemm3<", "k_gemm_fwd", "k_gemm_bf3_fwd", "k_gemm5<"),
     K_BN_FWD: ("k_bn_finalize", "k_bn_apply"),
     K_READOUT: ("k_readout",),
     K_BN_BWD: ("k_bn_bwd",),
-    K_GEMM_DW: ("k_gemm3_tn", "k_gemm_dw"),
-    K_GEMM_DA: ("k_gemm3<", "k_gemm_da"),
+    K_GEMM_DW: ("k_gemm3_tn", "k_gemm_dw", "k_gemm_bf3_tn"),
+    K_GEMM_DA: ("k_gemm3<", "k_gemm_da", "k_gemm5<"),
     K_AGG_BWD: ("k_agg_bwd",),
     K_DW_DENSE: ("k_dw_dense",),
     K_DW_REDUCE: ("k_dw_reduce",),
@@ -154,7 +158,21 @@ def _in_class(kcls, name):
     if "k_gemm3<" in name:  # k_gemm3<BM, BN, BK, WGM, WGN, EPI>: EPI 0 = forward, 1 = dA
         epi = name.split(">")[0].rsplit(",", 1)[-1].strip()
         return (kcls == K_GEMM_FWD) == (epi == "0")
+    if "k_gemm5<" in name:  # k_gemm5<BM, BN, WGM, WGN, FWD>: the forward epilogue or dA
+        fwd = name.split(">")[0].rsplit(",", 1)[-1].strip()
+        return (kcls == K_GEMM_FWD) == (fwd == "true")
     return True
+
+
+def split_bf16(kcls, d):
+    """Whether the executor runs class kcls on the split-bf16 GEMMs at width d (net.hip fwd_bf3, gemm3.hip
+    launch_gemm3_dw; their switches HGNN_FWD_BF3 / HGNN_DW_BF3)."""
+    import os
+    if kcls == K_GEMM_FWD:
+        return (2 * d) % 64 == 0 and os.environ.get("HGNN_FWD_BF3", "1") != "0"
+    if kcls == K_GEMM_DW:
+        return os.environ.get("HGNN_DW_BF3", "1") != "0"
+    return False
 
 
 def pmc_traffic(kcls, path):
@@ -178,19 +196,23 @@ def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, s
     """bench.py 'roofline' object for a kernel class measured over `steps` steps."""
     fl, by = class_work(kcls, counts, order, f_in, d, n_layers, jt)
     sec = max(ms_total / 1e3, 1e-12)
+    extra = {}
     if kcls in (K_GEMM_FWD, K_GEMM_DA, K_GEMM_DW):
         achieved = fl * steps / sec / 1e12
         peak, unit, bound = PEAK_FP32_MFMA_TFS, "TFLOP/s", "mfma"
+        if split_bf16(kcls, d):
+            peak = round(PEAK_SPLIT_BF16_TFS, 1)
+            extra["peak_note"] = ("fp32 algorithmic FLOPs against the split-bf16 rate: dense bf16 MFMA peak "
+                                  f"{PEAK_BF16_MFMA_TFS:.1f} TFLOP/s / 6 products per fp32 product")
     else:
         achieved = by * steps / sec / 1e9
         peak, unit, bound = PEAK_HBM_GBS, "GB/s", "hbm"
     per_launch = launches / max(steps, 1)
-    extra = {}
     if kcls in (K_AGG_FWD, K_AGG_BWD):
         rq = agg_requested_bytes(kcls, counts, order, f_in, d, n_layers, jt)
         rq_gbs = rq * steps / sec / 1e9
-        extra = {"requested_bytes_per_launch": rq / max(per_launch, 1e-9), "requested_gbs": round(rq_gbs, 1),
-                 "requested_frac": round(rq_gbs / PEAK_HBM_GBS, 4)}
+        extra.update({"requested_bytes_per_launch": rq / max(per_launch, 1e-9), "requested_gbs": round(rq_gbs, 1),
+                      "requested_frac": round(rq_gbs / PEAK_HBM_GBS, 4)})
     return {**extra, **{
         "kernel": NAMES[kcls],
         "bound": bound,
