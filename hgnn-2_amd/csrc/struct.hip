@@ -355,11 +355,13 @@ __global__ void __launch_bounds__(X_THREADS) k_extract(ExtractArgs a) {
     }
 }
 
-// ---- LDS-staged extraction: one 1024-thread block per (graph, family) loads the graph's dense
-// blocks into LDS in one round of unconditional loads (16 per thread in flight), then builds the
+// ---- LDS-staged extraction: one 512-thread block per (graph, family) loads the graph's dense
+// blocks into LDS in rounds of unconditional loads (16 per thread in flight), then builds the
 // row lists of both orientations and checks the padding from LDS.  Families: 0 = WL (line graph
 // only), 1 = W + Pm/Pd.  Same lists, entry for entry, as k_extract (ascending columns per row).
-constexpr int XL_THREADS = 1024;
+// 512 threads: the 1 024 blocks of config 2 resident in one round (4 per CU); 38.3 us per launch against 42.9
+// (1 024 threads, two rounds) and 55.0 (256), step 1.237-1.255 vs 1.250-1.262 ms in three alternating pairs
+constexpr int XL_THREADS = 512;
 
 __device__ __forceinline__ void lds_fill(float* __restrict__ dst, const float* __restrict__ src, int n) {
     constexpr int U = 16;
