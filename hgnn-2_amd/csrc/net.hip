@@ -43,6 +43,11 @@ struct Half {
     size_t wc3 = 0;                 // Wcat as three bf16 planes [3][2d][bf3_ld(kp)] (split-bf16 forward GEMM)
 };
 
+// Buffer ring of the backward: a dY / bias-partial buffer (and, for the node halves whose dense dW the side
+// stream reads, a dA buffer) per half, up to this many halves, so the main stream never waits mid-backward
+// for the side stream's dW of an earlier half before reusing a buffer (config 2: 8 halves, no such joins)
+constexpr int BWD_NBUF = 16;
+
 struct Program {
     int cap_n = 0, cap_e = 0, jt = 0, d = 0, c2 = 0;
     int c2p = 0;  // 2d rounded up to 4: row stride of dY and of the repacked WT (dA GEMM's float4 k)
@@ -54,7 +59,9 @@ struct Program {
     size_t node_off = 0, edge_off = 0, totals = 0, err = 0;
     size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
     int entry_stride_w = 4;
-    size_t dy = 0, dy2 = 0, da = 0, da2 = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0, dbpart = 0, dbpart2 = 0;
+    size_t da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0;
+    int nbuf = 0;  // ring length: min(halves, BWD_NBUF)
+    size_t dyk[BWD_NBUF] = {}, dbk[BWD_NBUF] = {}, dak[BWD_NBUF] = {};
     size_t bytes = 0;
 };
 
@@ -242,15 +249,22 @@ Program build_program(const hgnn_net_config* c) {
         max_slab = std::max(max_slab, dw3_slab_floats(cap, P.c2, h.k));
         max_cap = std::max(max_cap, cap);
     }
-    P.dbpart = B.take((size_t)bn_bwd_tiles(max_cap > 0 ? max_cap : 1) * P.c2 * sizeof(float));
-    P.dbpart2 = B.take((size_t)bn_bwd_tiles(max_cap > 0 ? max_cap : 1) * P.c2 * sizeof(float));
+    // ring slot q % nbuf for the q-th half of the backward's walk (the last half first)
+    P.nbuf = std::max(1, std::min((int)P.halves.size(), BWD_NBUF));
+    for (int i = 0; i < P.nbuf; ++i) {
+        P.dbk[i] = B.take((size_t)bn_bwd_tiles(max_cap > 0 ? max_cap : 1) * P.c2 * sizeof(float));
+        P.dyk[i] = B.take((size_t)max_cap * P.c2p * sizeof(float));
+        size_t na = 0;  // the node halves of this slot (their dA is read by the side stream's dense dW)
+        for (int q = i; q < (int)P.halves.size(); q += P.nbuf) {
+            const Half& h = P.halves[P.halves.size() - 1 - q];
+            if (!h.edge) na = std::max(na, (size_t)P.cap_n * h.kp);
+        }
+        if (na) P.dak[i] = B.take(na * sizeof(float));
+    }
     P.a_last = B.take((size_t)P.cap_n * P.k_last * sizeof(float));
     P.colsum = B.take((size_t)c->bs * P.k_last * sizeof(float));
     max_da = std::max(max_da, (size_t)P.cap_n * P.k_last);
-    P.dy = B.take((size_t)max_cap * P.c2p * sizeof(float));
-    P.dy2 = B.take((size_t)max_cap * P.c2p * sizeof(float));
-    P.da = B.take(max_da * sizeof(float));
-    P.da2 = B.take(max_da * sizeof(float));  // dA alternates like dY: the side stream's dense dW reads it
+    P.da = B.take(max_da * sizeof(float));  // dA of the halves the side stream does not read, and the readout's
     P.slabs = B.take(max_slab * sizeof(float));
     P.bnb_part = B.take((size_t)bn_bwd_tiles(max_cap) * P.c2 * 4 * sizeof(float));
     P.bnb_sums = B.take((size_t)P.c2 * 4 * sizeof(float));
@@ -402,7 +416,7 @@ struct Timer {
 struct SideStream {
     int dev = -1;
     hipStream_t s = nullptr;
-    hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
+    hipEvent_t fork[2] = {nullptr, nullptr}, join[BWD_NBUF + 1] = {};  // join[BWD_NBUF]: the end of the backward
 };
 
 static int side_stream(hipStream_t main_s, SideStream** out) {
@@ -417,17 +431,13 @@ static int side_stream(hipStream_t main_s, SideStream** out) {
         HGNN_HOST_CHECK(hipSetDevice(dev));
         if (ss.s) {
             (void)hipStreamDestroy(ss.s);
-            for (int i = 0; i < 2; ++i) {
-                (void)hipEventDestroy(ss.fork[i]);
-                (void)hipEventDestroy(ss.join[i]);
-            }
+            for (int i = 0; i < 2; ++i) (void)hipEventDestroy(ss.fork[i]);
+            for (int i = 0; i <= BWD_NBUF; ++i) (void)hipEventDestroy(ss.join[i]);
         }
         ss = SideStream{};
         HGNN_HOST_CHECK(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
-        for (int i = 0; i < 2; ++i) {
-            HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming));
-            HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming));
-        }
+        for (int i = 0; i < 2; ++i) HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming));
+        for (int i = 0; i <= BWD_NBUF; ++i) HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming));
         ss.dev = dev;
         HGNN_HOST_CHECK(hipSetDevice(cur));
     }
@@ -728,10 +738,13 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     // cross-stream event record / wait costs the main stream ~6-7 us of idle GPU per fork)
     static const bool use_side = env_flag("HGNN_SIDE", true);
     if (use_side) TRY(side_stream(s, &side));
-    // dY and the bias partials alternate between two buffers, so the side stream's
-    // dW of half i may still read its pair while the main stream runs half i+1.
-    bool pending[2] = {false, false};
-    int parity = 0;
+    // dY, the bias partials and the side-read dA of the q-th half (of the reverse walk) live in ring slot
+    // q % nbuf, so the side stream's dW of an earlier half may still read its slot while the main stream runs
+    // the next halves; the main stream waits for the side stream only where a slot comes round again (more
+    // than BWD_NBUF halves) and once at the end.  (Two alternating slots and a join per half before round 4:
+    // each mid-backward join idles the main stream.)
+    bool pending[BWD_NBUF] = {};
+    int slot = 0, q = 0;
     // The side stream also takes the dense operator gradient (W.requires_grad) of a node
     // half: it only accumulates into dW, so it leaves the dA -> aggregation-backward chain.
     // (Measured alternative, not kept: the gather half of the aggregation backward on a third
@@ -741,8 +754,8 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
                        float* dab) -> int {
         const int nz = dw3_chunks(cap, P.c2, h.k);
         if (side) {
-            HGNN_HOST_CHECK(hipEventRecord(side->fork[parity], s));
-            HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, side->fork[parity], 0));
+            HGNN_HOST_CHECK(hipEventRecord(side->fork[q & 1], s));
+            HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, side->fork[q & 1], 0));
         }
         hipStream_t main_s = s;
         // HGNN_SERIAL_BWD=1 (diagnostics): everything on the main stream, so a kernel trace shows
@@ -759,10 +772,12 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, nz, P.c2, P.c2, h.k, P.d,
                                                    grads[h.pw_lin], grads[h.pw_relu], dbp, grads[h.pb_lin],
                                                    grads[h.pb_relu], s));
-            if (side) r = hipEventRecord(side->join[parity], s) == hipSuccess ? 0 : HGNN_ERR_HIP;
+            // a join only where the slot comes round again (the end of the backward has its own)
+            if (side && q + P.nbuf < (int)P.halves.size())
+                r = hipEventRecord(side->join[slot], s) == hipSuccess ? 0 : HGNN_ERR_HIP;
         } while (0);
         s = main_s;
-        pending[parity] = side != nullptr;
+        pending[slot] = side != nullptr && q + P.nbuf < (int)P.halves.size();
         return r;
     };
     // per-layer completion events (hgnn_net_backward_ex): recorded once the first half (in program
@@ -780,11 +795,11 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         const Half& h = P.halves[hi];
         const int cap = h.edge ? P.cap_e : P.cap_n;
         const int* tot = h.edge ? tot_e : tot_n;
-        float* dyb = at<float>(ws, parity ? P.dy2 : P.dy);
-        float* dbp = at<float>(ws, parity ? P.dbpart2 : P.dbpart);
-        if (pending[parity]) {  // the dW two halves back still reads this dY / bias-partial pair
-            HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[parity], 0));
-            pending[parity] = false;
+        float* dyb = at<float>(ws, P.dyk[slot]);
+        float* dbp = at<float>(ws, P.dbk[slot]);
+        if (pending[slot]) {  // the dW nbuf halves back still reads this slot
+            HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[slot], 0));
+            pending[slot] = false;
         }
         if (!init[h.out]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[h.out].grad), 0,
                                                           (size_t)cap * P.c2 * sizeof(float), s));
@@ -814,7 +829,9 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             TRY(fork_dw(h, cap, tot, dyb, dbp, false, nullptr));
             return 0;
         }
-        float* da = at<float>(ws, parity ? P.da2 : P.da);
+        // the side stream's dense dW reads a node half's dA: its own slot buffer; other halves share P.da
+        const bool ndw_side = ndw && side;
+        float* da = at<float>(ws, ndw_side && P.dak[slot] ? P.dak[slot] : P.da);
         TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2p, tot, cap, P.c2p, at<float>(ws, h.wt), P.c2p, h.k, da, h.kp, s));
         // dW starts once dA is done: two MFMA GEMMs side by side only slow each other,
         // dW beside the latency-bound dense-dW / aggregation-backward kernels does not
@@ -855,12 +872,14 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         if (np) init[h.pin] = 1;
         return 0;
     };
-    for (int hi = (int)P.halves.size() - 1; hi >= 0; --hi, parity ^= 1) {
+    for (int hi = (int)P.halves.size() - 1; hi >= 0; --hi, ++q, slot = q % P.nbuf) {
         TRY(half_bwd(hi));
         TRY(mark(hi));
     }
-    for (int p = 0; p < 2; ++p)
-        if (pending[p]) HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[p], 0));
+    if (side) {  // the side stream runs in order: its last work done means all of it is
+        HGNN_HOST_CHECK(hipEventRecord(side->join[BWD_NBUF], side->s));
+        HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[BWD_NBUF], 0));
+    }
     if (c->need_dx) {
         if (!dX) return HGNN_ERR_ARG;
         if (!init[0]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[0].grad), 0,

@@ -259,7 +259,8 @@ class _NetFn(torch.autograd.Function):
             inp.d_E_batch = Eb.data_ptr()
             inp.d_mask_lg = mask_lg.data_ptr()
         run = L.ptr_array(spec.running)
-        args = (ctypes.byref(cfg), ctypes.byref(inp), L.ptr_array(params), run, ctypes.c_void_p(ws.data_ptr()),
+        pp = L.ptr_array(params)
+        args = (ctypes.byref(cfg), ctypes.byref(inp), pp, run, ctypes.c_void_p(ws.data_ptr()),
                 ctypes.c_void_p(out.data_ptr()), L.stream_handle(dev))
         if _timer is not None:
             st = lib.hgnn_net_forward_timed(*args, ctypes.c_void_p(_timer.handle))
@@ -270,6 +271,7 @@ class _NetFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.ws = ws
         ctx.inp = inp  # device pointers of the inputs below, read again by the backward
+        ctx.param_ptrs = pp  # the parameters' pointers (saved below: an in-place change raises)
         ctx.spec = spec
         # saved through autograd: an in-place change of an input or a weight between forward and
         # backward raises the usual version error instead of giving wrong gradients
@@ -290,7 +292,7 @@ class _NetFn(torch.autograd.Function):
         cfg.need_dw = 1 if dW is not None else 0
         with torch.cuda.device(X.device):
             st = L.lib().hgnn_net_backward_ex(
-                ctypes.byref(cfg), ctypes.byref(ctx.inp), None, L.ptr_array(params),
+                ctypes.byref(cfg), ctypes.byref(ctx.inp), None, ctx.param_ptrs,
                 ctypes.c_void_p(ctx.ws.data_ptr()), ctypes.c_void_p(dout.data_ptr()), L.ptr_array(grads), L.ptr(dX),
                 L.ptr(dW), L.stream_handle(X.device), ctypes.c_void_p(_timer.handle) if _timer is not None else None,
                 evs, nev)
@@ -309,10 +311,10 @@ def _grad_targets(spec, params):
             evs = (ctypes.c_void_p * max(1, len(dp.event_handles)))(*dp.event_handles)
             return list(views), evs, len(dp.event_handles)
         # some p.grad present: fresh tensors, accumulated by autograd (dp.py, gradient accumulation)
-    # one allocation for all of them (50 empty_like calls were ~0.1 ms of host time per step)
-    sizes = [p.numel() for p in params]
-    flat = torch.empty(sum(sizes), dtype=torch.float32, device=params[0].device)
-    return [v.view(p.shape) for v, p in zip(flat.split(sizes), params)], None, 0
+    # one allocation for all of them (50 empty_like calls were ~0.1 ms of host time per step), cut into the
+    # parameters' shapes in one C++ call (split + view per parameter in Python cost ~0.3 ms per step)
+    flat = torch.empty(sum(p.numel() for p in params), dtype=torch.float32, device=params[0].device)
+    return list(torch._C._nn.unflatten_dense_tensors(flat, params)), None, 0
 
 
 def run_net(spec, X, W, N_batch, mask, XL=None, WL=None, Pm=None, Pd=None, E_batch=None, mask_lg=None):
@@ -351,9 +353,26 @@ def run_net(spec, X, W, N_batch, mask, XL=None, WL=None, Pm=None, Pd=None, E_bat
         return _NetFn.apply(spec, tensors, X, W, *params)
 
 
+_checked_last = [None, None]  # (signature, parameter list) of the last call that passed the checks
+
+
 def _checked_params(spec, f_in, jt, dev):
     """Every parameter's shape against the widths the executor will read (the C ABI gets bare
-    pointers: a mismatch would be an out-of-bounds device read), dtype and device."""
+    pointers: a mismatch would be an out-of-bounds device read), dtype and device.  A call with the same
+    parameter objects at the same storage addresses, widths and device as the last one that passed
+    returns its list without re-checking (~70 us of host time per forward)."""
+    params = spec.params
+    sig = (spec.kind, spec.order, spec.d, spec.n_layers, spec.dim_out, f_in, jt, dev,
+           tuple(map(id, params)), tuple(p.data_ptr() for p in params))
+    if _checked_last[0] == sig:
+        return _checked_last[1]
+    out = _check_params(spec, f_in, jt, dev)
+    if all(a is b for a, b in zip(out, params)):  # contiguous as given: nothing copied, safe to reuse
+        _checked_last[0], _checked_last[1] = sig, out
+    return out
+
+
+def _check_params(spec, f_in, jt, dev):
     lg = spec.kind == 1
     ks, k_last = expected_k(spec.kind, spec.order, f_in, spec.d, spec.n_layers, jt)
     params = list(spec.params)

@@ -30,13 +30,31 @@ def use_torch_ops():
 from models.layers import layers_mnb
 
 
+# The parameters in ABI order, read through the modules' _modules / _parameters dicts: the attribute path
+# (nn.Module.__getattr__, two per parameter) cost ~130 us of host time per forward at config 2; a name that
+# is not a registered submodule / parameter falls back to it
+def _sub(mod, name):
+    m = mod._modules.get(name)
+    return m if m is not None else getattr(mod, name)
+
+
+def _param(mod, name):
+    p = mod._parameters.get(name)
+    return p if p is not None else getattr(mod, name)
+
+
+def _pair(mod, name):
+    m = _sub(mod, name)
+    return [_param(m, "weight"), _param(m, "bias")]
+
+
 def _lg_params(layer):
-    return [layer.cv1.weight, layer.cv1.bias, layer.cv2.weight, layer.cv2.bias, layer.bn1.weight, layer.bn1.bias,
-            layer.cv3.weight, layer.cv3.bias, layer.cv4.weight, layer.cv4.bias, layer.bn2.weight, layer.bn2.bias]
+    return (_pair(layer, "cv1") + _pair(layer, "cv2") + _pair(layer, "bn1") + _pair(layer, "cv3") + _pair(layer, "cv4") +
+            _pair(layer, "bn2"))
 
 
 def _simple_params(layer):
-    return [layer.cv1.weight, layer.cv1.bias, layer.cv2.weight, layer.cv2.bias, layer.bn1.weight, layer.bn1.bias]
+    return _pair(layer, "cv1") + _pair(layer, "cv2") + _pair(layer, "bn1")
 
 
 class GNN_simple(nn.Module):
