@@ -653,9 +653,29 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         return launch_dw_dense(dw_args(gin, da, lda, readout, accumulate), s);
     };
 
+    SideStream* side = nullptr;
+    // HGNN_SIDE=0: the weight-gradient work stays on the main stream, with no events at all (a
+    // cross-stream event record / wait costs the main stream ~6-7 us of idle GPU per fork)
+    static const bool use_side = env_flag("HGNN_SIDE", true);
+    if (use_side) TRY(side_stream(s, &side));
+    static const bool serial_bwd = env_flag("HGNN_SERIAL_BWD", false);
+    // the readout's parameter gradients and its dense dW only feed gradients: on the side stream, forked
+    // here, beside the main stream's readout aggregation backward and first halves
+    hipStream_t rs = s;
+    if (side && !serial_bwd) {
+        HGNN_HOST_CHECK(hipEventRecord(side->fork[1], s));
+        HGNN_HOST_CHECK(hipStreamWaitEvent(side->s, side->fork[1], 0));
+        rs = side->s;
+    }
     // readout
-    TL(HGNN_K_READOUT, launch_readout_bwd_params(dout, at<float>(ws, P.colsum), c->bs, c->nmax, c->dim_out, P.k_last,
-                                  grads[P.p_fcw], grads[P.p_fcb], at<void>(ws, P.rb_scratch), s));
+    {
+        hipStream_t main_s = s;
+        s = rs;  // TL records its timer events on the stream the kernel runs on
+        TL(HGNN_K_READOUT, launch_readout_bwd_params(dout, at<float>(ws, P.colsum), c->bs, c->nmax, c->dim_out,
+                                                     P.k_last, grads[P.p_fcw], grads[P.p_fcb],
+                                                     at<void>(ws, P.rb_scratch), s));
+        s = main_s;
+    }
     // HGNN_READOUT_ROW=0: the readout gradient materialised as a [rows][K] buffer and gathered.  The
     // readout-row kernels hold a graph's rows in LDS: configurations beyond it (wide 2d with a large
     // Nmax / Emax) take the materialised form as well.
@@ -686,7 +706,12 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     }
     const DwDenseArgs dwr = need_dw ? dw_args(P.last_gin, nullptr, 0, true, 0) : DwDenseArgs{};
     if (ro_row && (lgr || lpr || need_dw) && readout_row_fits(ra, need_dw ? &dwr : nullptr)) {
-        if (need_dw) TL(HGNN_K_DW_DENSE, launch_dw_readout(dwr, s));
+        if (need_dw) {
+            hipStream_t main_s = s;
+            s = rs;
+            TL(HGNN_K_DW_DENSE, launch_dw_readout(dwr, s));
+            s = main_s;
+        }
         if (lgr || lpr) TL(HGNN_K_AGG_BWD, launch_readout_agg_bwd(ra, s));
         if (lgr) init[P.last_gin] = 1;
         if (lpr) init[P.last_pin] = 1;
@@ -733,11 +758,6 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         if (lp) init[P.last_pin] = 1;
     }
 
-    SideStream* side = nullptr;
-    // HGNN_SIDE=0: the weight-gradient work stays on the main stream, with no events at all (a
-    // cross-stream event record / wait costs the main stream ~6-7 us of idle GPU per fork)
-    static const bool use_side = env_flag("HGNN_SIDE", true);
-    if (use_side) TRY(side_stream(s, &side));
     // dY, the bias partials and the side-read dA of the q-th half (of the reverse walk) live in ring slot
     // q % nbuf, so the side stream's dW of an earlier half may still read its slot while the main stream runs
     // the next halves; the main stream waits for the side stream only where a slot comes round again (more
