@@ -83,7 +83,10 @@ static bool vec_ok(int cpl, int c, const void* base, std::initializer_list<long 
 // Entry lists are fetched lane-parallel (lane e holds entry e of a 64-entry chunk)
 // and broadcast with readlane, and U feature rows are loaded before any is used,
 // so a row of n entries costs ~n/U dependent memory round trips instead of 2n.
-constexpr int AGG_U = 4;
+#ifndef AGG_UNROLL
+#define AGG_UNROLL 4
+#endif
+constexpr int AGG_U = AGG_UNROLL;
 // rows (waves) per block of the aggregation kernels; AGG_BLOCK_WAVES at build time (A/B)
 #ifndef AGG_BLOCK_WAVES
 #define AGG_BLOCK_WAVES 4

@@ -246,3 +246,28 @@ def test_small_ccn_validation_word_reported_and_cleared():
     with pytest.raises(RuntimeError, match="self loop"):
         w.check(False)
     w.check(False)
+
+
+def test_spec_params_and_checked_params_cache():
+    """The executor's parameter list (read through the modules' dicts) is the modules' parameters in ABI
+    order, the same objects attribute access gives; the cached parameter check re-checks a replaced
+    parameter and raises on a wrong shape."""
+    import hgnn_amd.net as N
+    from models.gnns.model_mnb import GNN_lg, GNN_simple
+    m = GNN_lg(0, 16, 4, 5, 1, 1, 2)
+    dev = torch.device("cpu")
+    spec = m._spec(dev)
+    ref = []
+    for layer in m._layers():
+        for sub in ("cv1", "cv2", "bn1", "cv3", "cv4", "bn2"):
+            mod = getattr(layer, sub)
+            ref += [mod.weight, mod.bias]
+    ref += [m.layerlast.fc.weight, m.layerlast.fc.bias]
+    assert len(spec.params) == len(ref) and all(a is b for a, b in zip(spec.params, ref))
+    assert len(GNN_simple(0, 2, 5, 5, 1, 1)._spec(dev).params) == 4 * 6 + 2  # layer0 + 3 mid layers, fc
+    first = N._checked_params(spec, 5, 3, dev)
+    again = N._checked_params(m._spec(dev), 5, 3, dev)
+    assert again is first  # same objects at the same addresses: the cached list
+    m.layer0.cv1.weight = torch.nn.Parameter(torch.zeros(16, 3, 1))
+    with pytest.raises(RuntimeError, match="conv weight"):
+        N._checked_params(m._spec(dev), 5, 3, dev)
