@@ -387,7 +387,7 @@ def main():
             roof_hbm[RF.NAMES[k]] = {x: e[x] for x in (
                 "bound", "achieved", "peak", "unit", "frac", "traffic", "algorithmic_bytes_per_launch",
                 "launches_per_step", "avg_launch_us", "requested_bytes_per_launch", "requested_gbs",
-                "requested_frac") if x in e}
+                "requested_frac", "traffic_gbs", "traffic_frac") if x in e}
             roof_hbm[RF.NAMES[k]]["traffic_source"] = traffic_note
 
     # forward-only line (config "cfg2f"): the north star's HBM target is stated on the batched

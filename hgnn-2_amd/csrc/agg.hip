@@ -270,8 +270,8 @@ static void agg_fwd_v(const AggFwdArgs& a, dim3 g, hipStream_t s) {
     const bool v = (CG == 0 || vec_ok(CG, a.cg, a.xg, {})) && (CP == 0 || vec_ok(CP, a.cp, a.xp, {})) &&
                    (CG == 0 || vec_ok(CG, a.cg, a.out, {a.ldo, (long long)kk})) &&
                    (CP == 0 || vec_ok(CP, a.cp, a.out, {a.ldo, (long long)JT * a.cg, (long long)a.cp}));
-    if (v) hipLaunchKernelGGL((k_agg_fwd<JT, CG, CP, true>), g, dim3(AGG_NT), 0, s, a);
-    else hipLaunchKernelGGL((k_agg_fwd<JT, CG, CP, false>), g, dim3(AGG_NT), 0, s, a);
+    if (v) HGNN_KLAUNCH((k_agg_fwd<JT, CG, CP, true>), g, dim3(AGG_NT), 0, s, a);
+    else HGNN_KLAUNCH((k_agg_fwd<JT, CG, CP, false>), g, dim3(AGG_NT), 0, s, a);
 }
 
 template <int JT, int CG>
@@ -459,11 +459,11 @@ template <int JT, int C>
 static int agg_bwd_single(const AggBwdArgs& a, hipStream_t s) {
     const dim3 g(ceil_div(a.cap_rows, AGG_WV));
     if (a.ing) {
-        if (bwd_vec_g(C, a)) hipLaunchKernelGGL((k_agg_bwd<JT, C, C, true, 1>), g, dim3(AGG_NT), 0, s, a, a, 0);
-        else hipLaunchKernelGGL((k_agg_bwd<JT, C, C, false, 1>), g, dim3(AGG_NT), 0, s, a, a, 0);
+        if (bwd_vec_g(C, a)) HGNN_KLAUNCH((k_agg_bwd<JT, C, C, true, 1>), g, dim3(AGG_NT), 0, s, a, a, 0);
+        else HGNN_KLAUNCH((k_agg_bwd<JT, C, C, false, 1>), g, dim3(AGG_NT), 0, s, a, a, 0);
     } else {
-        if (bwd_vec_p(C, a)) hipLaunchKernelGGL((k_agg_bwd<3, C, C, true, 2>), g, dim3(AGG_NT), 0, s, a, a, 0);
-        else hipLaunchKernelGGL((k_agg_bwd<3, C, C, false, 2>), g, dim3(AGG_NT), 0, s, a, a, 0);
+        if (bwd_vec_p(C, a)) HGNN_KLAUNCH((k_agg_bwd<3, C, C, true, 2>), g, dim3(AGG_NT), 0, s, a, a, 0);
+        else HGNN_KLAUNCH((k_agg_bwd<3, C, C, false, 2>), g, dim3(AGG_NT), 0, s, a, a, 0);
     }
     HGNN_LAUNCH_CHECK();
     return 0;
@@ -496,7 +496,7 @@ int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s) {
 template <int JT, int C>
 static int agg_bwd_pair_c(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t s) {
     const int gb = ceil_div(ga.cap_rows, AGG_WV), pb = ceil_div(pa.cap_rows, AGG_WV);
-    hipLaunchKernelGGL((k_agg_bwd<JT, C, C, true, 3>), dim3(gb + pb), dim3(AGG_NT), 0, s, ga, pa, gb);
+    HGNN_KLAUNCH((k_agg_bwd<JT, C, C, true, 3>), dim3(gb + pb), dim3(AGG_NT), 0, s, ga, pa, gb);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(256) k_bn_finalize(BnFwdArgs a) {
 }
 
 int launch_bn_finalize(const BnFwdArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_bn_finalize, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, a);
+    HGNN_KLAUNCH(k_bn_finalize, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -123,7 +123,7 @@ int launch_bn_apply(const float* y, const int* total_rows, int cap_rows, int c, 
     int blocks = (int)ceil_div<long long>(n, 256);
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_bn_apply, dim3(blocks), dim3(256), 0, s, y, total_rows, c, mean, std, w, b, z);
+    HGNN_KLAUNCH(k_bn_apply, dim3(blocks), dim3(256), 0, s, y, total_rows, c, mean, std, w, b, z);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -869,8 +869,8 @@ __global__ void __launch_bounds__(256 * L) k_bn_bwd_apply2s(BnBwdArgs a) {
 template <int L>
 static void bn2s_launch(const BnBwdArgs& a, hipStream_t s) {
     const int t2 = ceil_div(a.cap_rows, BN2_ROWS);
-    hipLaunchKernelGGL(k_bn_bwd_part2s<L>, dim3(t2), dim3(256 * L), 0, s, a);
-    hipLaunchKernelGGL(k_bn_bwd_apply2s<L>, dim3(t2), dim3(256 * L), 0, s, a);
+    HGNN_KLAUNCH(k_bn_bwd_part2s<L>, dim3(t2), dim3(256 * L), 0, s, a);
+    HGNN_KLAUNCH(k_bn_bwd_apply2s<L>, dim3(t2), dim3(256 * L), 0, s, a);
 }
 
 static bool bn2_enabled() {
@@ -897,10 +897,10 @@ template <int L>
 static void bn2_launch(const BnBwdArgs& a, hipStream_t s) {
     const int t2 = ceil_div(a.cap_rows, BN2_ROWS);
     if constexpr (L == 64)  // 256 channels: two blocks of 128 per tile
-        hipLaunchKernelGGL((k_bn_bwd_part2<32, 64>), dim3(t2, 2), dim3(BN2_THREADS), 0, s, a);
+        HGNN_KLAUNCH((k_bn_bwd_part2<32, 64>), dim3(t2, 2), dim3(BN2_THREADS), 0, s, a);
     else
-        hipLaunchKernelGGL(k_bn_bwd_part2<L>, dim3(t2), dim3(BN2_THREADS), 0, s, a);
-    hipLaunchKernelGGL(k_bn_bwd_apply2<L>, dim3(t2), dim3(BN2_THREADS), 0, s, a);
+        HGNN_KLAUNCH(k_bn_bwd_part2<L>, dim3(t2), dim3(BN2_THREADS), 0, s, a);
+    HGNN_KLAUNCH(k_bn_bwd_apply2<L>, dim3(t2), dim3(BN2_THREADS), 0, s, a);
 }
 
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
@@ -928,15 +928,15 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
         return 0;
     }
     if (tiles > 0) {
-        if (v4) hipLaunchKernelGGL(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
+        if (v4) HGNN_KLAUNCH(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, a);
+        else HGNN_KLAUNCH(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
     }
     HGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bn_bwd_fin, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, a);
+    HGNN_KLAUNCH(k_bn_bwd_fin, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, a);
     HGNN_LAUNCH_CHECK();
     if (!apply) return 0;
-    if (v4) hipLaunchKernelGGL(k_bn_bwd_apply4, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_bn_bwd_apply, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);
+    if (v4) HGNN_KLAUNCH(k_bn_bwd_apply4, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);
+    else HGNN_KLAUNCH(k_bn_bwd_apply, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -1000,7 +1000,7 @@ __global__ void __launch_bounds__(RO_THREADS) k_readout_fwd(const float* __restr
 
 int launch_readout_fwd(const float* a, int k, const int* node_off, int bs, int nmax, const float* fcw,
                        const float* fcb, int dim_out, float* colsum, float* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_readout_fwd, dim3(bs), dim3(RO_THREADS), 0, s, a, k, node_off, nmax, fcw, fcb, dim_out,
+    HGNN_KLAUNCH(k_readout_fwd, dim3(bs), dim3(RO_THREADS), 0, s, a, k, node_off, nmax, fcw, fcb, dim_out,
                        colsum, out);
     HGNN_LAUNCH_CHECK();
     return 0;
@@ -1024,7 +1024,7 @@ int launch_readout_bwd_da(const float* dout, const int* node_off, int bs, int ca
                           const float* fcw, int dim_out, int k, float* da, hipStream_t s) {
     (void)cap_rows;
     (void)total_rows;
-    hipLaunchKernelGGL(k_readout_bwd_da, dim3(bs), dim3(256), 0, s, dout, node_off, fcw, dim_out, k, da);
+    HGNN_KLAUNCH(k_readout_bwd_da, dim3(bs), dim3(256), 0, s, dout, node_off, fcw, dim_out, k, da);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -1132,7 +1132,7 @@ int launch_readout_agg_bwd(const ReadoutAggArgs& a, hipStream_t s) {
     const size_t lds = readout_agg_bwd_lds(a);
     if (lds > RO_LDS_CAP) return HGNN_ERR_UNSUPPORTED;
     allow_ro_lds(k_readout_agg_bwd, lds);
-    hipLaunchKernelGGL(k_readout_agg_bwd, dim3(a.bs, a.p_out ? 2 : 1), dim3(RA_THREADS), lds, s, a);
+    HGNN_KLAUNCH(k_readout_agg_bwd, dim3(a.bs, a.p_out ? 2 : 1), dim3(RA_THREADS), lds, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -1184,7 +1184,7 @@ int launch_dw_readout(const DwDenseArgs& a, hipStream_t s) {
     const size_t lds = dw_readout_lds(a);
     if (lds > RO_LDS_CAP || !a.dout) return HGNN_ERR_UNSUPPORTED;
     allow_ro_lds(k_dw_readout, lds);
-    hipLaunchKernelGGL(k_dw_readout, dim3(a.bs), dim3(256), lds, s, a);
+    HGNN_KLAUNCH(k_dw_readout, dim3(a.bs), dim3(256), lds, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -1253,11 +1253,11 @@ size_t readout_bwd_scratch_bytes(int dim_out, int k) {
 int launch_readout_bwd_params(const float* dout, const float* colsum, int bs, int nmax, int dim_out, int k,
                               float* dfcw, float* dfcb, void* scratch, hipStream_t s) {
     double* part = static_cast<double*>(scratch);
-    hipLaunchKernelGGL(k_readout_bwd_part, dim3(ceil_div(k, 64), RB_CHUNKS), dim3(256), 0, s, dout, colsum, bs,
+    HGNN_KLAUNCH(k_readout_bwd_part, dim3(ceil_div(k, 64), RB_CHUNKS), dim3(256), 0, s, dout, colsum, bs,
                        dim_out, k, part);
     HGNN_LAUNCH_CHECK();
     const int n = dim_out * k > dim_out ? dim_out * k : dim_out;
-    hipLaunchKernelGGL(k_readout_bwd_params, dim3(ceil_div(n, 256)), dim3(256), 0, s, dout, part, bs, nmax,
+    HGNN_KLAUNCH(k_readout_bwd_params, dim3(ceil_div(n, 256)), dim3(256), 0, s, dout, part, bs, nmax,
                        dim_out, k, dfcw, dfcb);
     HGNN_LAUNCH_CHECK();
     return 0;

@@ -2254,7 +2254,7 @@ template <int CM, int HC, int NB, bool L0>
 int launch_c2_fwd_t(const CcnPlanView& v, const int* tot, const float* fin, const float* X, int cin, const float* W,
                     const float* b, int h, int ncap, int nodes, float* fout, float* nsum, hipStream_t s) {
     const size_t lds = c2_dyn_lds(ncap, HC);
-    hipLaunchKernelGGL((k_c2_fwd<CM, HC, NB, L0>), dim3(nodes > 0 ? nodes : 1), dim3(256), lds, s, v, tot, fin, X, cin,
+    HGNN_KLAUNCH((k_c2_fwd<CM, HC, NB, L0>), dim3(nodes > 0 ? nodes : 1), dim3(256), lds, s, v, tot, fin, X, cin,
                        W, b, h, ncap, fout, nsum);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
@@ -2278,7 +2278,7 @@ int launch_c2_bwd_t(const CcnPlanView& v, const int* tot, float* dF, const float
                     const float* fin, const float* X, int cin, const float* W, int h, int ncap, int nodes, float* rdp,
                     float* trd, float* ppart, float* g0, hipStream_t s) {
     const size_t lds = c2_dyn_lds(ncap, HC);
-    hipLaunchKernelGGL((k_c2_bwd<CM, HC, NB, L0>), dim3(nodes > 0 ? nodes : 1), dim3(256), lds, s, v, tot, dF, dtop,
+    HGNN_KLAUNCH((k_c2_bwd<CM, HC, NB, L0>), dim3(nodes > 0 ? nodes : 1), dim3(256), lds, s, v, tot, dF, dtop,
                        dtop_ld, F, fin, X, cin, W, h, ncap, rdp, trd, ppart, g0);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
@@ -2305,21 +2305,21 @@ int launch_c2_gather(const CcnPlanView& v, const int* tot, const C2Dp& g, const 
                      int dsum_ld, int dsum_off, long long dmax, int nodes, float* dout, hipStream_t s) {
     const dim3 grid(nodes > 0 ? nodes : 1);
     if (h <= 2)
-        hipLaunchKernelGGL((k_c2_gather<2, 8>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
+        HGNN_KLAUNCH((k_c2_gather<2, 8>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
     else if (h <= 8)
-        hipLaunchKernelGGL((k_c2_gather<8, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
+        HGNN_KLAUNCH((k_c2_gather<8, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
     else
-        hipLaunchKernelGGL((k_c2_gather<16, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
+        HGNN_KLAUNCH((k_c2_gather<16, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld, dsum_off, dout);
     HGNN_LAUNCH_CHECK();
     if (dmax > C2_NCAP) {
         if (h <= 2)
-            hipLaunchKernelGGL((k_c2_gather_big<2, 4>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld,
+            HGNN_KLAUNCH((k_c2_gather_big<2, 4>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld,
                                dsum_off, dout);
         else if (h <= 8)
-            hipLaunchKernelGGL((k_c2_gather_big<8, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld,
+            HGNN_KLAUNCH((k_c2_gather_big<8, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld,
                                dsum_off, dout);
         else
-            hipLaunchKernelGGL((k_c2_gather_big<16, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld,
+            HGNN_KLAUNCH((k_c2_gather_big<16, 1>), grid, dim3(256), 0, s, v, tot, g, W, h, dsum, dsum_ld,
                                dsum_off, dout);
         HGNN_LAUNCH_CHECK();
     }
@@ -2336,7 +2336,7 @@ extern "C" {
 int hgnn_collapse6to3(const float* d_F, float* d_out, int c, int n, void* stream) {
     if (!d_F || !d_out || c <= 0 || n <= 0) return HGNN_ERR_ARG;
     const long long tot = (long long)n * n * 18 * c;
-    hipLaunchKernelGGL(k_collapse6to3, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_F,
+    HGNN_KLAUNCH(k_collapse6to3, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_F,
                        d_out, c, n);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
@@ -2345,7 +2345,7 @@ int hgnn_collapse6to3(const float* d_F, float* d_out, int c, int n, void* stream
 int hgnn_collapse6to3_backward(const float* d_dout, float* d_dF, int c, int n, void* stream) {
     if (!d_dout || !d_dF || c <= 0 || n <= 0) return HGNN_ERR_ARG;
     const long long tot = (long long)c * n * n * n * n * n;
-    hipLaunchKernelGGL(k_collapse6to3_bwd, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+    HGNN_KLAUNCH(k_collapse6to3_bwd, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        d_dout, d_dF, c, n);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
@@ -2377,12 +2377,12 @@ static int ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_
     int r = launch_plan(d_n_batch, nullptr, cfg->bs, cfg->nmax, 0, m, s);
     if (r) return r;
     CcnPlanView v = plan_view(cfg, L, plan_ws);
-    hipLaunchKernelGGL(k_ccn_nbrs, dim3(cfg->bs, (cfg->nmax + CCN_NB_ROWS - 1) / CCN_NB_ROWS), dim3(256), 0, s, d_adj,
+    HGNN_KLAUNCH(k_ccn_nbrs, dim3(cfg->bs, (cfg->nmax + CCN_NB_ROWS - 1) / CCN_NB_ROWS), dim3(256), 0, s, d_adj,
                        cfg->nmax, v.node_off, P<int>(plan_ws, L.deg), P<int>(plan_ws, L.nbr),
                        P<int>(plan_ws, L.selfpos), P<int>(plan_ws, L.graph), P<unsigned long long>(plan_ws, L.bits),
                        P<int>(plan_ws, L.bcnt), m.err, cfg->order == 1 ? CCN1_MAXD : CCN_BIGD);
     HGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ccn_scan, dim3(1), dim3(1024), 0, s, P<int>(plan_ws, L.deg), m.totals,
+    HGNN_KLAUNCH(k_ccn_scan, dim3(1), dim3(1024), 0, s, P<int>(plan_ws, L.deg), m.totals,
                        P<int>(plan_ws, L.off1), P<int>(plan_ws, L.off2), m.totals + 2);
     HGNN_LAUNCH_CHECK();
     long long nodes = (long long)cfg->bs * cfg->nmax;
@@ -2403,7 +2403,7 @@ static int ccn_plan(const hgnn_ccn_config* cfg, const float* d_adj, const int64_
         h_sums[2] = nodes;
         h_sums[3] = cfg->nmax;
     }
-    hipLaunchKernelGGL(k_ccn_pos, dim3((unsigned)((nodes + 3) / 4 > 0 ? (nodes + 3) / 4 : 1)), dim3(256), 0, s, v,
+    HGNN_KLAUNCH(k_ccn_pos, dim3((unsigned)((nodes + 3) / 4 > 0 ? (nodes + 3) / 4 : 1)), dim3(256), 0, s, v,
                        m.totals, P<unsigned long long>(plan_ws, L.bits), P<int>(plan_ws, L.bcnt),
                        P<int>(plan_ws, L.pos), max_sum_d2, m.err);
     HGNN_LAUNCH_CHECK();
@@ -2447,7 +2447,7 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
     const int nodes = (int)sums[2];
     const int h = cfg->hidden, f = cfg->f_in;
     float* Xp = P<float>(W, L.xp);
-    hipLaunchKernelGGL(k_ccn_pack_x, dim3(cfg->bs), dim3(256), 0, s, d_X, v.node_off, cfg->nmax, f, Xp);
+    HGNN_KLAUNCH(k_ccn_pack_x, dim3(cfg->bs), dim3(256), 0, s, d_X, v.node_off, cfg->nmax, f, Xp);
     HGNN_LAUNCH_CHECK();
     d_X = Xp;
     for (int l = 0; l < cfg->layers; ++l) {
@@ -2456,7 +2456,7 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
         const float* w = params[2 * l];
         const float* b = params[2 * l + 1];
         if (cfg->order == 1) {
-            hipLaunchKernelGGL(k_ccn1_fwd, dim3(nodes > 0 ? (nodes + 3) / 4 : 1), dim3(256), 0, s, v, tot, fin,
+            HGNN_KLAUNCH(k_ccn1_fwd, dim3(nodes > 0 ? (nodes + 3) / 4 : 1), dim3(256), 0, s, v, tot, fin,
                                l == 0 ? 1 : 0, d_X, cin, w, b, h, P<float>(W, L.coll[l]), P<float>(W, L.F[l]));
         } else {
             const bool narrow = cin <= C2_CMAX && h <= C2_HMAX;
@@ -2465,11 +2465,11 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
             if (r) return r;
             if (sums[3] > CCN_MAXD) {  // degrees 65..256 present (or possible): their nodes in the large-degree kernel
                 if (narrow)
-                    hipLaunchKernelGGL((k_ccn2_fwd_big<C2_CMAX, C2_HMAX>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s,
+                    HGNN_KLAUNCH((k_ccn2_fwd_big<C2_CMAX, C2_HMAX>), dim3(nodes > 0 ? nodes : 1), dim3(256), 0, s,
                                        v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h, save_of(L, W, l),
                                        P<float>(W, L.F[l]), P<float>(W, L.nsum[l]));
                 else
-                    hipLaunchKernelGGL((k_ccn2_fwd_big<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nodes > 0 ? nodes : 1),
+                    HGNN_KLAUNCH((k_ccn2_fwd_big<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nodes > 0 ? nodes : 1),
                                        dim3(256), 0, s, v, tot, fin, l == 0 ? 1 : 0, d_X, cin, w, b, h,
                                        save_of(L, W, l), P<float>(W, L.F[l]), P<float>(W, L.nsum[l]));
             }
@@ -2492,9 +2492,9 @@ int hgnn_ccn_forward(const hgnn_ccn_config* cfg, const long long* sums, const fl
     ra.feat = P<float>(W, L.feat);
     ra.out = d_out;
     ra.nch = ro_chunks(cfg->order == 2 ? nodes : sums[0], cfg->bs);
-    hipLaunchKernelGGL(k_ccn_readout_part, dim3(cfg->bs, ra.nch), dim3(256), 0, s, ra, P<double>(W, L.rpart));
+    HGNN_KLAUNCH(k_ccn_readout_part, dim3(cfg->bs, ra.nch), dim3(256), 0, s, ra, P<double>(W, L.rpart));
     HGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ccn_readout, dim3(cfg->bs), dim3(256), 0, s, ra, P<double>(W, L.rpart));
+    HGNN_KLAUNCH(k_ccn_readout, dim3(cfg->bs), dim3(256), 0, s, ra, P<double>(W, L.rpart));
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
 }
@@ -2513,7 +2513,7 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
     const int h = cfg->hidden, f = cfg->f_in, Lv = cfg->layers;
     const int nf = f + Lv * h;
     float* dsum = P<float>(W, L.dsum);
-    hipLaunchKernelGGL(k_ccn_readout_bwd,
+    HGNN_KLAUNCH(k_ccn_readout_bwd,
                        dim3((cfg->bs * nf + 255) / 256 + (cfg->n_out * nf + cfg->n_out + 3) / 4), dim3(256), 0, s,
                        d_dout, P<float>(W, L.feat), params[2 * Lv], cfg->bs, cfg->n_out, nf, dsum, grads[2 * Lv],
                        grads[2 * Lv + 1]);
@@ -2528,7 +2528,7 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
     const bool bigd = cfg->order == 2 && sums[3] > CCN_MAXD;
     const bool top_direct = cfg->order == 2 && !bigd;
     if (!top_direct) {
-        hipLaunchKernelGGL(k_ccn_bcast, dim3(nb1), dim3(64), 0, s, v, tot, cfg->order, dsum, nf, f + (Lv - 1) * h, h,
+        HGNN_KLAUNCH(k_ccn_bcast, dim3(nb1), dim3(64), 0, s, v, tot, cfg->order, dsum, nf, f + (Lv - 1) * h, h,
                            dF);
         HGNN_LAUNCH_CHECK();
     }
@@ -2538,7 +2538,7 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
         const int K = (cfg->order == 1 ? 2 : 18) * cin;
         float* ppart = P<float>(W, L.ppart);
         if (cfg->order == 1) {
-            hipLaunchKernelGGL(k_ccn1_bwd_node, dim3(nb4), dim3(256), 0, s, v, tot, dF, P<float>(W, L.F[l]),
+            HGNN_KLAUNCH(k_ccn1_bwd_node, dim3(nb4), dim3(256), 0, s, v, tot, dF, P<float>(W, L.F[l]),
                                P<float>(W, L.coll[l]), cin, w, h, P<float>(W, L.dcoll), ppart);
         } else {
             const bool narrow = cin <= C2_CMAX && h <= C2_HMAX;
@@ -2548,13 +2548,13 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
                 C2Grad gd{P<float>(W, L.g_sc), P<float>(W, L.g_sa), P<float>(W, L.g_d1), P<float>(W, L.g_d2),
                           P<float>(W, L.g_d3)};
                 if (narrow)
-                    hipLaunchKernelGGL((k_ccn2_bwd_node_big<C2_CMAX, C2_HMAX>), dim3(nb1), dim3(256), 0, s, v, tot, dF,
+                    HGNN_KLAUNCH((k_ccn2_bwd_node_big<C2_CMAX, C2_HMAX>), dim3(nb1), dim3(256), 0, s, v, tot, dF,
                                        P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
                 else
-                    hipLaunchKernelGGL((k_ccn2_bwd_node_big<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nb1), dim3(256), 0, s, v,
+                    HGNN_KLAUNCH((k_ccn2_bwd_node_big<C2_CMAX_WIDE, C2_HMAX_WIDE>), dim3(nb1), dim3(256), 0, s, v,
                                        tot, dF, P<float>(W, L.F[l]), save_of(L, W, l), cin, w, h, gd, ppart, g0p);
                 HGNN_LAUNCH_CHECK();
-                hipLaunchKernelGGL(k_c2_dp_big, dim3(nb1), dim3(256), 0, s, v, tot, dF, P<float>(W, L.F[l]), h,
+                HGNN_KLAUNCH(k_c2_dp_big, dim3(nb1), dim3(256), 0, s, v, tot, dF, P<float>(W, L.F[l]), h,
                                    P<float>(W, L.rdp), P<float>(W, L.trd));
                 HGNN_LAUNCH_CHECK();
             }
@@ -2565,18 +2565,18 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
             if (r) return r;
         }
         HGNN_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_ccn_param_reduce, dim3(h * K + h), dim3(256), 0, s, ppart, tot, h * K, h, grads[2 * l],
+        HGNN_KLAUNCH(k_ccn_param_reduce, dim3(h * K + h), dim3(256), 0, s, ppart, tot, h * K, h, grads[2 * l],
                            grads[2 * l + 1]);
         HGNN_LAUNCH_CHECK();
         const int lvl0 = l == 0 ? 1 : 0;
         float* dst = lvl0 ? P<float>(W, L.dxp) : dFn;
         const int doff = lvl0 ? 0 : f + (l - 1) * h;
         if (cfg->order == 1) {
-            hipLaunchKernelGGL(k_ccn1_bwd_gather, dim3(nb4), dim3(256), 0, s, v, tot, P<float>(W, L.dcoll), cin, dsum,
+            HGNN_KLAUNCH(k_ccn1_bwd_gather, dim3(nb4), dim3(256), 0, s, v, tot, P<float>(W, L.dcoll), cin, dsum,
                                nf, doff, lvl0, dst);
         } else {
             if (lvl0) {
-                hipLaunchKernelGGL(k_ccn2_dx0, dim3(nb4), dim3(256), 0, s, v, tot, P<float>(W, L.g0), cin, dsum, nf,
+                HGNN_KLAUNCH(k_ccn2_dx0, dim3(nb4), dim3(256), 0, s, v, tot, P<float>(W, L.g0), cin, dsum, nf,
                                    dst);
             } else {
                 const C2Dp g{dF, P<float>(W, L.rdp), P<float>(W, L.trd)};
@@ -2590,7 +2590,7 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
         dFn = t;
     }
     (void)rows;
-    hipLaunchKernelGGL(k_ccn_unpack_dx, dim3(cfg->bs), dim3(256), 0, s, P<float>(W, L.dxp), v.node_off, cfg->nmax, f,
+    HGNN_KLAUNCH(k_ccn_unpack_dx, dim3(cfg->bs), dim3(256), 0, s, P<float>(W, L.dxp), v.node_off, cfg->nmax, f,
                        d_dX);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;

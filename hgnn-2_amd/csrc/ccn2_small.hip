@@ -1135,7 +1135,7 @@ int ccn2_small_forward(const hgnn_ccn_config* c, const float* X, const float* ad
     a.tag = tag;
     static bool attr = false;
     q_lds_attr(&k_ccn2_small_fwd<Q_CF>, attr);
-    hipLaunchKernelGGL(k_ccn2_small_fwd<Q_CF>, dim3(c->bs), dim3(Q_NT), q_lds_bytes(c->nmax), s, a);
+    HGNN_KLAUNCH(k_ccn2_small_fwd<Q_CF>, dim3(c->bs), dim3(Q_NT), q_lds_bytes(c->nmax), s, a);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
 }
@@ -1154,13 +1154,13 @@ int ccn2_small_backward(const hgnn_ccn_config* c, const float* X, const float* a
     a.gfcb = grads[2 * c->layers + 1];
     static bool attr = false;
     q_lds_attr(&k_ccn2_small_bwd<Q_CF>, attr);
-    hipLaunchKernelGGL(k_ccn2_small_bwd<Q_CF>, dim3(c->bs), dim3(Q_NT), q_lds_bytes(c->nmax), s, a);
+    HGNN_KLAUNCH(k_ccn2_small_bwd<Q_CF>, dim3(c->bs), dim3(Q_NT), q_lds_bytes(c->nmax), s, a);
     HGNN_LAUNCH_CHECK();
     if (c->bs > 1) {
         int np = 0;
         for (int l = 0; l < c->layers; ++l) np += (int)q_prow(c, l);
         const int nf = q_nf(c);
-        hipLaunchKernelGGL(k_ccn2_small_reduce, dim3(np + (c->n_out * nf + c->n_out + 3) / 4), dim3(256), 0, s, a, np);
+        HGNN_KLAUNCH(k_ccn2_small_reduce, dim3(np + (c->n_out * nf + c->n_out + 3) / 4), dim3(256), 0, s, a, np);
         HGNN_LAUNCH_CHECK();
     }
     return HGNN_OK;

@@ -742,7 +742,7 @@ int hgnn_ccn_small_forward(const hgnn_ccn_config* cfg, const float* d_X, const f
         HGNN_HOST_CHECK(hipMemsetAsync(dprof, 0, 32 * 8, (hipStream_t)stream));
         a.prof = dprof;
     }
-    hipLaunchKernelGGL(k_ccn1_small_fwd<CS_CF>, dim3(cfg->bs), dim3(CS_NT), lds, (hipStream_t)stream, a);
+    HGNN_KLAUNCH(k_ccn1_small_fwd<CS_CF>, dim3(cfg->bs), dim3(CS_NT), lds, (hipStream_t)stream, a);
     HGNN_LAUNCH_CHECK();
     if (prof) {  // diagnostic: phase cycles of graph 0 (synchronises)
         unsigned long long hp[32];
@@ -779,17 +779,17 @@ int hgnn_ccn_small_backward(const hgnn_ccn_config* cfg, const float* d_X, const 
     if (cfg->hidden <= 2) {
         static bool attr = false;
         cs_lds_attr(&k_ccn1_small_bwd<CS_CF, 2>, attr);
-        hipLaunchKernelGGL((k_ccn1_small_bwd<CS_CF, 2>), dim3(cfg->bs), dim3(CS_NT), lds, s, a);
+        HGNN_KLAUNCH((k_ccn1_small_bwd<CS_CF, 2>), dim3(cfg->bs), dim3(CS_NT), lds, s, a);
     } else {
         static bool attr = false;
         cs_lds_attr(&k_ccn1_small_bwd<CS_CF, CS_CF>, attr);
-        hipLaunchKernelGGL((k_ccn1_small_bwd<CS_CF, CS_CF>), dim3(cfg->bs), dim3(CS_NT), lds, s, a);
+        HGNN_KLAUNCH((k_ccn1_small_bwd<CS_CF, CS_CF>), dim3(cfg->bs), dim3(CS_NT), lds, s, a);
     }
     HGNN_LAUNCH_CHECK();
     if (cfg->bs > 1) {
         const int nf = cfg->f_in + cfg->layers * cfg->hidden;
         const int outs = (int)cs_ptot(cfg) + cfg->n_out * nf + cfg->n_out;
-        hipLaunchKernelGGL(k_ccn1_small_reduce, dim3((outs + 3) / 4), dim3(256), 0, s, a);
+        HGNN_KLAUNCH(k_ccn1_small_reduce, dim3((outs + 3) / 4), dim3(256), 0, s, a);
         HGNN_LAUNCH_CHECK();
     }
     return HGNN_OK;

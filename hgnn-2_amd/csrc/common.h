@@ -10,6 +10,7 @@
 //    past the device total exit at once.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,6 +31,39 @@
     } while (0)
 
 namespace hgnn {
+
+// Per-dispatch kernel clock (bench.py's per-class timer, net.hip Timer): while t_clock is set on the
+// enqueuing thread, HGNN_KLAUNCH launches through hipExtLaunchKernel with a start / stop event pair that
+// the runtime binds to the kernel's own dispatch (its begin / end timestamps, as rocprofv3's kernel trace
+// reports them) -- no marker packets between the kernels of the stream, so timing changes neither the
+// stream's dispatch order nor what the kernel overlaps with.
+struct LaunchClock {
+    hipEvent_t* ev;  // pairs: start, stop
+    int* cls;        // class of each pair
+    int cap;         // pairs available
+    int* used;       // pairs taken
+    int k;           // class of the launches being enqueued
+};
+inline thread_local LaunchClock* t_clock = nullptr;
+inline bool clock_pair(hipEvent_t* a, hipEvent_t* b) {
+    LaunchClock* c = t_clock;
+    if (!c || *c->used >= c->cap) return false;
+    const int i = (*c->used)++;
+    c->cls[i] = c->k;
+    *a = c->ev[2 * i];
+    *b = c->ev[2 * i + 1];
+    return true;
+}
+
+// Every kernel launch of the library: hipLaunchKernelGGL, or, under a LaunchClock, the same launch with a
+// dispatch-bound event pair.  (Variadic so a template kernel's commas need no parentheses.)
+template <typename F, typename... Args>
+inline void klaunch(F kernel, const dim3& grid, const dim3& block, uint32_t lds, hipStream_t s, Args... args) {
+    hipEvent_t a, b;
+    if (clock_pair(&a, &b)) hipExtLaunchKernelGGL(kernel, grid, block, lds, s, a, b, 0u, args...);
+    else hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+}
+#define HGNN_KLAUNCH(...) hgnn::klaunch(__VA_ARGS__)
 
 // Device-side error bits (OR-ed into a workspace word; see include/hgnn_amd.h).
 enum : uint32_t {

@@ -120,15 +120,15 @@ int hgnn_conv1x1_forward(const float* d_x, const float* d_w, const float* d_b, f
     float* wt = (float*)(ws + w.wt);
     const int cinp = pad4(cin), coutp = pad4(cout);
     const long long rows = (long long)bs * n;
-    hipLaunchKernelGGL(k_to_rows, dim3(grid_for(rows * cinp)), dim3(256), 0, s, d_x, xt, bs, cin, n, cinp);
+    HGNN_KLAUNCH(k_to_rows, dim3(grid_for(rows * cinp)), dim3(256), 0, s, d_x, xt, bs, cin, n, cinp);
     HGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pad_weights, dim3(grid_for((long long)cout * cinp + (long long)cin * coutp)), dim3(256), 0, s,
+    HGNN_KLAUNCH(k_pad_weights, dim3(grid_for((long long)cout * cinp + (long long)cin * coutp)), dim3(256), 0, s,
                        d_w, cout, cin, wc, cinp, wt, coutp);
     HGNN_LAUNCH_CHECK();
     // the executor's fp32 MFMA GEMM (gemm3.hip, NT): Y = Xrows . Wc^T + b, ReLU applied on the way back
     int r = launch_gemm3_fwd(xt, cinp, nullptr, (int)rows, cinp, wc, cinp, cout, d_b, cout, yt, cout, nullptr, s);
     if (r) return r;
-    hipLaunchKernelGGL(k_from_rows, dim3(grid_for(rows * cout)), dim3(256), 0, s, yt, d_y, bs, cout, n, cout, relu);
+    HGNN_KLAUNCH(k_from_rows, dim3(grid_for(rows * cout)), dim3(256), 0, s, yt, d_y, bs, cout, n, cout, relu);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
 }
@@ -151,11 +151,11 @@ int hgnn_conv1x1_backward(const float* d_x, const float* d_w, const float* d_dy,
     const int cinp = pad4(cin), coutp = pad4(cout);
     const long long rows = (long long)bs * n;
     HGNN_HOST_CHECK(hipMemsetD32Async((hipDeviceptr_t)cnt, (int)rows, 1, s));
-    hipLaunchKernelGGL(k_to_rows, dim3(grid_for(rows * cinp)), dim3(256), 0, s, d_x, xt, bs, cin, n, cinp);
+    HGNN_KLAUNCH(k_to_rows, dim3(grid_for(rows * cinp)), dim3(256), 0, s, d_x, xt, bs, cin, n, cinp);
     HGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_to_rows, dim3(grid_for(rows * coutp)), dim3(256), 0, s, d_dy, yt, bs, cout, n, coutp);
+    HGNN_KLAUNCH(k_to_rows, dim3(grid_for(rows * coutp)), dim3(256), 0, s, d_dy, yt, bs, cout, n, coutp);
     HGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pad_weights, dim3(grid_for((long long)cout * cinp + (long long)cin * coutp)), dim3(256), 0, s,
+    HGNN_KLAUNCH(k_pad_weights, dim3(grid_for((long long)cout * cinp + (long long)cin * coutp)), dim3(256), 0, s,
                        d_w, cout, cin, wc, cinp, wt, coutp);
     HGNN_LAUNCH_CHECK();
     // dW = dYrows^T . Xrows (TN, row-chunk slabs) -> reduce; db = column sums of dY
@@ -164,13 +164,13 @@ int hgnn_conv1x1_backward(const float* d_x, const float* d_w, const float* d_dy,
     if (r) return r;
     r = launch_dw_reduce2(slabs, cnt, nz, cout, cout, cin, cout, d_dw, d_dw, nullptr, nullptr, nullptr, s);
     if (r) return r;
-    hipLaunchKernelGGL(k_bias_grad, dim3(cout), dim3(256), 0, s, d_dy, bs, cout, n, d_db);
+    HGNN_KLAUNCH(k_bias_grad, dim3(cout), dim3(256), 0, s, d_dy, bs, cout, n, d_db);
     HGNN_LAUNCH_CHECK();
     if (d_dx) {
         // dX = dYrows . Wt^T (NT); written over xt (x no longer needed)
         r = launch_gemm3_da(yt, coutp, nullptr, (int)rows, coutp, wt, coutp, cin, xt, cinp, s);
         if (r) return r;
-        hipLaunchKernelGGL(k_from_rows, dim3(grid_for(rows * cin)), dim3(256), 0, s, xt, d_dx, bs, cin, n, cinp, 0);
+        HGNN_KLAUNCH(k_from_rows, dim3(grid_for(rows * cin)), dim3(256), 0, s, xt, d_dx, bs, cin, n, cinp, 0);
         HGNN_LAUNCH_CHECK();
     }
     return HGNN_OK;

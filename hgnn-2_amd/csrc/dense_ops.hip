@@ -230,7 +230,7 @@ int hgnn_graph_oper_forward(const float* d_A, const float* d_X, float* d_out, in
                             void* stream) {
     if (!d_A || !d_X || !d_out || bs < 0 || n < 0 || j <= 0 || f < 0) return HGNN_ERR_ARG;
     if (bs == 0 || n == 0 || f == 0) return HGNN_OK;
-    hipLaunchKernelGGL(k_gop_fwd, dim3(bs, j), dim3(256), 0, (hipStream_t)stream, d_A, d_X, d_out, n, j, f);
+    HGNN_KLAUNCH(k_gop_fwd, dim3(bs, j), dim3(256), 0, (hipStream_t)stream, d_A, d_X, d_out, n, j, f);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
 }
@@ -240,11 +240,11 @@ int hgnn_graph_oper_backward(const float* d_A, const float* d_X, const float* d_
     if (!d_A || !d_X || !d_dout || bs < 0 || n < 0 || j <= 0 || f < 0) return HGNN_ERR_ARG;
     if (bs == 0 || n == 0) return HGNN_OK;
     if (d_dX && f > 0) {
-        hipLaunchKernelGGL(k_gop_bwd_x, dim3(bs), dim3(256), 0, (hipStream_t)stream, d_A, d_dout, d_dX, n, j, f);
+        HGNN_KLAUNCH(k_gop_bwd_x, dim3(bs), dim3(256), 0, (hipStream_t)stream, d_A, d_dout, d_dX, n, j, f);
         HGNN_LAUNCH_CHECK();
     }
     if (d_dA) {
-        hipLaunchKernelGGL(k_gop_bwd_a, dim3(bs), dim3(256), 0, (hipStream_t)stream, d_X, d_dout, d_dA, n, j, f);
+        HGNN_KLAUNCH(k_gop_bwd_a, dim3(bs), dim3(256), 0, (hipStream_t)stream, d_X, d_dout, d_dA, n, j, f);
         HGNN_LAUNCH_CHECK();
     }
     return HGNN_OK;
@@ -254,7 +254,7 @@ int hgnn_p_multi_forward(const float* d_P, long sb, long sn, long sm, const floa
                          int n, int m, int f, void* stream) {
     if (!d_P || !d_X || !d_out || bs < 0 || n < 0 || m < 0 || f < 0) return HGNN_ERR_ARG;
     if (bs == 0 || n == 0 || f == 0) return HGNN_OK;
-    hipLaunchKernelGGL(k_pm_fwd, dim3(bs), dim3(256), 0, (hipStream_t)stream, d_P, sb, sn, sm, d_X, d_out, n, m, f);
+    HGNN_KLAUNCH(k_pm_fwd, dim3(bs), dim3(256), 0, (hipStream_t)stream, d_P, sb, sn, sm, d_X, d_out, n, m, f);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
 }
@@ -263,7 +263,7 @@ int hgnn_p_multi_backward(const float* d_P, long sb, long sn, long sm, const flo
                           float* d_dX, float* d_dP, int bs, int n, int m, int f, void* stream) {
     if (!d_P || !d_X || !d_dout || !d_dX || bs < 0 || n < 0 || m < 0 || f < 0) return HGNN_ERR_ARG;
     if (bs == 0 || m == 0) return HGNN_OK;
-    hipLaunchKernelGGL(k_pm_bwd, dim3(bs), dim3(256), 0, (hipStream_t)stream, d_P, sb, sn, sm, d_X, d_dout, d_dX,
+    HGNN_KLAUNCH(k_pm_bwd, dim3(bs), dim3(256), 0, (hipStream_t)stream, d_P, sb, sn, sm, d_X, d_dout, d_dX,
                        d_dP, n, m, f);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
@@ -275,10 +275,10 @@ int hgnn_bn_forward(const float* d_X, const int64_t* d_nb, const float* d_mask, 
         return HGNN_ERR_ARG;
     hipStream_t s = (hipStream_t)stream;
     if (training) {
-        hipLaunchKernelGGL(k_bnd_stats, dim3(c), dim3(256), 0, s, d_X, d_nb, d_mask, d_mean, d_std, bs, c, n);
+        HGNN_KLAUNCH(k_bnd_stats, dim3(c), dim3(256), 0, s, d_X, d_nb, d_mask, d_mean, d_std, bs, c, n);
         HGNN_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_bnd_apply, dim3(blocks_for((long long)bs * c * n)), dim3(256), 0, s, d_X, d_mask, d_mean,
+    HGNN_KLAUNCH(k_bnd_apply, dim3(blocks_for((long long)bs * c * n)), dim3(256), 0, s, d_X, d_mask, d_mean,
                        d_std, d_w, d_b, d_out, bs, c, n);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
@@ -292,9 +292,9 @@ int hgnn_bn_backward(const float* d_X, const int64_t* d_nb, const float* d_mask,
     if (bs <= 0 || c <= 0 || n <= 0) return HGNN_ERR_ARG;
     hipStream_t s = (hipStream_t)stream;
     float* sums = d_scratch;
-    hipLaunchKernelGGL(k_bnd_bwd_stats, dim3(c), dim3(256), 0, s, d_X, d_mask, d_mean, d_std, d_dout, sums, bs, c, n);
+    HGNN_KLAUNCH(k_bnd_bwd_stats, dim3(c), dim3(256), 0, s, d_X, d_mask, d_mean, d_std, d_dout, sums, bs, c, n);
     HGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bnd_bwd_apply, dim3(blocks_for((long long)bs * c * n)), dim3(256), 0, s, d_X, d_nb, d_mask,
+    HGNN_KLAUNCH(k_bnd_bwd_apply, dim3(blocks_for((long long)bs * c * n)), dim3(256), 0, s, d_X, d_nb, d_mask,
                        d_mean, d_std, d_w, d_dout, sums, d_dX, d_dw, d_db, bs, c, n, training);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;

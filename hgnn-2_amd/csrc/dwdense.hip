@@ -239,9 +239,9 @@ static void launch_fc(const DwDenseArgs& a, int maxi, int gy, size_t lds, hipStr
     allow_lds<FC, 1>(lds);
     allow_lds<FC, 3>(lds);
     allow_lds<FC, 5>(lds);
-    if (maxi <= 1) hipLaunchKernelGGL((k_dw_dense<FC, 1>), dim3(a.bs, gy), dim3(256), lds, s, a);
-    else if (maxi <= 3) hipLaunchKernelGGL((k_dw_dense<FC, 3>), dim3(a.bs, gy), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL((k_dw_dense<FC, 5>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    if (maxi <= 1) HGNN_KLAUNCH((k_dw_dense<FC, 1>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    else if (maxi <= 3) HGNN_KLAUNCH((k_dw_dense<FC, 3>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    else HGNN_KLAUNCH((k_dw_dense<FC, 5>), dim3(a.bs, gy), dim3(256), lds, s, a);
 }
 
 // Narrow inputs (F <= 16: layer 0's node features, the GNN_simple layers of config 1): the outer
@@ -296,7 +296,7 @@ int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
         const size_t lds = sizeof(float) * (size_t)a.nmax * (a.jt * a.f + a.f);
         if (lds <= 64 * 1024) {
             const int gy = std::max(1, std::min(16, 512 / std::max(1, a.bs)));
-            hipLaunchKernelGGL(k_dw_dense_narrow, dim3(a.bs, gy), dim3(256), lds, s, a);
+            HGNN_KLAUNCH(k_dw_dense_narrow, dim3(a.bs, gy), dim3(256), lds, s, a);
             HGNN_LAUNCH_CHECK();
             return 0;
         }

@@ -747,7 +747,7 @@ int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const in
         return !e || e[0] != '0';
     }();
     if (bf3) return launch_gemm_bf3_dw(dy, lddy, a, lda, r_valid, r_cap, o, k, nz, slabs, xcd, s);
-    hipLaunchKernelGGL((k_gemm3_tn<128, 128, 32, 4, 2>), dim3(ceil_div(o, 128), ceil_div(k, 128), nz), dim3(512), 0, s,
+    HGNN_KLAUNCH((k_gemm3_tn<128, 128, 32, 4, 2>), dim3(ceil_div(o, 128), ceil_div(k, 128), nz), dim3(512), 0, s,
                        dy, lddy, a, lda, slabs, o, k, r_valid, nz, xcd && nz % 8 == 0 ? 1 : 0);
     HGNN_LAUNCH_CHECK();
     return 0;
@@ -780,10 +780,10 @@ int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int
     if (mfma16 && g5 > 0 && n % 64 == 0 && n <= 512 && (g5 == 2 || waves32 < 2 * 1024)) {
         const int gx = ceil_div(ceil_div(m_cap, 64), 8) * 8;
         if (g5 == 3)  // 64 x 32 tiles of 4 waves: twice the blocks, finer per-CU balance
-            hipLaunchKernelGGL((k_gemm5<64, 32, 2, 2, true>), dim3(gx, n / 32), dim3(256), 0, s, a, lda, wc, ldw,
+            HGNN_KLAUNCH((k_gemm5<64, 32, 2, 2, true>), dim3(gx, n / 32), dim3(256), 0, s, a, lda, wc, ldw,
                                m_valid, m_cap, n, k, y, ldy, 1, bias, relu_from, bn_part);
         else
-            hipLaunchKernelGGL((k_gemm5<64, 64, 2, 4, true>), dim3(gx, n / 64), dim3(512), 0, s, a, lda, wc, ldw,
+            HGNN_KLAUNCH((k_gemm5<64, 64, 2, 4, true>), dim3(gx, n / 64), dim3(512), 0, s, a, lda, wc, ldw,
                                m_valid, m_cap, n, k, y, ldy, 1, bias, relu_from, bn_part);
         HGNN_LAUNCH_CHECK();
         return 0;
@@ -812,9 +812,9 @@ int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int
     if (n <= 128) {
         // 64-column tiles up to 2d = 128: twice the blocks of 64 x 128 tiles, measured (round-1 GEMM lab)
         // edge forward 47.7 -> 40.7 us, node forward 34 -> 28 us
-        hipLaunchKernelGGL((k_gemm3<64, 64, 32, 2, 2, E3_FWD>), dim3(gx, ceil_div(n, 64)), dim3(256), 0, s, p);
+        HGNN_KLAUNCH((k_gemm3<64, 64, 32, 2, 2, E3_FWD>), dim3(gx, ceil_div(n, 64)), dim3(256), 0, s, p);
     } else {
-        hipLaunchKernelGGL((k_gemm3<64, 128, 32, 2, 2, E3_FWD>), dim3(gx, ceil_div(n, 128)), dim3(256), 0, s, p);
+        HGNN_KLAUNCH((k_gemm3<64, 128, 32, 2, 2, E3_FWD>), dim3(gx, ceil_div(n, 128)), dim3(256), 0, s, p);
     }
     HGNN_LAUNCH_CHECK();
     return 0;
@@ -837,8 +837,9 @@ int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, in
             return !e || e[0] != '0';
         }();
         const int gx = xcd ? ceil_div(ceil_div(m_cap, 64), 8) * 8 : ceil_div(m_cap, 64);
-        hipLaunchKernelGGL((k_gemm5<64, 64, 2, 2>), dim3(gx, ceil_div(kout, 64)), dim3(256), 0, s,
-                           dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda, xcd ? 1 : 0);
+        HGNN_KLAUNCH((k_gemm5<64, 64, 2, 2>), dim3(gx, ceil_div(kout, 64)), dim3(256), 0, s,
+                           dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda, xcd ? 1 : 0,
+                           static_cast<const float*>(nullptr), 0, static_cast<float*>(nullptr));
         HGNN_LAUNCH_CHECK();
         return 0;
     }
@@ -853,7 +854,7 @@ int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, in
     p.n = kout;
     p.c = da;
     p.ldc = ldda;
-    hipLaunchKernelGGL((k_gemm3<64, 128, 32, 2, 2, E3_STORE>), dim3(ceil_div(m_cap, 64), ceil_div(kout, 128)),
+    HGNN_KLAUNCH((k_gemm3<64, 128, 32, 2, 2, E3_STORE>), dim3(ceil_div(m_cap, 64), ceil_div(kout, 128)),
                        dim3(256), 0, s, p);
     HGNN_LAUNCH_CHECK();
     return 0;

@@ -307,7 +307,7 @@ int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const
     if (nz <= 0) return HGNN_ERR_ARG;
     if ((long long)r_cap * (lda > lddy ? lda : lddy) >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     // ring depth 2: step times 1.300-1.302 ms against 1.306-1.314 (4) and 1.313-1.323 (6), alternating runs
-    hipLaunchKernelGGL(k_gemm_bf3_tn<2>, dim3(ceil_div(o, 128), ceil_div(k, 128), nz), dim3(D_NT), 0, s, dy, lddy, a, lda,
+    HGNN_KLAUNCH(k_gemm_bf3_tn<2>, dim3(ceil_div(o, 128), ceil_div(k, 128), nz), dim3(D_NT), 0, s, dy, lddy, a, lda,
                        slabs, o, k, r_valid, nz, xcd && nz % 8 == 0 ? 1 : 0);
     HGNN_LAUNCH_CHECK();
     return 0;
@@ -322,7 +322,7 @@ int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, 
         return HGNN_ERR_UNSUPPORTED;
     if ((long long)m_cap * lda * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     const int gx = ceil_div(ceil_div(m_cap, G_BM), 8) * 8;
-    hipLaunchKernelGGL(k_gemm_bf3_fwd, dim3(gx, ceil_div(n, G_BN)), dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid,
+    HGNN_KLAUNCH(k_gemm_bf3_fwd, dim3(gx, ceil_div(n, G_BN)), dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid,
                        m_cap, n, k, y, ldy, bias, relu_from, bn_part);
     HGNN_LAUNCH_CHECK();
     return 0;

@@ -132,12 +132,15 @@ int launch_agg_bwd_pair(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t 
 
 // ---------------------------------------------------------------- GEMM (gemm3.hip, gemm_bf3.hip, repack.hip)
 // fp32 x as three bf16 parts x1 + x2 + x3 (residual below 2^-26 |x|): the operand form of the split-bf16
-// GEMM (gemm_bf3.hip)
+// GEMM (gemm_bf3.hip).  A non-finite x1 (x = +-Inf / NaN, or |x| above the bf16 maximum, which rounds to
+// Inf) keeps x2 = x3 = 0, so the GEMM sees Inf / NaN where an fp32 GEMM would, not Inf - Inf = NaN parts.
 __device__ __forceinline__ void split3(float x, __bf16& a, __bf16& b, __bf16& c) {
     a = (__bf16)x;
-    const float r = x - (float)a;
+    const float fa = (float)a;
+    const bool fin = __builtin_isfinite(fa);
+    const float r = fin ? x - fa : 0.f;
     b = (__bf16)r;
-    c = (__bf16)(r - (float)b);
+    c = (__bf16)(fin ? r - (float)b : 0.f);
 }
 __host__ __device__ inline int bf3_ld(int k) { return (k + 15) / 16 * 16; }  // plane row length (bf16)
 // The forward Conv1d-pair GEMM on bf16 MFMA (three-way split, fp32 accuracy): Y = A . B^T + bias, ReLU

@@ -386,18 +386,39 @@ Src make_src(const Program& P, void* ws, const hgnn_csr_batch* csr) {
         if (_r) return _r;      \
     } while (0)
 
-// Optional per-kernel-class event timer (bench.py times the dominant kernel
-// inside its timed region with it).  Disabled (nullptr) on the normal path.
+// Optional per-kernel-class timer (bench.py times the dominant kernel class and the aggregation classes
+// inside their timed regions with it).  Disabled (nullptr) on the normal path.  Default: every dispatch
+// of a timed class gets an event pair bound to the dispatch itself (common.h LaunchClock: its begin / end
+// timestamps, rocprofv3's kernel-trace duration); HGNN_TIMER_MARKERS=1: the round-1..4 form, marker
+// events recorded on the stream around each call (the interval also holds the next dispatch's start-up
+// and changes what the side stream's blocks share the CUs with).
 struct Timer {
     std::vector<hipEvent_t> ev;   // pairs: start, stop
     std::vector<int> cls;
     int used = 0;
     unsigned mask = 0;
+    bool markers = false;
+};
+
+struct ClockScope {  // t_clock for the launches of one TL call
+    LaunchClock c;
+    LaunchClock* prev;
+    ClockScope(Timer* tm, int k) : prev(t_clock) {
+        c = LaunchClock{tm->ev.data(), tm->cls.data(), (int)tm->cls.size(), &tm->used, k};
+        t_clock = &c;
+    }
+    ~ClockScope() { t_clock = prev; }
 };
 
 #define TL(k, x)                                                                        \
     do {                                                                                \
         const bool _t = tm && (tm->mask & (1u << (k))) && tm->used < (int)tm->cls.size(); \
+        if (_t && !tm->markers) {                                                       \
+            ClockScope _cs(tm, (k));                                                    \
+            int _r = (x);                                                               \
+            if (_r) return _r;                                                          \
+            break;                                                                      \
+        }                                                                               \
         if (_t) HGNN_HOST_CHECK(hipEventRecord(tm->ev[2 * tm->used], s));                \
         int _r = (x);                                                                   \
         if (_r) return _r;                                                              \
@@ -712,7 +733,9 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             TL(HGNN_K_DW_DENSE, launch_dw_readout(dwr, s));
             s = main_s;
         }
-        if (lgr || lpr) TL(HGNN_K_AGG_BWD, launch_readout_agg_bwd(ra, s));
+        // the readout class (k_readout_agg_bwd: R_b broadcast, no dA read), not agg_bwd: the aggregation
+        // class and its HBM roofline are the k_agg_bwd gathers of the halves
+        if (lgr || lpr) TL(HGNN_K_READOUT, launch_readout_agg_bwd(ra, s));
         if (lgr) init[P.last_gin] = 1;
         if (lpr) init[P.last_pin] = 1;
     } else if (needs_grad(P.last_gin) || needs_grad(P.last_pin) || need_dw) {
@@ -928,8 +951,25 @@ struct ReplayEntry {
     int seen = 0;
     bool failed = false;
     hipGraphExec_t exec = nullptr;
+    hipEvent_t done = nullptr;  // recorded on the caller's stream after each launch of exec
     unsigned long long last = 0;
 };
+
+// Destroy an entry's executable graph once its last launch has finished: a wait on that launch's
+// event, not a device-wide synchronisation (which would also wait for other streams, e.g. the DP
+// communication stream, and is not allowed while another stream of the device is capturing).
+static void replay_release(ReplayEntry& x) {
+    if (x.done) (void)hipEventSynchronize(x.done);
+    if (x.exec) (void)hipGraphExecDestroy(x.exec);
+    if (x.done) (void)hipEventDestroy(x.done);
+    x.exec = nullptr;
+    x.done = nullptr;
+}
+
+static int replay_launch(ReplayEntry& x, hipStream_t s) {
+    if (hipGraphLaunch(x.exec, s) != hipSuccess) return HGNN_ERR_HIP;
+    return hipEventRecord(x.done, s) == hipSuccess ? 0 : HGNN_ERR_HIP;
+}
 struct ReplayCache {
     std::vector<ReplayEntry> e;
     unsigned long long tick = 0;
@@ -985,9 +1025,7 @@ struct KeyBuilder {
 
 static int replay_reset(ReplayCache& rc, int dev) {
     if (rc.dev >= 0) {
-        (void)hipDeviceSynchronize();
-        for (auto& x : rc.e)
-            if (x.exec) (void)hipGraphExecDestroy(x.exec);
+        for (auto& x : rc.e) replay_release(x);
         if (rc.cap) (void)hipStreamDestroy(rc.cap);
     }
     rc = ReplayCache{};
@@ -1018,17 +1056,14 @@ static int replayed(std::vector<uintptr_t> key, hipStream_t s, F&& enqueue) {
         }
     if (hit && hit->exec) {
         hit->last = ++rc.tick;
-        return hipGraphLaunch(hit->exec, s) == hipSuccess ? 0 : HGNN_ERR_HIP;
+        return replay_launch(*hit, s);
     }
     if (!hit) {
         if (rc.e.size() >= REPLAY_MAX) {  // evict the least recently used entry
             size_t v = 0;
             for (size_t i = 1; i < rc.e.size(); ++i)
                 if (rc.e[i].last < rc.e[v].last) v = i;
-            if (rc.e[v].exec) {
-                (void)hipDeviceSynchronize();  // it may still run on some stream
-                (void)hipGraphExecDestroy(rc.e[v].exec);
-            }
+            replay_release(rc.e[v]);  // waits for its last launch only
             rc.e.erase(rc.e.begin() + v);
         }
         rc.e.push_back(ReplayEntry{});
@@ -1043,15 +1078,19 @@ static int replayed(std::vector<uintptr_t> key, hipStream_t s, F&& enqueue) {
     hipGraph_t gr = nullptr;
     const hipError_t ee = hipStreamEndCapture(rc.cap, &gr);
     hipGraphExec_t x = nullptr;
-    const bool ok = r == 0 && ee == hipSuccess && gr && hipGraphInstantiate(&x, gr, nullptr, nullptr, 0) == hipSuccess;
+    hipEvent_t done = nullptr;
+    const bool ok = r == 0 && ee == hipSuccess && gr && hipGraphInstantiate(&x, gr, nullptr, nullptr, 0) == hipSuccess &&
+                    hipEventCreateWithFlags(&done, hipEventDisableTiming) == hipSuccess;
     if (gr) (void)hipGraphDestroy(gr);
     if (!ok) {
         (void)hipGetLastError();
+        if (x) (void)hipGraphExecDestroy(x);
         hit->failed = true;
         return r ? r : enqueue(s);
     }
     hit->exec = x;
-    return hipGraphLaunch(x, s) == hipSuccess ? 0 : HGNN_ERR_HIP;
+    hit->done = done;
+    return replay_launch(*hit, s);
 }
 
 static int n_running(const hgnn_net_config* c) { return 2 * (c->kind == 1 ? 2 : 1) * (c->n_layers - 1); }
@@ -1157,6 +1196,7 @@ void* hgnn_timer_create(int max_launches, unsigned class_mask) {
     t->ev.resize(2 * (size_t)max_launches);
     t->cls.resize(max_launches);
     t->mask = class_mask;
+    t->markers = env_flag("HGNN_TIMER_MARKERS", false);
     for (auto& e : t->ev) {
         if (hipEventCreate(&e) != hipSuccess) {
             delete t;

@@ -20,7 +20,7 @@ int launch_repack(const RepackTable& t, hipStream_t s) {
     if (t.n <= 0) return 0;
     RepackTable u = t;
     u.y = repack_y(t);
-    hipLaunchKernelGGL(k_repack, dim3(u.n, u.y), dim3(256), 0, s, u);
+    HGNN_KLAUNCH(k_repack, dim3(u.n, u.y), dim3(256), 0, s, u);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -150,13 +150,13 @@ int launch_dw_reduce2(const float* slabs, const int* r_valid, int nz, int o, int
     // slab groups by the slab count: more groups when there are many slabs per output
     const int nb = dbpart ? o_real : 0;
     if (total % 4 == 0 && ((long long)o * k) % 4 == 0 && ((uintptr_t)slabs & 15) == 0) {
-        hipLaunchKernelGGL(k_dw_reduce4, dim3(ceil_div(total, 256) + nb), dim3(256), 0, s, slabs, r_valid, nz, o, o_real,
+        HGNN_KLAUNCH(k_dw_reduce4, dim3(ceil_div(total, 256) + nb), dim3(256), 0, s, slabs, r_valid, nz, o, o_real,
                            k, split, dw0, dw1, dbpart, db0, db1);
     } else if (nz > 32) {
-        hipLaunchKernelGGL(k_dw_reduce2<16>, dim3(ceil_div(total, 16) + nb), dim3(256), 0, s, slabs, r_valid, nz,
+        HGNN_KLAUNCH(k_dw_reduce2<16>, dim3(ceil_div(total, 16) + nb), dim3(256), 0, s, slabs, r_valid, nz,
                            o, o_real, k, split, dw0, dw1, dbpart, db0, db1);
     } else {
-        hipLaunchKernelGGL(k_dw_reduce2<4>, dim3(ceil_div(total, 64) + nb), dim3(256), 0, s, slabs, r_valid, nz,
+        HGNN_KLAUNCH(k_dw_reduce2<4>, dim3(ceil_div(total, 64) + nb), dim3(256), 0, s, slabs, r_valid, nz,
                            o, o_real, k, split, dw0, dw1, dbpart, db0, db1);
     }
     HGNN_LAUNCH_CHECK();

@@ -87,7 +87,7 @@ int launch_plan(const int64_t* nb, const int64_t* eb, int bs, int nmax, int emax
     RepackTable t{};
     if (rt) t = *rt;
     t.y = repack_y(t);
-    hipLaunchKernelGGL(k_plan, dim3(1 + t.n * t.y), dim3(256), 0, s, nb, eb, bs, nmax, emax, m, t);
+    HGNN_KLAUNCH(k_plan, dim3(1 + t.n * t.y), dim3(256), 0, s, nb, eb, bs, nmax, emax, m, t);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -498,16 +498,16 @@ static void extract_lds_launch(const ExtractArgs& a, size_t lds, hipStream_t s) 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_extract_lds<JT>, dim3(a.bs, a.dual ? 2 : 1), dim3(XL_THREADS), lds, s, a);
+    HGNN_KLAUNCH(k_extract_lds<JT>, dim3(a.bs, a.dual ? 2 : 1), dim3(XL_THREADS), lds, s, a);
 }
 
 static int extract_one(const ExtractArgs& a, dim3 grid, hipStream_t s) {
     switch (a.jtot) {
-        case 3: hipLaunchKernelGGL(k_extract<3>, grid, dim3(X_THREADS), 0, s, a); break;
-        case 4: hipLaunchKernelGGL(k_extract<4>, grid, dim3(X_THREADS), 0, s, a); break;
-        case 5: hipLaunchKernelGGL(k_extract<5>, grid, dim3(X_THREADS), 0, s, a); break;
-        case 6: hipLaunchKernelGGL(k_extract<6>, grid, dim3(X_THREADS), 0, s, a); break;
-        case 7: hipLaunchKernelGGL(k_extract<7>, grid, dim3(X_THREADS), 0, s, a); break;
+        case 3: HGNN_KLAUNCH(k_extract<3>, grid, dim3(X_THREADS), 0, s, a); break;
+        case 4: HGNN_KLAUNCH(k_extract<4>, grid, dim3(X_THREADS), 0, s, a); break;
+        case 5: HGNN_KLAUNCH(k_extract<5>, grid, dim3(X_THREADS), 0, s, a); break;
+        case 6: HGNN_KLAUNCH(k_extract<6>, grid, dim3(X_THREADS), 0, s, a); break;
+        case 7: HGNN_KLAUNCH(k_extract<7>, grid, dim3(X_THREADS), 0, s, a); break;
         default: return 2;
     }
     HGNN_LAUNCH_CHECK();
@@ -572,7 +572,7 @@ __global__ void k_pack_nodes(const float* __restrict__ X, int f, int nmax, Batch
 
 int launch_pack_nodes(const float* X, int bs, int f, int nmax, BatchMeta m, float* out,
                       hipStream_t s) {
-    hipLaunchKernelGGL(k_pack_nodes, dim3(bs), dim3(128), 0, s, X, f, nmax, m, out);
+    HGNN_KLAUNCH(k_pack_nodes, dim3(bs), dim3(128), 0, s, X, f, nmax, m, out);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -586,7 +586,7 @@ __global__ void k_pack_edges(const float* __restrict__ XL, int emax, BatchMeta m
 }
 
 int launch_pack_edges(const float* XL, int bs, int emax, BatchMeta m, float* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_pack_edges, dim3(bs), dim3(128), 0, s, XL, emax, m, out);
+    HGNN_KLAUNCH(k_pack_edges, dim3(bs), dim3(128), 0, s, XL, emax, m, out);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -605,7 +605,7 @@ __global__ void k_unpack_nodes(const float* __restrict__ in, int f, int nmax, Ba
 
 int launch_unpack_nodes(const float* in, int bs, int f, int nmax, BatchMeta m, float* X,
                         hipStream_t s) {
-    hipLaunchKernelGGL(k_unpack_nodes, dim3(bs), dim3(128), 0, s, in, f, nmax, m, X);
+    HGNN_KLAUNCH(k_unpack_nodes, dim3(bs), dim3(128), 0, s, in, f, nmax, m, X);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

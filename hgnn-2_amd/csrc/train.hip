@@ -138,7 +138,7 @@ extern "C" {
 int hgnn_mse_loss(const float* d_out, const float* d_t, int n, float t_mean, float t_std, float* d_stats,
                   float* d_dout, void* stream) {
     if (!d_out || !d_t || !d_stats || n < 0) return HGNN_ERR_ARG;
-    hipLaunchKernelGGL(k_mse_loss, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), d_out, d_t, n, t_mean,
+    HGNN_KLAUNCH(k_mse_loss, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), d_out, d_t, n, t_mean,
                        t_std, d_stats, d_dout);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
@@ -147,7 +147,7 @@ int hgnn_mse_loss(const float* d_out, const float* d_t, int n, float t_mean, flo
 int hgnn_xent_loss(const float* d_out, const float* d_t, int n, int c, float* d_stats, float* d_dout,
                    uint32_t* d_err, void* stream) {
     if (!d_out || !d_t || !d_stats || !d_err || n < 0 || c < 1) return HGNN_ERR_ARG;
-    hipLaunchKernelGGL(k_xent_loss, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), d_out, d_t, n, c,
+    HGNN_KLAUNCH(k_xent_loss, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), d_out, d_t, n, c,
                        d_stats, d_dout, d_err);
     HGNN_LAUNCH_CHECK();
     return HGNN_OK;
@@ -181,7 +181,7 @@ int hgnn_adamax_step(int n_tensors, float* const* params, const float* const* gr
         }
         tab.start[tab.count] = blocks;
         if (blocks == 0) continue;
-        hipLaunchKernelGGL(k_adamax, dim3(blocks), dim3(256), 0, s, tab, lr_c, w, (float)beta2, (float)eps,
+        HGNN_KLAUNCH(k_adamax, dim3(blocks), dim3(256), 0, s, tab, lr_c, w, (float)beta2, (float)eps,
                            (float)weight_decay);
         HGNN_LAUNCH_CHECK();
     }

@@ -31,6 +31,7 @@ from .net import (_capturing, _require_cuda, _f32, _i64, _raise_bits, check_erro
 # kernels (csrc/ccn_small.hip, csrc/ccn2_small.hip): no plan, no workspace sizing, 1 + 1 dispatches per call
 # for one graph.  HGNN_CCN_SMALL=0 (or setting this to False) keeps every call on the general path.
 SMALL = os.environ.get("HGNN_CCN_SMALL", "1") != "0"
+SMALL2_WS_CAP = 512 << 20  # bytes: the CCN-2D small path's workspace bound per call (CcnSpec.small)
 
 CCN_MAX_DEGREE = {1: 1024, 2: 256}  # csrc/ccn.hip CCN1_MAXD, CCN_BIGD (by order)
 CCN2_MAX_CHANNELS = 16  # csrc/ccn.hip C2_CMAX_WIDE: CCN-2D f_in and hidden
@@ -58,6 +59,11 @@ class CcnSpec:
             lib = L.lib()
             c = (cfg, lib.hgnn_ccn_small_workspace_bytes(ctypes.byref(cfg))) \
                 if lib.hgnn_ccn_small_supported(ctypes.byref(cfg)) else False
+            # CCN-2D's small path reserves (L + 2) nmax^3 hidden floats per graph for its levels (~0.8 MB
+            # per QM9 graph at L = 2, ~30x the rows the graph uses): batches beyond SMALL2_WS_CAP of
+            # workspace go to the general path, whose workspace follows the batch's real sum of d^2
+            if c and self.order == 2 and c[1] > SMALL2_WS_CAP:
+                c = False
             self._small[key] = c
         return c or None
 

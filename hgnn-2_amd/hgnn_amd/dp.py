@@ -19,9 +19,10 @@ which tests/test_dp_cpu.py and tests/test_gpu_dp.py check.
   bucket while the earlier layers are still being differentiated.  The
   gradients are written by the executor straight into one flat buffer, so the
   collective needs no packing copies.
-* average_running_stats: the BN running statistics (plain attributes, not
-  state, batch_normalization.py:30-38) averaged across ranks after a step, so
-  every rank -- and a checkpoint written by rank 0 -- holds the same eval-mode
+* BN running statistics (plain attributes, not state, batch_normalization.py:30-38)
+  averaged across ranks in every step -- LayerBucketAllReduce carries them in the
+  last layer's bucket, average_running_stats is the stand-alone collective -- so
+  every rank, and a checkpoint written by rank 0, holds the same eval-mode
   statistics.
 * GradAllReduce: the single flat all-reduce for any module (used by TrainStep
   when no executor events are available).
@@ -128,7 +129,9 @@ class LayerBucketAllReduce:
     into self.flat and records the per-layer events.  Call the object after loss.backward():
     it enqueues, last layer first, a wait on the layer's events and the all-reduce of its
     bucket on a communication stream, then joins that stream and divides by the world size.
-    sync_running=True also averages the BN running statistics.
+    sync_running=True also averages the BN running statistics: they are copied into the tail of the
+    flat buffer (the last layer's bucket, reduced first) and back after the division, so the step
+    has no collective beyond the gradient buckets.
 
     Gradient accumulation: the overlapped path needs every p.grad to be None at backward time
     (optimizer.zero_grad(), whose default is set_to_none=True).  When a p.grad is present
@@ -148,17 +151,23 @@ class LayerBucketAllReduce:
         per = 12 if spec.kind == 1 else 6
         n_layers = spec.n_layers - 1
         sizes = [p.numel() for p in self.params]
-        self.flat = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
+        # the BN running statistics ride at the end of the buffer, in the last layer's bucket (the first
+        # one reduced): averaged by the gradients' own collectives, no second collective per step
+        self.n_run = sum(t.numel() for t in running_stats(model)) if sync_running else 0
+        self.n_grad = sum(sizes)
+        self.flat = torch.zeros(self.n_grad + self.n_run, dtype=torch.float32, device=dev)
+        self.run_tail = self.flat[self.n_grad:]
         self.views = []
         off = 0
         for p, k in zip(self.params, sizes):
             self.views.append(self.flat[off:off + k].view_as(p))
             off += k
-        # bucket l = layer l's parameters; the fc pair joins the last layer's bucket
+        # bucket l = layer l's parameters; the fc pair and the running statistics join the last layer's bucket
         self.buckets = []
         off = 0
         for l in range(n_layers):
-            n = sum(sizes[l * per:(l + 1) * per]) + (sizes[-2] + sizes[-1] if l == n_layers - 1 else 0)
+            last = l == n_layers - 1
+            n = sum(sizes[l * per:(l + 1) * per]) + (sizes[-2] + sizes[-1] + self.n_run if last else 0)
             self.buckets.append((off, n))
             off += n
         assert off == self.flat.numel()
@@ -203,15 +212,25 @@ class LayerBucketAllReduce:
         self.fresh = False
         if world == 1:
             return
+        run = running_stats(self.model) if self.n_run else []
+        if run and sum(t.numel() for t in run) != self.n_run:
+            raise RuntimeError("LayerBucketAllReduce: the model's BN running statistics changed size")
+
+        def pack_running():
+            # the running statistics are final once the forward has run (the executor updates them in place)
+            if run:
+                torch._foreach_copy_(self._tail_views(run), run)
         cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         if fresh or cur is None:
             # no per-layer events this step: one collective over the whole buffer after the backward
             if cur is not None:
                 self.comm.wait_stream(cur)
                 with torch.cuda.stream(self.comm):
+                    pack_running()
                     dist.all_reduce(self.flat, group=self.group)
                 cur.wait_stream(self.comm)
             else:
+                pack_running()
                 dist.all_reduce(self.flat, group=self.group)
         else:
             mk = None
@@ -219,12 +238,15 @@ class LayerBucketAllReduce:
                 mk = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
                 mk[0].record(cur)
             for l in reversed(range(len(self.buckets))):
+                # the events are recorded in the backward, after the forward that wrote the running statistics
                 self.comm.wait_event(self.events[2 * l])
                 self.comm.wait_event(self.events[2 * l + 1])
                 if mk is not None and l == len(self.buckets) - 1:
                     mk[1].record(self.comm)
                 off, n = self.buckets[l]
                 with torch.cuda.stream(self.comm):
+                    if l == len(self.buckets) - 1:
+                        pack_running()
                     dist.all_reduce(self.flat[off:off + n], group=self.group)
             if mk is not None:
                 mk[2].record(self.comm)
@@ -233,8 +255,16 @@ class LayerBucketAllReduce:
                 mk[3].record(cur)
                 self.marks.append(mk)
         self.flat.div_(world)
-        if self.sync_running:
-            average_running_stats(self.model, self.group)
+        if run:
+            torch._foreach_copy_(run, self._tail_views(run))
+
+    def _tail_views(self, run):
+        out = []
+        off = 0
+        for t in run:
+            out.append(self.run_tail[off:off + t.numel()].view_as(t))
+            off += t.numel()
+        return out
 
     def timing_summary(self):
         """Mean over the timed calls (ms): 'span' from the first bucket's collective start to the

@@ -359,11 +359,14 @@ _checked_last = [None, None]  # (signature, parameter list) of the last call tha
 def _checked_params(spec, f_in, jt, dev):
     """Every parameter's shape against the widths the executor will read (the C ABI gets bare
     pointers: a mismatch would be an out-of-bounds device read), dtype and device.  A call with the same
-    parameter objects at the same storage addresses, widths and device as the last one that passed
-    returns its list without re-checking (~70 us of host time per forward)."""
+    parameter objects at the same storage addresses, shapes, dtypes, contiguity, widths and device as the
+    last one that passed returns its list without re-checking (~70 us of host time per forward)."""
     params = spec.params
+    # shape, dtype and contiguity too: an in-place metadata change at the same address (p.data = a view,
+    # resize_, a dtype view) must not hit the cache
     sig = (spec.kind, spec.order, spec.d, spec.n_layers, spec.dim_out, f_in, jt, dev,
-           tuple(map(id, params)), tuple(p.data_ptr() for p in params))
+           tuple(map(id, params)),
+           tuple((p.data_ptr(), tuple(p.shape), p.dtype, p.is_contiguous()) for p in params))
     if _checked_last[0] == sig:
         return _checked_last[1]
     out = _check_params(spec, f_in, jt, dev)

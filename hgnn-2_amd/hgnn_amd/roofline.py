@@ -73,7 +73,9 @@ def class_work(kcls, counts, order, f_in, d, n_layers, jt=3):
             fl += 2.0 * r * c2 * k
             by += 4.0 * (r * c2 + r * k + c2 * k)
     elif kcls in (K_AGG_FWD, K_AGG_BWD):
-        items = [(e, k, cg, cp) for e, k, cg, cp in halves] + [(False, k_last, c2, c2)]
+        # the last layer's forward aggregation is a k_agg_fwd launch; its backward is the readout class
+        # (k_readout_agg_bwd: the readout gradient R_b broadcast per graph, no [rows][K] dA read)
+        items = [(e, k, cg, cp) for e, k, cg, cp in halves] + ([(False, k_last, c2, c2)] if kcls == K_AGG_FWD else [])
         for edge, k, cg, cp in items:
             r, ro = rows(edge), rows(not edge)
             s_bytes = 8.0 * (r + r) + 16.0 * (nnz_g(edge) + counts["nnz_p"])
@@ -106,7 +108,7 @@ def agg_requested_bytes(kcls, counts, order, f_in, d, n_layers, jt=3):
             by += 4.0 * (nnz_g(edge) * cg + counts["nnz_p"] * cp + r * k) + 8.0 * 2 * r + 16.0 * (
                 nnz_g(edge) + counts["nnz_p"])
     elif kcls == K_AGG_BWD:
-        for edge, k, cg, cp in halves + [(False, k_last, c2, c2)]:
+        for edge, k, cg, cp in halves:
             r, ro = rows(edge), rows(not edge)
             by += 4.0 * ((nnz_g(edge) + r) * cg + 2 * counts["nnz_p"] * cp + r * cg + ro * cp) + 8.0 * (r + ro) + 16.0 * (
                 nnz_g(edge) + counts["nnz_p"])
@@ -142,7 +144,7 @@ CLASS_KERNELS = {
     K_AGG_FWD: ("k_agg_fwd",),
     K_GEMM_FWD: ("k_gemm3<", "k_gemm_fwd", "k_gemm_bf3_fwd", "k_gemm5<"),
     K_BN_FWD: ("k_bn_finalize", "k_bn_apply"),
-    K_READOUT: ("k_readout",),
+    K_READOUT: ("k_readout",),  # incl. k_readout_agg_bwd (net.hip times it in this class)
     K_BN_BWD: ("k_bn_bwd",),
     K_GEMM_DW: ("k_gemm3_tn", "k_gemm_dw", "k_gemm_bf3_tn"),
     K_GEMM_DA: ("k_gemm3<", "k_gemm_da", "k_gemm5<"),
@@ -208,6 +210,12 @@ def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, s
         achieved = by * steps / sec / 1e9
         peak, unit, bound = PEAK_HBM_GBS, "GB/s", "hbm"
     per_launch = launches / max(steps, 1)
+    traffic = pmc_traffic(kcls, pmc_path)
+    avg_s = ms_total / 1e3 / max(launches, 1)
+    if traffic is not None and bound == "hbm":
+        # the HBM bytes the PMC counters saw per launch, over the same per-launch time
+        extra["traffic_gbs"] = round(traffic / avg_s / 1e9, 1)
+        extra["traffic_frac"] = round(traffic / avg_s / 1e9 / PEAK_HBM_GBS, 4)
     if kcls in (K_AGG_FWD, K_AGG_BWD):
         rq = agg_requested_bytes(kcls, counts, order, f_in, d, n_layers, jt)
         rq_gbs = rq * steps / sec / 1e9
@@ -220,7 +228,7 @@ def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, s
         "peak": peak,
         "unit": unit,
         "frac": round(achieved / peak, 4),
-        "traffic": pmc_traffic(kcls, pmc_path),
+        "traffic": traffic,
         "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_traffic.json)",
         "algorithmic_bytes_per_launch": by / max(per_launch, 1e-9),
         "launches_per_step": per_launch,

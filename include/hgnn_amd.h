@@ -321,17 +321,21 @@ int hgnn_ccn_backward(const hgnn_ccn_config* cfg, const long long* sums, const f
  * builds the receptive fields, runs every level and the readout -- no plan, no host sync, one
  * dispatch forward, one backward (+ one reduction over the graphs when bs > 1).  The per-graph
  * drop-in call of scripts/train_ccn.py:31-73 (net(X, A + I) per graph) and QM9-size batches.  Same
- * layouts and results as hgnn_ccn_forward / _backward: outputs and dX in the same fp32 order (order 2:
- * the weight gradients too; order 1 sums them in a different order).  d_n_batch may be NULL (every
+ * layouts and results as hgnn_ccn_forward / _backward: outputs and dX in the same fp32 order (order 2
+ * at bs = 1: the weight gradients too -- a batch of several graphs reduces its per-node parameter
+ * partials in another order; order 1 sums them in a different order).  d_n_batch may be NULL (every
  * graph has nmax nodes).
  * supported: 1 if cfg fits (order 1: the LDS of the backward, 4 nmax^2 (hidden L + 2 max(f_in, hidden)
  * + 2 hidden) + 8 KB, within 160 KB; order 2: 8 waves x (6.5 KB + 10 nmax^2 B) + 8 KB), else 0 (use
- * the general path).  Order 2's workspace holds each graph's levels (nmax^3 rows per level bound).
+ * the general path).  Order 2's workspace holds each graph's levels at a bound of nmax^3 rows per
+ * level: (L + 2) nmax^3 hidden floats per graph (about 4 MB per graph at nmax = 32, L = 15) -- the
+ * Python layer sends batches above 512 MB of that region to the general path (hgnn_amd/ccn.py).
  * Validation (self loops, symmetric pattern, 0 <= n_b <= nmax): a graph with bits stores
- * *d_err = tag * 256 + bits (0 < tag < 2^23; nothing is stored when the batch is valid), so a caller
- * that increases tag per call never zeroes the word and reads a new error as a tag above the last one
- * it reported.  d_err may be the device alias of a host-mapped word (hgnn_host_word_alloc): the
- * check is then a host read, with no copy or event per call.
+ * *d_err = tag * 256 + bits (0 < tag < 2^23, a plain store; nothing is stored when the batch is valid;
+ * tag only labels the store).  The caller reports any nonzero word and clears it (clear-on-report): a
+ * store that lands between the caller's read and its clear is lost.  d_err may be the device alias of
+ * a host-mapped word (hgnn_host_word_alloc): the check is then a host read, with no copy or event per
+ * call.
  * The workspace holds the readout features between forward and backward. */
 int hgnn_ccn_small_supported(const hgnn_ccn_config* cfg);
 /* A 64-byte host-mapped, coherent word block (zeroed): *host_ptr for the host, *dev_ptr for kernels. */

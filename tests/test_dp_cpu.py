@@ -102,3 +102,66 @@ def test_shard_graphs_balanced_partition():
         counts = [len(s) for s in sh]
         assert max(counts) - min(counts) <= max(1, len(costs) // (world * 20)), counts
     assert shard_graphs([3, 1, 2], 2) == [[0], [1, 2]]
+
+
+def _bucket_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "hgnn-2_amd"))
+    from hgnn_amd.dp import LayerBucketAllReduce, running_stats
+    from models.gnns.model_mnb import GNN_lg
+    torch.manual_seed(0)
+    m = GNN_lg(0, 8, 3, 5, 1, 1, 2)
+    ar = LayerBucketAllReduce(m)
+    g = torch.Generator().manual_seed(100 + rank)
+    for p in m.parameters():
+        p.grad = torch.randn(p.shape, generator=g)
+    for t in running_stats(m):
+        t.copy_(torch.randn(t.shape, generator=g))
+    ar.grad_targets()  # p.grad present: the one-collective (fresh) path, as after accumulated backwards
+    ar()
+    if rank == 0:
+        q.put(({k: p.grad.numpy().copy() for k, p in m.named_parameters()},
+               [t.numpy().copy() for t in running_stats(m)], ar.buckets[-1], ar.n_grad, ar.n_run))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world3_layer_buckets_carry_running_stats():
+    """LayerBucketAllReduce's CPU path (the fresh-gradient form, one collective): gradients and the BN
+    running statistics -- carried in the tail of the last layer's bucket, no second collective --
+    come out as the average over three ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    grads, run, last_bucket, n_grad, n_run = q.get(timeout=300)
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "hgnn-2_amd"))
+    from hgnn_amd.dp import running_stats
+    from models.gnns.model_mnb import GNN_lg
+    torch.manual_seed(0)
+    m = GNN_lg(0, 8, 3, 5, 1, 1, 2)
+    names = [k for k, _ in m.named_parameters()]
+    want_g = {k: torch.zeros(p.shape) for k, p in m.named_parameters()}
+    want_r = [torch.zeros(t.shape) for t in running_stats(m)]
+    for r in range(world):
+        g = torch.Generator().manual_seed(100 + r)
+        for k in names:
+            want_g[k] += torch.randn(want_g[k].shape, generator=g) / world
+        for w in want_r:
+            w += torch.randn(w.shape, generator=g) / world
+    for k in names:
+        assert torch.allclose(torch.from_numpy(grads[k]), want_g[k], rtol=1e-6, atol=1e-7), k
+    for got_t, w in zip(run, want_r):
+        assert torch.allclose(torch.from_numpy(got_t), w, rtol=1e-6, atol=1e-7)
+    off, n = last_bucket
+    assert off + n == n_grad + n_run and n_run == sum(w.numel() for w in want_r)

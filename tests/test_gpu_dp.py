@@ -1,10 +1,10 @@
-"""World-size-2 data parallelism with the real HIP executor (SURVEY.md §8 e).
+"""World-size-2 and -8 data parallelism with the real HIP executor (SURVEY.md §8 e).
 
-Two ranks (gloo on GPU tensors, both on cuda:0) take Σ(N+M)-balanced shards of one global batch
+Two (or eight: config 4's 4096-graph global batch) ranks (gloo on GPU tensors, all on cuda:0) take Σ(N+M)-balanced shards of one global batch
 (hgnn_amd.dp.shard_graphs), run GNN_lg forward + backward through the executor with the per-layer
 bucketed all-reduce (hgnn_amd.dp.LayerBucketAllReduce: the executor writes the gradients into the
 flat buffer and records per-layer events that the communication stream waits on) and average
-their BN running statistics.  Checked against the fp64 oracle run on each shard (oracle/ref_mnb.py):
+their BN running statistics (carried in the last layer's bucket).  Checked against the fp64 oracle run on each shard (oracle/ref_mnb.py):
 "2 reference batches, gradients averaged" -- the semantics of gradient-only DP (the reference itself
 has one batch: models/layers/batch_normalization.py:80-93).
 """
@@ -154,29 +154,32 @@ def test_world2_bucketed_allreduce_matches_shard_average(mode):
         assert np.array_equal(got[0]["grad." + k], got[1]["grad." + k]), k
 
 
-def test_world2_config4_rank_shape_d128():
-    """Config 4's per-rank shape: GNN_lg d=128, 5 layers, 512 graphs per rank (a global batch of
-    1024 split in two Σ(N+M)-balanced shards), one step with the overlapped per-layer buckets;
-    the averaged gradients and running statistics against the fp64 oracle's two-shard average."""
+def _run_world(world, d, nl, ng, timeout=300):
+    """Start `world` ranks of _worker on cuda:0 (one step, p.grad None), compute the fp64 oracle of every
+    shard in this process while they run, then collect the ranks' gradients and running statistics."""
     import multiprocessing as mp
-    d, nl, ng = 128, 5, 1024
     ctx = mp.get_context("forkserver")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, "none", (d, nl, ng, 1))) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, "none", (d, nl, ng, 1))) for r in range(world)]
     for pr in procs:
         pr.start()
-    got = dict(q.get(timeout=300) for _ in range(2))
+    graphs, shards = _shards(world, ng)
+    oracle = [_oracle_shard(graphs, shards[r], d, nl, 1) for r in range(world)]
+    got = dict(q.get(timeout=timeout) for _ in range(world))
     for pr in procs:
         pr.join(timeout=120)
         assert pr.exitcode == 0
-    graphs, shards = _shards(2, ng)
-    assert sorted(shards[0] + shards[1]) == list(range(ng))
-    assert abs(len(shards[0]) - len(shards[1])) <= 16
-    (g0, s0), (g1, s1) = (_oracle_shard(graphs, shards[r], d, nl, 1) for r in (0, 1))
-    ref = {k: (g0[k] + g1[k]) / 2 for k in g0}
+    return graphs, shards, oracle, got
+
+
+def _check_world(world, nl, shards, oracle, got, ng):
+    """Every rank's gradients against the fp64 oracle's shard average (SURVEY.md §8 c gradient bound),
+    running statistics against the average of the shards' running statistics, all ranks identical."""
+    assert sorted(i for s in shards for i in s) == list(range(ng))
+    ref = {k: sum(g[k] for g, _ in oracle) / world for k in oracle[0][0]}
     gmax = max(v.abs().max().item() for v in ref.values())
-    for r in (0, 1):
+    for r in range(world):
         res = got[r]
         assert res["flat_is_grad"]
         for k, v in ref.items():
@@ -186,8 +189,31 @@ def test_world2_config4_rank_shape_d128():
         for l in range(nl - 1):
             for nm in ("bn1", "bn2"):
                 for key in ("running_mean", "running_std"):
-                    want = ((s0[f"layer{l}.{nm}"][key] + s1[f"layer{l}.{nm}"][key]) / 2).numpy()
+                    want = (sum(s[f"layer{l}.{nm}"][key] for _, s in oracle) / world).numpy()
                     np.testing.assert_allclose(res["running"][i], want, rtol=1e-4, atol=1e-5)
                     i += 1
     for k in ref:
-        assert np.array_equal(got[0]["grad." + k], got[1]["grad." + k]), k
+        for r in range(1, world):
+            assert np.array_equal(got[0]["grad." + k], got[r]["grad." + k]), (r, k)
+
+
+def test_world2_config4_rank_shape_d128():
+    """Config 4's per-rank shape: GNN_lg d=128, 5 layers, 512 graphs per rank (a global batch of
+    1024 split in two Σ(N+M)-balanced shards), one step with the overlapped per-layer buckets;
+    the averaged gradients and running statistics against the fp64 oracle's two-shard average."""
+    d, nl, ng = 128, 5, 1024
+    graphs, shards, oracle, got = _run_world(2, d, nl, ng)
+    assert abs(len(shards[0]) - len(shards[1])) <= 16
+    _check_world(2, nl, shards, oracle, got, ng)
+
+
+def test_world8_config4_global_batch_4096_d128():
+    """Config 4 itself on one device: 8 ranks (gloo over device tensors), GNN_lg d=128, 5 layers, one
+    global batch of 4096 QM9-shape graphs in 8 Σ(N+M)-balanced shards of ~512, one step with the
+    per-layer buckets and the running statistics in the same collectives.  Gradients and running
+    statistics against the fp64 oracle's 8-shard average ("8 reference batches, gradients averaged",
+    models/layers/batch_normalization.py:80-93), all 8 ranks bitwise identical."""
+    d, nl, ng, world = 128, 5, 4096, 8
+    graphs, shards, oracle, got = _run_world(world, d, nl, ng, timeout=600)
+    assert max(len(s) for s in shards) - min(len(s) for s in shards) <= 16
+    _check_world(world, nl, shards, oracle, got, ng)
