@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bs", type=int, default=512, help="graphs per GPU")
-    ap.add_argument("--d", type=int, default=64)
+    ap.add_argument("--d", "--dim", dest="d", type=int, default=64)
     ap.add_argument("--layers", type=int, default=5)
     ap.add_argument("--order", type=int, default=2)
     ap.add_argument("--settle-s", type=float, default=1.0,
@@ -175,7 +175,8 @@ def launch_ranks(n):
     import subprocess
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.abspath(__file__)] + sys.argv[1:]
+           os.path.abspath(__file__)] + ["--dim" if a == "--d" else a for a in sys.argv[1:]]
+    # (torch.distributed.run's own parser takes "--d" for an ambiguous abbreviation of its options)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
@@ -297,7 +298,16 @@ def main():
     # comparable with the rocprofv3 trace of the same command
     hbm_classes = [RF.K_AGG_FWD, RF.K_AGG_BWD]
     timed = ([dominant] + [k for k in hbm_classes if k != dominant]) if dominant is not None else []
-    timers = {k: KernelTimer(max(1, per[k][1] // prof_steps * args.steps + 8), [k]) for k in timed}
+    # in-kernel stamps (HGNN_TIMER_STAMPS): each wave of a timed launch writes its entry / exit time, nothing
+    # is added to the stream -- event pairs around a dispatch make that dispatch itself slower (the
+    # aggregation backward 19 -> 30 us per launch inside rocprofv3's own trace of a round-5 bench run)
+    from hgnn_amd.net import TIMER_STAMPS
+    wave_bound = 2 * (X.shape[0] * (X.shape[2] + XL.shape[2])) + 16384  # waves of the largest timed launch
+
+    def stamp_timer(k, steps_):
+        n = max(1, per[k][1] // prof_steps * steps_ + 8)
+        return KernelTimer(n, [k], mode=TIMER_STAMPS, stamp_words=2 * n * wave_bound)
+    timers = {k: stamp_timer(k, args.steps) for k in timed}
     graph = None
     if args.graph:
         # The step (~90 kernel launches + Python autograd) is captured once and replayed; every
@@ -377,8 +387,9 @@ def main():
         ms, n = timer_ms[dominant]
         roof = RF.roofline_entry(dominant, ms, n, counts, args.order, 5, args.d, args.layers, args.steps, pmc_path=pmc)
         roof["traffic_source"] = traffic_note
-        roof["timed_in"] = (f"a region of its own: {args.steps} eager steps with HIP events around this class's "
-                            "launches only (each aggregation class in another such region)")
+        roof["timed_in"] = (f"a region of its own: {args.steps} eager steps, every wave of this class's launches "
+                            "stamping s_memrealtime at entry and exit (a launch = last exit - first entry; no "
+                            "events in the stream); each aggregation class in another such region")
         roof["class_ms_per_step_profile"] = {RF.NAMES[k]: round(v[0] / prof_steps, 4) for k, v in per.items()}
         roof_hbm = {}
         for k in hbm_classes:
@@ -407,7 +418,8 @@ def main():
             fwd()
         torch.cuda.synchronize()
         fms = (time.perf_counter() - t0) * 1e3 / args.steps
-        with KT(4096, [RF.K_AGG_FWD]) as tf:
+        nl = (args.layers * 2) * args.steps + 8  # aggregation launches of the forwards, with room
+        with KT(nl, [RF.K_AGG_FWD], mode=TIMER_STAMPS, stamp_words=2 * nl * wave_bound) as tf:
             for _ in range(args.steps):
                 fwd()
             torch.cuda.synchronize()

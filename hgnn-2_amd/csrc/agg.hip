@@ -143,6 +143,7 @@ struct LaneBn {
 
 template <int JT, int CG, int CP, bool V>
 __global__ void __launch_bounds__(AGG_NT) k_agg_fwd(AggFwdArgs a) {
+    WaveStamp stamp(a.stamps);
     const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * AGG_WV + (threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     if (r >= *a.total_rows) return;
@@ -265,7 +266,9 @@ static int cpl_of(int c) {
 }
 
 template <int JT, int CG, int CP>
-static void agg_fwd_v(const AggFwdArgs& a, dim3 g, hipStream_t s) {
+static void agg_fwd_v(const AggFwdArgs& a0, dim3 g, hipStream_t s) {
+    AggFwdArgs a = a0;
+    a.stamps = clock_stamps((long long)g.x * AGG_WV);
     const int kk = JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
     const bool v = (CG == 0 || vec_ok(CG, a.cg, a.xg, {})) && (CP == 0 || vec_ok(CP, a.cp, a.xp, {})) &&
                    (CG == 0 || vec_ok(CG, a.cg, a.out, {a.ldo, (long long)kk})) &&
@@ -431,6 +434,7 @@ __device__ __forceinline__ void agg_bwd_p(const AggBwdArgs& a, int r, int lane) 
 // MODE 1: G only (ga); 2: P only (pa); 3: blocks [0, gb) G on ga, the rest P on pa.
 template <int JT, int CG, int CP, bool V, int MODE>
 __global__ void __launch_bounds__(AGG_NT) k_agg_bwd(AggBwdArgs ga, AggBwdArgs pa, int gb) {
+    WaveStamp stamp(ga.stamps);
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     if (MODE == 1 || (MODE == 3 && (int)blockIdx.x < gb)) {
@@ -456,8 +460,10 @@ static bool bwd_vec_p(int cpl, const AggBwdArgs& a) {
 }
 
 template <int JT, int C>
-static int agg_bwd_single(const AggBwdArgs& a, hipStream_t s) {
-    const dim3 g(ceil_div(a.cap_rows, AGG_WV));
+static int agg_bwd_single(const AggBwdArgs& a0, hipStream_t s) {
+    const dim3 g(ceil_div(a0.cap_rows, AGG_WV));
+    AggBwdArgs a = a0;
+    a.stamps = clock_stamps((long long)g.x * AGG_WV);
     if (a.ing) {
         if (bwd_vec_g(C, a)) HGNN_KLAUNCH((k_agg_bwd<JT, C, C, true, 1>), g, dim3(AGG_NT), 0, s, a, a, 0);
         else HGNN_KLAUNCH((k_agg_bwd<JT, C, C, false, 1>), g, dim3(AGG_NT), 0, s, a, a, 0);
@@ -494,8 +500,10 @@ int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s) {
 }
 
 template <int JT, int C>
-static int agg_bwd_pair_c(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t s) {
-    const int gb = ceil_div(ga.cap_rows, AGG_WV), pb = ceil_div(pa.cap_rows, AGG_WV);
+static int agg_bwd_pair_c(const AggBwdArgs& ga0, const AggBwdArgs& pa, hipStream_t s) {
+    const int gb = ceil_div(ga0.cap_rows, AGG_WV), pb = ceil_div(pa.cap_rows, AGG_WV);
+    AggBwdArgs ga = ga0;
+    ga.stamps = clock_stamps((long long)(gb + pb) * AGG_WV);
     HGNN_KLAUNCH((k_agg_bwd<JT, C, C, true, 3>), dim3(gb + pb), dim3(AGG_NT), 0, s, ga, pa, gb);
     HGNN_LAUNCH_CHECK();
     return 0;

@@ -37,17 +37,59 @@ namespace hgnn {
 // the runtime binds to the kernel's own dispatch (its begin / end timestamps, as rocprofv3's kernel trace
 // reports them) -- no marker packets between the kernels of the stream, so timing changes neither the
 // stream's dispatch order nor what the kernel overlaps with.
+//
+// Stamp mode (st != nullptr): no events at all.  The kernels of the timed classes take a stamp slot
+// (clock_stamps, a null pointer otherwise) and every wave of the launch writes s_memrealtime (100 MHz,
+// chip-wide) at entry and at exit (WaveStamp): the launch's duration is max(exit) - min(entry), read after
+// the timed region.  Event timing -- markers or dispatch-bound pairs -- changes the timed kernel itself
+// (every timed dispatch gets a completion signal with a system-scope release: the aggregation backward ran
+// 19 -> 30 us per launch inside rocprofv3's own trace while bench.py timed it), stamps do not.
 struct LaunchClock {
-    hipEvent_t* ev;  // pairs: start, stop
-    int* cls;        // class of each pair
-    int cap;         // pairs available
-    int* used;       // pairs taken
+    hipEvent_t* ev;  // pairs: start, stop (event modes)
+    int* cls;        // class of each launch
+    int cap;         // launches available
+    int* used;       // launches taken
     int k;           // class of the launches being enqueued
+    uint64_t* st = nullptr;  // stamp mode: device stamp buffer
+    int* st_off = nullptr;   // per launch: first word of its slot
+    int* st_n = nullptr;     // per launch: words of its slot (2 per wave)
+    long long st_cap = 0;    // words available
+    long long* st_used = nullptr;
 };
 inline thread_local LaunchClock* t_clock = nullptr;
+// Stamp slot of a launch of `waves` waves (stamp mode), else nullptr.
+inline uint64_t* clock_stamps(long long waves) {
+    LaunchClock* c = t_clock;
+    if (!c || !c->st || *c->used >= c->cap || *c->st_used + 2 * waves > c->st_cap) return nullptr;
+    const int i = (*c->used)++;
+    c->cls[i] = c->k;
+    c->st_off[i] = (int)*c->st_used;
+    c->st_n[i] = (int)(2 * waves);
+    *c->st_used += 2 * waves;
+    return c->st + c->st_off[i];
+}
+#ifdef __HIP_DEVICE_COMPILE__
+#define HGNN_REALTIME() __builtin_amdgcn_s_memrealtime()
+#else
+#define HGNN_REALTIME() 0ull
+#endif
+// Entry / exit stamps of one wave (wave id = linear block id x waves per block + wave in block), written
+// by lane 0 with a plain vector store; the destructor covers every return path of the kernel.
+struct WaveStamp {
+    uint64_t* p;
+    __device__ __forceinline__ explicit WaveStamp(uint64_t* slot) : p(nullptr) {
+        if (!slot) return;
+        const long long b = blockIdx.x + (long long)gridDim.x * (blockIdx.y + (long long)gridDim.y * blockIdx.z);
+        p = slot + 2 * (b * (blockDim.x >> 6) + (threadIdx.x >> 6));
+        if ((threadIdx.x & 63) == 0) p[0] = HGNN_REALTIME();
+    }
+    __device__ __forceinline__ ~WaveStamp() {
+        if (p && (threadIdx.x & 63) == 0) p[1] = HGNN_REALTIME();
+    }
+};
 inline bool clock_pair(hipEvent_t* a, hipEvent_t* b) {
     LaunchClock* c = t_clock;
-    if (!c || *c->used >= c->cap) return false;
+    if (!c || !c->ev || *c->used >= c->cap) return false;
     const int i = (*c->used)++;
     c->cls[i] = c->k;
     *a = c->ev[2 * i];

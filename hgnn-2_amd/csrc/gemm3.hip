@@ -530,7 +530,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm5(const float* __restric
                                                           const int* __restrict__ m_valid, int m_cap, int N, int K,
                                                           float* __restrict__ C, int ldc, int xcd,
                                                           const float* __restrict__ bias = nullptr,
-                                                          int relu_from = 0, float* __restrict__ bn_part = nullptr) {
+                                                          int relu_from = 0, float* __restrict__ bn_part = nullptr,
+                                                          uint64_t* stamps = nullptr) {
+    WaveStamp stamp(stamps);
     constexpr int BK = 32, NW = WGM * WGN, ST = 2;
     constexpr int TM = BM / WGM, TN = BN / WGN, AM = TM / 16, AN = TN / 16;
     constexpr int AI = BM * BK * 4 / 1024, BI = BN * BK * 4 / 1024;  // 1-KB wave instructions per stage
@@ -781,10 +783,12 @@ int launch_gemm3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int
         const int gx = ceil_div(ceil_div(m_cap, 64), 8) * 8;
         if (g5 == 3)  // 64 x 32 tiles of 4 waves: twice the blocks, finer per-CU balance
             HGNN_KLAUNCH((k_gemm5<64, 32, 2, 2, true>), dim3(gx, n / 32), dim3(256), 0, s, a, lda, wc, ldw,
-                               m_valid, m_cap, n, k, y, ldy, 1, bias, relu_from, bn_part);
+                         m_valid, m_cap, n, k, y, ldy, 1, bias, relu_from, bn_part,
+                         clock_stamps((long long)gx * (n / 32) * 4));
         else
             HGNN_KLAUNCH((k_gemm5<64, 64, 2, 4, true>), dim3(gx, n / 64), dim3(512), 0, s, a, lda, wc, ldw,
-                               m_valid, m_cap, n, k, y, ldy, 1, bias, relu_from, bn_part);
+                         m_valid, m_cap, n, k, y, ldy, 1, bias, relu_from, bn_part,
+                         clock_stamps((long long)gx * (n / 64) * 8));
         HGNN_LAUNCH_CHECK();
         return 0;
     }
@@ -837,9 +841,10 @@ int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, in
             return !e || e[0] != '0';
         }();
         const int gx = xcd ? ceil_div(ceil_div(m_cap, 64), 8) * 8 : ceil_div(m_cap, 64);
-        HGNN_KLAUNCH((k_gemm5<64, 64, 2, 2>), dim3(gx, ceil_div(kout, 64)), dim3(256), 0, s,
-                           dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda, xcd ? 1 : 0,
-                           static_cast<const float*>(nullptr), 0, static_cast<float*>(nullptr));
+        const dim3 g(gx, ceil_div(kout, 64));
+        HGNN_KLAUNCH((k_gemm5<64, 64, 2, 2>), g, dim3(256), 0, s, dy, lddy, wt, ldw, m_valid, m_cap, kout, o, da, ldda,
+                     xcd ? 1 : 0, static_cast<const float*>(nullptr), 0, static_cast<float*>(nullptr),
+                     clock_stamps((long long)g.x * g.y * 4));
         HGNN_LAUNCH_CHECK();
         return 0;
     }

@@ -33,7 +33,9 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
                                                        const __bf16* __restrict__ B, long long pb, int ldb,
                                                        const int* __restrict__ m_valid, int m_cap, int N, int K,
                                                        float* __restrict__ Y, int ldy, const float* __restrict__ bias,
-                                                       int relu_from, float* __restrict__ bn_part) {
+                                                       int relu_from, float* __restrict__ bn_part,
+                                                       uint64_t* stamps) {
+    WaveStamp stamp(stamps);
     __shared__ __attribute__((aligned(16))) char lds[2 * G_STAGE];
     const int M = m_valid ? *m_valid : m_cap;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -190,7 +192,9 @@ template <int PD>
 __global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn(const float* __restrict__ A, int lda,
                                                       const float* __restrict__ B, int ldb,
                                                       float* __restrict__ slabs, int M, int N,
-                                                      const int* __restrict__ r_valid, int nz, int xcd_remap) {
+                                                      const int* __restrict__ r_valid, int nz, int xcd_remap,
+                                                      uint64_t* stamps) {
+    WaveStamp stamp(stamps);
     static_assert(PD >= 2, "a ring of at least two stages");
     __shared__ __attribute__((aligned(16))) char lds[2 * D_STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -307,8 +311,9 @@ int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const
     if (nz <= 0) return HGNN_ERR_ARG;
     if ((long long)r_cap * (lda > lddy ? lda : lddy) >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     // ring depth 2: step times 1.300-1.302 ms against 1.306-1.314 (4) and 1.313-1.323 (6), alternating runs
-    HGNN_KLAUNCH(k_gemm_bf3_tn<2>, dim3(ceil_div(o, 128), ceil_div(k, 128), nz), dim3(D_NT), 0, s, dy, lddy, a, lda,
-                       slabs, o, k, r_valid, nz, xcd && nz % 8 == 0 ? 1 : 0);
+    const dim3 g(ceil_div(o, 128), ceil_div(k, 128), nz);
+    HGNN_KLAUNCH(k_gemm_bf3_tn<2>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz,
+                 xcd && nz % 8 == 0 ? 1 : 0, clock_stamps((long long)g.x * g.y * g.z * (D_NT / 64)));
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -322,8 +327,9 @@ int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, 
         return HGNN_ERR_UNSUPPORTED;
     if ((long long)m_cap * lda * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     const int gx = ceil_div(ceil_div(m_cap, G_BM), 8) * 8;
-    HGNN_KLAUNCH(k_gemm_bf3_fwd, dim3(gx, ceil_div(n, G_BN)), dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid,
-                       m_cap, n, k, y, ldy, bias, relu_from, bn_part);
+    const dim3 g(gx, ceil_div(n, G_BN));
+    HGNN_KLAUNCH(k_gemm_bf3_fwd, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, bias, relu_from,
+                 bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)));
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -106,6 +106,7 @@ struct AggFwdArgs {
     // the row's zero padding [pad_from, ldo): 0 = after the parts this launch writes, -1 = none
     // (a G-only launch beside a P-only one, which writes the padding)
     int pad_from;
+    uint64_t* stamps;  // set by the launch under a stamp-mode clock (common.h WaveStamp), else null
 };
 int launch_agg_fwd(const AggFwdArgs& a, hipStream_t s);
 
@@ -124,6 +125,7 @@ struct AggBwdArgs {
     float* out;
     int ldo;
     int accumulate;
+    uint64_t* stamps;  // the launch's stamp slot (common.h WaveStamp), else null
 };
 int launch_agg_bwd(const AggBwdArgs& a, hipStream_t s);  // exactly one of ing / inp
 // the G gather of ga and the P gather of pa (different outputs) in one grid when they

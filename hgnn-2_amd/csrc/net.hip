@@ -387,24 +387,47 @@ Src make_src(const Program& P, void* ws, const hgnn_csr_batch* csr) {
     } while (0)
 
 // Optional per-kernel-class timer (bench.py times the dominant kernel class and the aggregation classes
-// inside their timed regions with it).  Disabled (nullptr) on the normal path.  Default: every dispatch
-// of a timed class gets an event pair bound to the dispatch itself (common.h LaunchClock: its begin / end
-// timestamps, rocprofv3's kernel-trace duration); HGNN_TIMER_MARKERS=1: the round-1..4 form, marker
-// events recorded on the stream around each call (the interval also holds the next dispatch's start-up
-// and changes what the side stream's blocks share the CUs with).
+// inside their timed regions with it).  Disabled (nullptr) on the normal path.  Modes (hgnn_timer_create_ex):
+//   HGNN_TIMER_STAMPS     the launches of the timed classes that carry a stamp slot (the aggregation and GEMM
+//                         kernels) write s_memrealtime per wave at entry and exit (common.h WaveStamp); a
+//                         launch's time = max(exit) - min(entry).  Nothing is added to the stream, so the timed
+//                         kernel runs as in an untimed step.
+//   HGNN_TIMER_DISPATCH   every dispatch of a timed class gets an event pair bound to the dispatch itself
+//                         (hipExtLaunchKernel); every class is covered, but a timed dispatch runs slower (its
+//                         completion signal's system-scope release: 19 -> 30 us per aggregation-backward launch
+//                         inside rocprofv3's own trace).
+//   HGNN_TIMER_MARKERS    marker events recorded on the stream around each call (the round-1..4 form).
 struct Timer {
     std::vector<hipEvent_t> ev;   // pairs: start, stop
     std::vector<int> cls;
     int used = 0;
     unsigned mask = 0;
-    bool markers = false;
+    int mode = HGNN_TIMER_DISPATCH;
+    uint64_t* st = nullptr;  // stamp buffer (device)
+    long long st_cap = 0, st_used = 0;
+    std::vector<int> st_off, st_n;
+    std::vector<double> st_ms;  // per launch, filled on the first read after a region
+    bool st_read = false;
 };
 
 struct ClockScope {  // t_clock for the launches of one TL call
     LaunchClock c;
     LaunchClock* prev;
     ClockScope(Timer* tm, int k) : prev(t_clock) {
-        c = LaunchClock{tm->ev.data(), tm->cls.data(), (int)tm->cls.size(), &tm->used, k};
+        c = LaunchClock{};
+        c.cls = tm->cls.data();
+        c.cap = (int)tm->cls.size();
+        c.used = &tm->used;
+        c.k = k;
+        if (tm->mode == HGNN_TIMER_STAMPS) {
+            c.st = tm->st;
+            c.st_off = tm->st_off.data();
+            c.st_n = tm->st_n.data();
+            c.st_cap = tm->st_cap;
+            c.st_used = &tm->st_used;
+        } else {
+            c.ev = tm->ev.data();
+        }
         t_clock = &c;
     }
     ~ClockScope() { t_clock = prev; }
@@ -413,7 +436,7 @@ struct ClockScope {  // t_clock for the launches of one TL call
 #define TL(k, x)                                                                        \
     do {                                                                                \
         const bool _t = tm && (tm->mask & (1u << (k))) && tm->used < (int)tm->cls.size(); \
-        if (_t && !tm->markers) {                                                       \
+        if (_t && tm->mode != HGNN_TIMER_MARKERS) {                                     \
             ClockScope _cs(tm, (k));                                                    \
             int _r = (x);                                                               \
             if (_r) return _r;                                                          \
@@ -1190,13 +1213,30 @@ int hgnn_net_backward(const hgnn_net_config* cfg, const hgnn_net_inputs* in, con
                          static_cast<hipStream_t>(stream));
 }
 
-void* hgnn_timer_create(int max_launches, unsigned class_mask) {
+void* hgnn_timer_create_ex(int max_launches, unsigned class_mask, int mode, long long stamp_words) {
     if (max_launches <= 0) return nullptr;
+    if (mode != HGNN_TIMER_STAMPS && mode != HGNN_TIMER_DISPATCH && mode != HGNN_TIMER_MARKERS) return nullptr;
     Timer* t = new Timer();
-    t->ev.resize(2 * (size_t)max_launches);
     t->cls.resize(max_launches);
     t->mask = class_mask;
-    t->markers = env_flag("HGNN_TIMER_MARKERS", false);
+    t->mode = mode;
+    if (mode == HGNN_TIMER_STAMPS) {
+        if (stamp_words <= 0 || stamp_words > (1ll << 31) - 1) {
+            delete t;
+            return nullptr;
+        }
+        t->st_off.resize(max_launches);
+        t->st_n.resize(max_launches);
+        t->st_cap = stamp_words;
+        if (hipMalloc(&t->st, (size_t)stamp_words * 8) != hipSuccess ||
+            hipMemset(t->st, 0, (size_t)stamp_words * 8) != hipSuccess) {
+            if (t->st) (void)hipFree(t->st);
+            delete t;
+            return nullptr;
+        }
+        return t;
+    }
+    t->ev.resize(2 * (size_t)max_launches);
     for (auto& e : t->ev) {
         if (hipEventCreate(&e) != hipSuccess) {
             delete t;
@@ -1206,8 +1246,43 @@ void* hgnn_timer_create(int max_launches, unsigned class_mask) {
     return t;
 }
 
+void* hgnn_timer_create(int max_launches, unsigned class_mask) {
+    const char* e = getenv("HGNN_TIMER_MARKERS");
+    return hgnn_timer_create_ex(max_launches, class_mask,
+                                e && e[0] == '1' ? HGNN_TIMER_MARKERS : HGNN_TIMER_DISPATCH, 0);
+}
+
 void hgnn_timer_reset(void* timer) {
-    if (timer) static_cast<Timer*>(timer)->used = 0;
+    if (!timer) return;
+    Timer* t = static_cast<Timer*>(timer);
+    t->used = 0;
+    if (t->st) {
+        (void)hipDeviceSynchronize();
+        (void)hipMemset(t->st, 0, (size_t)t->st_used * 8);
+        t->st_used = 0;
+        t->st_read = false;
+    }
+}
+
+// Stamp mode: a launch's time = max over its waves' exit stamps - min over their entry stamps (100 MHz).
+static int timer_read_stamps(Timer* t) {
+    if (t->st_read) return HGNN_OK;
+    if (hipDeviceSynchronize() != hipSuccess) return HGNN_ERR_HIP;
+    std::vector<uint64_t> h((size_t)t->st_used);
+    if (t->st_used && hipMemcpy(h.data(), t->st, (size_t)t->st_used * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return HGNN_ERR_HIP;
+    t->st_ms.assign(t->used, 0.0);
+    for (int i = 0; i < t->used; ++i) {
+        uint64_t lo = ~0ull, hi = 0;
+        for (int w = 0; w < t->st_n[i] / 2; ++w) {
+            const uint64_t a = h[t->st_off[i] + 2 * w], b = h[t->st_off[i] + 2 * w + 1];
+            if (a && a < lo) lo = a;
+            if (b > hi) hi = b;
+        }
+        t->st_ms[i] = hi > lo && lo != ~0ull ? (double)(hi - lo) * 1e-5 : 0.0;  // 10 ns ticks -> ms
+    }
+    t->st_read = true;
+    return HGNN_OK;
 }
 
 int hgnn_timer_elapsed(void* timer, int kernel_class, double* total_ms, int* launches) {
@@ -1215,6 +1290,18 @@ int hgnn_timer_elapsed(void* timer, int kernel_class, double* total_ms, int* lau
     Timer* t = static_cast<Timer*>(timer);
     double tot = 0.0;
     int n = 0;
+    if (t->mode == HGNN_TIMER_STAMPS) {
+        const int r = timer_read_stamps(t);
+        if (r) return r;
+        for (int i = 0; i < t->used; ++i)
+            if (t->cls[i] == kernel_class) {
+                tot += t->st_ms[i];
+                ++n;
+            }
+        *total_ms = tot;
+        *launches = n;
+        return HGNN_OK;
+    }
     for (int i = 0; i < t->used; ++i) {
         if (t->cls[i] != kernel_class) continue;
         float ms = 0.f;
@@ -1232,6 +1319,10 @@ void hgnn_timer_destroy(void* timer) {
     if (!timer) return;
     Timer* t = static_cast<Timer*>(timer);
     for (auto& e : t->ev) (void)hipEventDestroy(e);
+    if (t->st) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(t->st);
+    }
     delete t;
 }
 

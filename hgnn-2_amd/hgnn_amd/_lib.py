@@ -86,6 +86,7 @@ SIGNATURES = {
     "hgnn_bn_forward": ([_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _I, _VP], _I),
     "hgnn_bn_backward": ([_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _I, _VP], _I),
     "hgnn_timer_create": ([_I, ctypes.c_uint], _VP),
+    "hgnn_timer_create_ex": ([_I, ctypes.c_uint, _I, ctypes.c_longlong], _VP),
     "hgnn_timer_reset": ([_VP], None),
     "hgnn_timer_elapsed": ([_VP, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)], _I),
     "hgnn_timer_destroy": ([_VP], None),

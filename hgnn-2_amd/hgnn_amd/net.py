@@ -22,14 +22,24 @@ _pending = []
 _timer = None
 
 
-class KernelTimer:
-    """HIP-event timer around every launch of the selected kernel classes (HGNN_K_*)."""
+TIMER_STAMPS, TIMER_DISPATCH, TIMER_MARKERS = 0, 1, 2  # include/hgnn_amd.h HGNN_TIMER_*
 
-    def __init__(self, max_launches, classes):
+
+class KernelTimer:
+    """Timer of every launch of the selected kernel classes (HGNN_K_*).  mode TIMER_STAMPS: in-kernel
+    s_memrealtime stamps per wave (the aggregation and GEMM kernels; the timed kernels run as in an untimed
+    step), stamp_words device words (2 per wave of every timed launch); TIMER_DISPATCH: dispatch-bound HIP
+    event pairs (every class; a timed dispatch runs slower); None: the library's default (dispatch events,
+    or markers with HGNN_TIMER_MARKERS=1)."""
+
+    def __init__(self, max_launches, classes, mode=None, stamp_words=0):
         mask = 0
         for c in classes:
             mask |= 1 << c
-        self.handle = L.lib().hgnn_timer_create(max_launches, mask)
+        if mode is None:
+            self.handle = L.lib().hgnn_timer_create(max_launches, mask)
+        else:
+            self.handle = L.lib().hgnn_timer_create_ex(max_launches, mask, mode, stamp_words)
         if not self.handle:
             raise RuntimeError("hgnn_amd: could not create the kernel timer")
 

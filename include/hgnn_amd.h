@@ -157,9 +157,22 @@ int hgnn_net_backward_ex(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
                          void* const* events, int n_events);
 
 /* Kernel classes for the optional launch timer (bench.py measures the
- * dominant kernel with HIP events on the launching stream, inside its timed
- * region).  A timer records a start/stop event pair around every launch of a
- * class in `class_mask` (bit k = class k). */
+ * dominant kernel class and the aggregation classes inside timed regions of
+ * its own steps).  A timer times every launch of a class in `class_mask`
+ * (bit k = class k) in one of three modes (hgnn_timer_create_ex):
+ *   HGNN_TIMER_STAMPS    the aggregation and GEMM kernels write a 100 MHz
+ *                        s_memrealtime stamp per wave at entry and exit into
+ *                        the timer's device buffer (2 words per wave, stamp_words
+ *                        in all); a launch lasts max(exit) - min(entry).  Nothing
+ *                        is added to the stream, so a timed kernel runs as in an
+ *                        untimed step; classes without stamp slots are not timed;
+ *   HGNN_TIMER_DISPATCH  an event pair bound to each dispatch (hipExtLaunchKernel):
+ *                        every class, but the timed dispatch runs slower;
+ *   HGNN_TIMER_MARKERS   event records on the stream around each launch call.
+ * hgnn_timer_create: DISPATCH (MARKERS with HGNN_TIMER_MARKERS=1). */
+#define HGNN_TIMER_STAMPS 0
+#define HGNN_TIMER_DISPATCH 1
+#define HGNN_TIMER_MARKERS 2
 #define HGNN_K_STRUCT 0    /* plan, dense->list extraction, pack/unpack */
 #define HGNN_K_AGG_FWD 1   /* aggregation gather (graph_oper + P_multi)  */
 #define HGNN_K_GEMM_FWD 2  /* fused Conv1d pair GEMM + bias/ReLU/BN partials */
@@ -172,8 +185,10 @@ int hgnn_net_backward_ex(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
 #define HGNN_K_DW_DENSE 9  /* dense operator gradient dW (W.requires_grad) */
 #define HGNN_K_DW_REDUCE 10 /* dW slab + bias reductions                    */
 void* hgnn_timer_create(int max_launches, unsigned class_mask);
+void* hgnn_timer_create_ex(int max_launches, unsigned class_mask, int mode, long long stamp_words);
 void hgnn_timer_reset(void* timer);
-/* Waits for the recorded events; sums the durations of class `kernel_class`. */
+/* Waits for the timed work (stamp mode: a device synchronisation and one copy of
+ * the stamp buffer); sums the durations of class `kernel_class`. */
 int hgnn_timer_elapsed(void* timer, int kernel_class, double* total_ms, int* launches);
 void hgnn_timer_destroy(void* timer);
 int hgnn_net_forward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
