@@ -97,7 +97,9 @@ def test_config4_rank_share_d128_512_vs_oracle():
     b = _batch(dg.qm9_shape_dataset(512, seed=1004))
     model = GNN_lg(0, 128, 5, 5, 1, 1, 2).cuda()
     fu.det_init(model, 4)
-    _check(model, b, 5, 2, dx_relax=True)
+    # the plain §8(c) dX bound (measured round 5 at 0.037 of it, profiles/r05_parity_margins.jsonl; the
+    # round-2..4 fallback to twice the reference's fp32 error is no longer taken)
+    _check(model, b, 5, 2)
 
 
 @pytest.mark.parametrize("J,order", [(2, 1), (2, 2), (2, 3), (3, 2)])
@@ -120,7 +122,8 @@ def test_gnn_simple_j2_vs_oracle():
     fu.det_init(model, 61)
     # outputs reach |y| = 412 here (SBM-50, A^2 slice): measured |gpu - ref64| = 1.33e-3 against the
     # reference fp32's own 5.2e-4 (3.2e-6 vs 1.3e-6 relative), inside the first leg (1e-5 relative) but
-    # 2.6x the reference's error, so the fp64 leg is held at 3x here
+    # 2.6x the reference's error, so the fp64 leg is held at 3x here (re-measured round 5: 1.34x the
+    # strict 2x bound, profiles/r05_parity_margins.jsonl -- this relaxation stays)
     _check(model, b, 6, 0, kind="simple", factor=3.0)
 
 

@@ -312,12 +312,11 @@ def test_gnn_lg_d128_config4_model_vs_oracle_fp64():
         err = (p.grad.cpu().double() - ref_g[k]).abs()
         assert torch.all(err <= 1e-4 * gmax + 1e-5 * ref_g[k].abs()), (k, err.max().item(), gmax)
     err = (X.grad.cpu().double() - ref_dx).abs().max().item()
-    # dX at this width is ill-conditioned: the reference's own fp32 evaluation (the oracle run in
-    # fp32, op for op) is 0.016 away from fp64 here, 2.5x the fixed 1e-4 * max|dX| bound; the GPU
-    # result must be within that bound or within twice the reference-fp32 error
-    _, _, _, dx32 = _oracle_lg(model, b, 4, 2, dtype=torch.float32)
-    ref32_err = (dx32.double() - ref_dx).abs().max().item()
-    assert err <= max(1e-4 * max(1.0, ref_dx.abs().max().item()), 2.0 * ref32_err), (err, ref32_err)
+    # the plain §8(c) bound: measured round 5 (tools/parity_margins.py, profiles/r05_parity_margins.jsonl) at
+    # 0.018 of it -- the reference's own fp32 evaluation is 2.5x over it here (dX at this width is
+    # ill-conditioned), the split-bf16 GEMMs are not; the round-2..4 relaxation (2x the reference's fp32
+    # error) is gone
+    assert err <= 1e-4 * max(1.0, ref_dx.abs().max().item()), err
 
 
 @pytest.mark.parametrize("name", LG_CASES + ["gnn_simple"])
@@ -393,12 +392,17 @@ def test_large_J_vs_oracle_fp64(J):
     X.requires_grad_(True)
     out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
     torch.nn.MSELoss()(out, T).backward()
-    # A^8 / A^16 of the weighted QM9-shape adjacencies reach ~1e6 and the outputs ~4e6, so the
-    # reference's own fp32 error is the scale: the north star's 1e-5 relative bound against both
-    # the reference-order fp32 forward and the fp64 anchor (instead of the two-leg 2 |ref32 - ref64|)
-    for ref in (ref32, ref_out):
-        err = (out.detach().cpu().double() - ref.double()).abs().max().item()
-        assert err <= 1e-5 * max(1.0, ref.abs().max().item()), (err, ref.abs().max().item())
+    if J == 5:
+        # the plain two-leg policy (measured round 5 at 0.20 of its fp64 leg, profiles/r05_parity_margins.jsonl)
+        o = PP.outputs_two_leg(out.detach(), ref32, ref_out)
+        assert o["pass"], o
+    else:
+        # J = 4: A^8 of the weighted QM9-shape adjacencies reaches ~1e6 and the outputs ~4e6; the fp64 leg
+        # measured round 5 at 2.64 vs a strict bound of 1.04 (2.5x; the reference fp32's own |ref32 - ref64|
+        # is 0.52 there), so this case keeps the north star's 1e-5 relative bound on both legs
+        for ref in (ref32, ref_out):
+            err = (out.detach().cpu().double() - ref.double()).abs().max().item()
+            assert err <= 1e-5 * max(1.0, ref.abs().max().item()), (err, ref.abs().max().item())
     gmax = max(g.abs().max().item() for g in ref_g.values())
     for k, p in model.named_parameters():
         err = (p.grad.cpu().double() - ref_g[k]).abs()
