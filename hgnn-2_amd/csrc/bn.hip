@@ -30,6 +30,7 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
 // lane (all loads in flight, clamped and selected after), wave sums only -- no block barriers.
 // (A block per channel with three block-wide fp64 reductions took ~5.3 us per launch.)
 __global__ void __launch_bounds__(256) k_bn_finalize(BnFwdArgs a) {
+    WaveStamp stamp(a.stamps);
     const int lane = threadIdx.x & 63;
     const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (ch >= a.c) return;
@@ -97,7 +98,9 @@ __global__ void __launch_bounds__(256) k_bn_finalize(BnFwdArgs a) {
 }
 
 int launch_bn_finalize(const BnFwdArgs& a, hipStream_t s) {
-    HGNN_KLAUNCH(k_bn_finalize, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, a);
+    BnFwdArgs b = a;
+    b.stamps = clock_stamps((long long)ceil_div(a.c, 4) * 4);
+    HGNN_KLAUNCH(k_bn_finalize, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, b);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -205,6 +208,7 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 __device__ __forceinline__ float& f4c(float4& v, int i) { return reinterpret_cast<float*>(&v)[i]; }
 
 __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
+    WaveStamp stamp(a.stamps);
     const int tile = blockIdx.x;
     const int total = *a.total_rows;
     const int r0 = tile * 64;
@@ -273,6 +277,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
 }
 
 __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
+    WaveStamp stamp(a.stamps);
     const int total = *a.total_rows;
     const float wv = *a.w;
     const float inv_n = total > 0 ? 1.0f / (float)total : 0.f;
@@ -367,6 +372,7 @@ static bool bn_vec4(const BnBwdArgs& a) {
 
 // One wave per channel, as k_bn_finalize: the 4 statistics of a channel over the tile partials.
 __global__ void __launch_bounds__(256) k_bn_bwd_fin(BnBwdArgs a) {
+    WaveStamp stamp(a.stamps);
     const int lane = threadIdx.x & 63;
     const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (ch >= a.c) return;
@@ -927,15 +933,19 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
         HGNN_LAUNCH_CHECK();
         return 0;
     }
+    BnBwdArgs as = a;  // a stamp slot per launch (stamp-mode clock only)
     if (tiles > 0) {
-        if (v4) HGNN_KLAUNCH(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, a);
+        as.stamps = v4 ? clock_stamps((long long)tiles * 4) : nullptr;
+        if (v4) HGNN_KLAUNCH(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, as);
         else HGNN_KLAUNCH(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
     }
     HGNN_LAUNCH_CHECK();
-    HGNN_KLAUNCH(k_bn_bwd_fin, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, a);
+    as.stamps = clock_stamps((long long)ceil_div(a.c, 4) * 4);
+    HGNN_KLAUNCH(k_bn_bwd_fin, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, as);
     HGNN_LAUNCH_CHECK();
     if (!apply) return 0;
-    if (v4) HGNN_KLAUNCH(k_bn_bwd_apply4, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);
+    as.stamps = v4 ? clock_stamps((long long)(tiles > 0 ? tiles : 1) * 4) : nullptr;
+    if (v4) HGNN_KLAUNCH(k_bn_bwd_apply4, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, as);
     else HGNN_KLAUNCH(k_bn_bwd_apply, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, a);
     HGNN_LAUNCH_CHECK();
     return 0;
@@ -954,7 +964,8 @@ __global__ void __launch_bounds__(RO_THREADS) k_readout_fwd(const float* __restr
                                                             const float* __restrict__ fcw,
                                                             const float* __restrict__ fcb, int dim_out,
                                                             float* __restrict__ colsum,
-                                                            float* __restrict__ out) {
+                                                            float* __restrict__ out, uint64_t* stamps) {
+    WaveStamp stamp(stamps);
     __shared__ double red[RO_THREADS / 64];
     const int b = blockIdx.x;
     const int r0 = node_off[b], r1 = node_off[b + 1];
@@ -1001,7 +1012,7 @@ __global__ void __launch_bounds__(RO_THREADS) k_readout_fwd(const float* __restr
 int launch_readout_fwd(const float* a, int k, const int* node_off, int bs, int nmax, const float* fcw,
                        const float* fcb, int dim_out, float* colsum, float* out, hipStream_t s) {
     HGNN_KLAUNCH(k_readout_fwd, dim3(bs), dim3(RO_THREADS), 0, s, a, k, node_off, nmax, fcw, fcb, dim_out,
-                       colsum, out);
+                 colsum, out, clock_stamps((long long)bs * (RO_THREADS / 64)));
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -1052,6 +1063,7 @@ __device__ __forceinline__ float readout_row(const float* __restrict__ dout, con
 constexpr int RA_THREADS = 256;
 
 __global__ void __launch_bounds__(RA_THREADS) k_readout_agg_bwd(ReadoutAggArgs a) {
+    WaveStamp stamp(a.stamps);
     const int b = blockIdx.x;
     const bool g = blockIdx.y == 0;
     float* out = g ? a.g_out : a.p_out;
@@ -1132,7 +1144,9 @@ int launch_readout_agg_bwd(const ReadoutAggArgs& a, hipStream_t s) {
     const size_t lds = readout_agg_bwd_lds(a);
     if (lds > RO_LDS_CAP) return HGNN_ERR_UNSUPPORTED;
     allow_ro_lds(k_readout_agg_bwd, lds);
-    HGNN_KLAUNCH(k_readout_agg_bwd, dim3(a.bs, a.p_out ? 2 : 1), dim3(RA_THREADS), lds, s, a);
+    ReadoutAggArgs as = a;
+    as.stamps = clock_stamps((long long)a.bs * (a.p_out ? 2 : 1) * (RA_THREADS / 64));
+    HGNN_KLAUNCH(k_readout_agg_bwd, dim3(a.bs, a.p_out ? 2 : 1), dim3(RA_THREADS), lds, s, as);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -1141,6 +1155,7 @@ int launch_readout_agg_bwd(const ReadoutAggArgs& a, hipStream_t s) {
 // u in LDS, then written to every row n.  X: BN of the producer applied on load, the BN of 0 at
 // padded m (as k_dw_dense); the dense layer input (xdense) as stored.
 __global__ void __launch_bounds__(256) k_dw_readout(DwDenseArgs a) {
+    WaveStamp stamp(a.stamps);
     extern __shared__ float sh[];
     const int b = blockIdx.x;
     const int nmax = a.nmax, J = a.jt, F = a.f, FP = F + 1;
@@ -1184,7 +1199,9 @@ int launch_dw_readout(const DwDenseArgs& a, hipStream_t s) {
     const size_t lds = dw_readout_lds(a);
     if (lds > RO_LDS_CAP || !a.dout) return HGNN_ERR_UNSUPPORTED;
     allow_ro_lds(k_dw_readout, lds);
-    HGNN_KLAUNCH(k_dw_readout, dim3(a.bs), dim3(256), lds, s, a);
+    DwDenseArgs as = a;
+    as.stamps = clock_stamps((long long)a.bs * 4);
+    HGNN_KLAUNCH(k_dw_readout, dim3(a.bs), dim3(256), lds, s, as);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -1195,7 +1212,9 @@ constexpr int RB_CHUNKS = 16;
 
 __global__ void __launch_bounds__(256) k_readout_bwd_part(const float* __restrict__ dout,
                                                           const float* __restrict__ colsum, int bs,
-                                                          int dim_out, int k, double* __restrict__ part) {
+                                                          int dim_out, int k, double* __restrict__ part,
+                                                          uint64_t* stamps) {
+    WaveStamp stamp(stamps);
     __shared__ double red[4][64];
     const int kk = blockIdx.x * 64 + (threadIdx.x & 63);
     const int g = threadIdx.x >> 6;
@@ -1230,7 +1249,8 @@ __global__ void __launch_bounds__(256) k_readout_bwd_params(const float* __restr
                                                             const double* __restrict__ part, int bs,
                                                             int nmax, int dim_out, int k,
                                                             float* __restrict__ dfcw,
-                                                            float* __restrict__ dfcb) {
+                                                            float* __restrict__ dfcb, uint64_t* stamps) {
+    WaveStamp stamp(stamps);
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx < dim_out * k) {
         double s = 0.0;
@@ -1254,11 +1274,11 @@ int launch_readout_bwd_params(const float* dout, const float* colsum, int bs, in
                               float* dfcw, float* dfcb, void* scratch, hipStream_t s) {
     double* part = static_cast<double*>(scratch);
     HGNN_KLAUNCH(k_readout_bwd_part, dim3(ceil_div(k, 64), RB_CHUNKS), dim3(256), 0, s, dout, colsum, bs,
-                       dim_out, k, part);
+                 dim_out, k, part, clock_stamps((long long)ceil_div(k, 64) * RB_CHUNKS * 4));
     HGNN_LAUNCH_CHECK();
     const int n = dim_out * k > dim_out ? dim_out * k : dim_out;
     HGNN_KLAUNCH(k_readout_bwd_params, dim3(ceil_div(n, 256)), dim3(256), 0, s, dout, part, bs, nmax,
-                       dim_out, k, dfcw, dfcb);
+                 dim_out, k, dfcw, dfcb, clock_stamps((long long)ceil_div(n, 256) * 4));
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -55,6 +55,8 @@ struct LaunchClock {
     int* st_n = nullptr;     // per launch: words of its slot (2 per wave)
     long long st_cap = 0;    // words available
     long long* st_used = nullptr;
+    uintptr_t strm = 0;          // the stream the launches go to
+    uintptr_t* st_strm = nullptr;  // per launch: its stream
 };
 inline thread_local LaunchClock* t_clock = nullptr;
 // Stamp slot of a launch of `waves` waves (stamp mode), else nullptr.
@@ -65,6 +67,7 @@ inline uint64_t* clock_stamps(long long waves) {
     c->cls[i] = c->k;
     c->st_off[i] = (int)*c->st_used;
     c->st_n[i] = (int)(2 * waves);
+    if (c->st_strm) c->st_strm[i] = c->strm;
     *c->st_used += 2 * waves;
     return c->st + c->st_off[i];
 }

@@ -120,6 +120,7 @@ __device__ __forceinline__ void dw_stage(const DwDenseArgs& a, int b, int off, i
 // more than the shorter kernel saves; retired in round 4.)
 template <int FC, int MAXI>
 __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
+    WaveStamp stamp(a.stamps);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int b = blockIdx.x;
     const int nmax = a.nmax, F = a.f;
@@ -235,7 +236,9 @@ static void allow_lds(size_t lds) {
 }
 
 template <int FC>
-static void launch_fc(const DwDenseArgs& a, int maxi, int gy, size_t lds, hipStream_t s) {
+static void launch_fc(const DwDenseArgs& a0, int maxi, int gy, size_t lds, hipStream_t s) {
+    DwDenseArgs a = a0;
+    a.stamps = clock_stamps((long long)a0.bs * gy * 4);
     allow_lds<FC, 1>(lds);
     allow_lds<FC, 3>(lds);
     allow_lds<FC, 5>(lds);
@@ -250,6 +253,7 @@ static void launch_fc(const DwDenseArgs& a, int maxi, int gy, size_t lds, hipStr
 // padded-position values as k_dw_dense (dG = 0 at padded n outside the readout, the BN of 0 at
 // padded m); f summed in order.
 __global__ void __launch_bounds__(256) k_dw_dense_narrow(DwDenseArgs a) {
+    WaveStamp stamp(a.stamps);
     extern __shared__ float sm[];
     const int b = blockIdx.x;
     const int nmax = a.nmax, J = a.jt, F = a.f, JF = J * F;
@@ -296,7 +300,9 @@ int launch_dw_dense(const DwDenseArgs& a, hipStream_t s) {
         const size_t lds = sizeof(float) * (size_t)a.nmax * (a.jt * a.f + a.f);
         if (lds <= 64 * 1024) {
             const int gy = std::max(1, std::min(16, 512 / std::max(1, a.bs)));
-            HGNN_KLAUNCH(k_dw_dense_narrow, dim3(a.bs, gy), dim3(256), lds, s, a);
+            DwDenseArgs as = a;
+            as.stamps = clock_stamps((long long)a.bs * gy * 4);
+            HGNN_KLAUNCH(k_dw_dense_narrow, dim3(a.bs, gy), dim3(256), lds, s, as);
             HGNN_LAUNCH_CHECK();
             return 0;
         }

@@ -57,6 +57,7 @@ struct ExtractArgs {
     int f;
     float* xo;
     float* xlo;
+    uint64_t* stamps;  // the launch's stamp slot under a stamp-mode clock (common.h WaveStamp), else null
 };
 int launch_extract(const ExtractArgs& a, hipStream_t s);
 
@@ -173,6 +174,7 @@ struct RepackTable {
     RepackItem it[REPACK_MAX];
     int n, d;
     int y;  // blocks per item (repack_y)
+    uint64_t* stamps;  // the launch's stamp slot under a stamp-mode clock (common.h WaveStamp), else null
 };
 int launch_repack(const RepackTable& t, hipStream_t s);
 // blocks per repack item: ~4 elements per thread of the largest item, 8..256 blocks (d = 64: 80
@@ -275,6 +277,7 @@ struct BnFwdArgs {
     float* run_std;
     int training;
     float momentum;
+    uint64_t* stamps;  // the launch's stamp slot under a stamp-mode clock (common.h WaveStamp), else null
 };
 int launch_bn_finalize(const BnFwdArgs& a, hipStream_t s);
 
@@ -300,6 +303,7 @@ struct BnBwdArgs {
     float* dw;             // scalar out
     float* db;             // scalar out
     float* dbpart;         // optional out: per-64-row-tile column sums of dy [tiles][c]
+    uint64_t* stamps;  // the launch's stamp slot under a stamp-mode clock (common.h WaveStamp), else null
 };
 // apply = 0: only the statistics (part + fin)
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply = 1);
@@ -356,6 +360,7 @@ struct DwDenseArgs {
     int bs, nmax;
     float* dW;             // (bs, nmax, nmax, jt)
     int accumulate;
+    uint64_t* stamps;  // the launch's stamp slot under a stamp-mode clock (common.h WaveStamp), else null
 };
 int launch_dw_dense(const DwDenseArgs& a, hipStream_t s);
 
@@ -388,6 +393,7 @@ struct ReadoutAggArgs {
     int p_cap;
     float* p_out;            // null: no P gather
     int p_acc;
+    uint64_t* stamps;  // the launch's stamp slot under a stamp-mode clock (common.h WaveStamp), else null
 };
 int launch_readout_agg_bwd(const ReadoutAggArgs& a, hipStream_t s);
 // whether the readout-row backward (launch_readout_agg_bwd and, with dw, launch_dw_readout) fits its

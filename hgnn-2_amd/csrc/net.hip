@@ -406,14 +406,16 @@ struct Timer {
     uint64_t* st = nullptr;  // stamp buffer (device)
     long long st_cap = 0, st_used = 0;
     std::vector<int> st_off, st_n;
+    std::vector<uintptr_t> st_strm;
     std::vector<double> st_ms;  // per launch, filled on the first read after a region
+    std::vector<uint64_t> st_lo, st_hi;  // per launch: first entry / last exit stamp (10 ns ticks)
     bool st_read = false;
 };
 
 struct ClockScope {  // t_clock for the launches of one TL call
     LaunchClock c;
     LaunchClock* prev;
-    ClockScope(Timer* tm, int k) : prev(t_clock) {
+    ClockScope(Timer* tm, int k, hipStream_t s) : prev(t_clock) {
         c = LaunchClock{};
         c.cls = tm->cls.data();
         c.cap = (int)tm->cls.size();
@@ -425,6 +427,8 @@ struct ClockScope {  // t_clock for the launches of one TL call
             c.st_n = tm->st_n.data();
             c.st_cap = tm->st_cap;
             c.st_used = &tm->st_used;
+            c.strm = reinterpret_cast<uintptr_t>(s);
+            c.st_strm = tm->st_strm.data();
         } else {
             c.ev = tm->ev.data();
         }
@@ -437,7 +441,7 @@ struct ClockScope {  // t_clock for the launches of one TL call
     do {                                                                                \
         const bool _t = tm && (tm->mask & (1u << (k))) && tm->used < (int)tm->cls.size(); \
         if (_t && tm->mode != HGNN_TIMER_MARKERS) {                                     \
-            ClockScope _cs(tm, (k));                                                    \
+            ClockScope _cs(tm, (k), s);                                                    \
             int _r = (x);                                                               \
             if (_r) return _r;                                                          \
             break;                                                                      \
@@ -1227,6 +1231,7 @@ void* hgnn_timer_create_ex(int max_launches, unsigned class_mask, int mode, long
         }
         t->st_off.resize(max_launches);
         t->st_n.resize(max_launches);
+        t->st_strm.resize(max_launches);
         t->st_cap = stamp_words;
         if (hipMalloc(&t->st, (size_t)stamp_words * 8) != hipSuccess ||
             hipMemset(t->st, 0, (size_t)stamp_words * 8) != hipSuccess) {
@@ -1272,6 +1277,8 @@ static int timer_read_stamps(Timer* t) {
     if (t->st_used && hipMemcpy(h.data(), t->st, (size_t)t->st_used * 8, hipMemcpyDeviceToHost) != hipSuccess)
         return HGNN_ERR_HIP;
     t->st_ms.assign(t->used, 0.0);
+    t->st_lo.assign(t->used, 0);
+    t->st_hi.assign(t->used, 0);
     for (int i = 0; i < t->used; ++i) {
         uint64_t lo = ~0ull, hi = 0;
         for (int w = 0; w < t->st_n[i] / 2; ++w) {
@@ -1280,6 +1287,8 @@ static int timer_read_stamps(Timer* t) {
             if (b > hi) hi = b;
         }
         t->st_ms[i] = hi > lo && lo != ~0ull ? (double)(hi - lo) * 1e-5 : 0.0;  // 10 ns ticks -> ms
+        t->st_lo[i] = lo == ~0ull ? 0 : lo;
+        t->st_hi[i] = hi;
     }
     t->st_read = true;
     return HGNN_OK;
@@ -1313,6 +1322,31 @@ int hgnn_timer_elapsed(void* timer, int kernel_class, double* total_ms, int* lau
     *total_ms = tot;
     *launches = n;
     return HGNN_OK;
+}
+
+int hgnn_timer_launches(void* timer, int max, int* cls, double* t_entry_us, double* t_exit_us, int* stream_idx) {
+    if (!timer || max < 0 || (max > 0 && (!cls || !t_entry_us || !t_exit_us))) return -HGNN_ERR_ARG;
+    Timer* t = static_cast<Timer*>(timer);
+    if (t->mode != HGNN_TIMER_STAMPS) return -HGNN_ERR_UNSUPPORTED;
+    const int r = timer_read_stamps(t);
+    if (r) return -r;
+    uint64_t base = ~0ull;
+    for (int i = 0; i < t->used; ++i)
+        if (t->st_lo[i] && t->st_lo[i] < base) base = t->st_lo[i];
+    const int n = t->used < max ? t->used : max;
+    std::vector<uintptr_t> seen;
+    for (int i = 0; i < n; ++i) {
+        cls[i] = t->cls[i];
+        if (stream_idx) {
+            int q = 0;
+            while (q < (int)seen.size() && seen[q] != t->st_strm[i]) ++q;
+            if (q == (int)seen.size()) seen.push_back(t->st_strm[i]);
+            stream_idx[i] = q;
+        }
+        t_entry_us[i] = t->st_lo[i] ? (double)(t->st_lo[i] - base) * 1e-2 : -1.0;
+        t_exit_us[i] = t->st_hi[i] ? (double)(t->st_hi[i] - base) * 1e-2 : -1.0;
+    }
+    return t->used;
 }
 
 void hgnn_timer_destroy(void* timer) {

@@ -86,7 +86,9 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
 // are combined in order through LDS; the bias gradients as in k_dw_reduce2.
 __global__ void __launch_bounds__(256) k_dw_reduce4(const float* __restrict__ slabs, const int* r_valid, int nz, int M,
                                                     int MR, int N, int split, float* dw0, float* dw1,
-                                                    const float* __restrict__ dbpart, float* db0, float* db1) {
+                                                    const float* __restrict__ dbpart, float* db0, float* db1,
+                                                    uint64_t* stamps) {
+    WaveStamp stamp(stamps);
     const int total = MR * N, nwb = (total + 255) / 256;
     if ((int)blockIdx.x >= nwb) {
         __shared__ double red[4];
@@ -151,7 +153,7 @@ int launch_dw_reduce2(const float* slabs, const int* r_valid, int nz, int o, int
     const int nb = dbpart ? o_real : 0;
     if (total % 4 == 0 && ((long long)o * k) % 4 == 0 && ((uintptr_t)slabs & 15) == 0) {
         HGNN_KLAUNCH(k_dw_reduce4, dim3(ceil_div(total, 256) + nb), dim3(256), 0, s, slabs, r_valid, nz, o, o_real,
-                           k, split, dw0, dw1, dbpart, db0, db1);
+                     k, split, dw0, dw1, dbpart, db0, db1, clock_stamps((long long)(ceil_div(total, 256) + nb) * 4));
     } else if (nz > 32) {
         HGNN_KLAUNCH(k_dw_reduce2<16>, dim3(ceil_div(total, 16) + nb), dim3(256), 0, s, slabs, r_valid, nz,
                            o, o_real, k, split, dw0, dw1, dbpart, db0, db1);

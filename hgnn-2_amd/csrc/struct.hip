@@ -22,6 +22,7 @@ namespace hgnn {
 __global__ void __launch_bounds__(256) k_plan(const int64_t* __restrict__ nb,
                                               const int64_t* __restrict__ eb, int bs,
                                               int nmax, int emax, BatchMeta m, RepackTable rt) {
+    WaveStamp stamp(rt.stamps);
     if (blockIdx.x > 0) {
         const int b = blockIdx.x - 1;
         repack_part(rt, b / rt.y, b % rt.y);
@@ -87,6 +88,7 @@ int launch_plan(const int64_t* nb, const int64_t* eb, int bs, int nmax, int emax
     RepackTable t{};
     if (rt) t = *rt;
     t.y = repack_y(t);
+    t.stamps = clock_stamps((long long)(1 + t.n * t.y) * 4);
     HGNN_KLAUNCH(k_plan, dim3(1 + t.n * t.y), dim3(256), 0, s, nb, eb, bs, nmax, emax, m, t);
     HGNN_LAUNCH_CHECK();
     return 0;
@@ -423,6 +425,7 @@ __device__ void lds_validate(const float* S, int R, int C, int NC, int rr, int r
 
 template <int JT>
 __global__ void __launch_bounds__(XL_THREADS) k_extract_lds(ExtractArgs a) {
+    WaveStamp stamp(a.stamps);
     extern __shared__ __attribute__((aligned(16))) float S[];
     const int b = blockIdx.x;
     const int fam = a.dual ? (int)blockIdx.y : 1;
@@ -498,7 +501,9 @@ static void extract_lds_launch(const ExtractArgs& a, size_t lds, hipStream_t s) 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         attr = true;
     }
-    HGNN_KLAUNCH(k_extract_lds<JT>, dim3(a.bs, a.dual ? 2 : 1), dim3(XL_THREADS), lds, s, a);
+    ExtractArgs as = a;
+    as.stamps = clock_stamps((long long)a.bs * (a.dual ? 2 : 1) * (XL_THREADS / 64));
+    HGNN_KLAUNCH(k_extract_lds<JT>, dim3(a.bs, a.dual ? 2 : 1), dim3(XL_THREADS), lds, s, as);
 }
 
 static int extract_one(const ExtractArgs& a, dim3 grid, hipStream_t s) {
@@ -592,7 +597,8 @@ int launch_pack_edges(const float* XL, int bs, int emax, BatchMeta m, float* out
 }
 
 __global__ void k_unpack_nodes(const float* __restrict__ in, int f, int nmax, BatchMeta m,
-                               float* __restrict__ X) {
+                               float* __restrict__ X, uint64_t* stamps) {
+    WaveStamp stamp(stamps);
     const int b = blockIdx.x;
     const int n0 = m.node_off[b];
     const int nb = m.node_off[b + 1] - n0;
@@ -605,7 +611,7 @@ __global__ void k_unpack_nodes(const float* __restrict__ in, int f, int nmax, Ba
 
 int launch_unpack_nodes(const float* in, int bs, int f, int nmax, BatchMeta m, float* X,
                         hipStream_t s) {
-    HGNN_KLAUNCH(k_unpack_nodes, dim3(bs), dim3(128), 0, s, in, f, nmax, m, X);
+    HGNN_KLAUNCH(k_unpack_nodes, dim3(bs), dim3(128), 0, s, in, f, nmax, m, X, clock_stamps((long long)bs * 2));
     HGNN_LAUNCH_CHECK();
     return 0;
 }

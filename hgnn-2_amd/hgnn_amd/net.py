@@ -52,6 +52,18 @@ class KernelTimer:
         L.check(L.lib().hgnn_timer_elapsed(self.handle, kcls, ctypes.byref(ms), ctypes.byref(n)), "timer")
         return ms.value, n.value
 
+    def launches(self, max_launches=65536):
+        """Stamp mode: [(class, entry_us, exit_us, stream)] of every timed launch in enqueue order (us from
+        the region's first stamp; stream numbered in order of first appearance)."""
+        cls = (ctypes.c_int * max_launches)()
+        t0 = (ctypes.c_double * max_launches)()
+        t1 = (ctypes.c_double * max_launches)()
+        sq = (ctypes.c_int * max_launches)()
+        n = L.lib().hgnn_timer_launches(self.handle, max_launches, cls, t0, t1, sq)
+        if n < 0:
+            L.check(-n, "timer launches")
+        return [(cls[i], t0[i], t1[i], sq[i]) for i in range(min(n, max_launches))]
+
     def close(self):
         if self.handle:
             L.lib().hgnn_timer_destroy(self.handle)

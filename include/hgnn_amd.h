@@ -190,6 +190,11 @@ void hgnn_timer_reset(void* timer);
 /* Waits for the timed work (stamp mode: a device synchronisation and one copy of
  * the stamp buffer); sums the durations of class `kernel_class`. */
 int hgnn_timer_elapsed(void* timer, int kernel_class, double* total_ms, int* launches);
+/* Stamp mode: every timed launch in enqueue order -- its class, its first-entry / last-exit times in us
+ * from the region's earliest stamp (-1: no stamp) and (stream_idx, optional) the stream it went to, numbered
+ * in order of first appearance.  Returns the number of launches (up to `max` written), or minus an
+ * HGNN_ERR_* code. */
+int hgnn_timer_launches(void* timer, int max, int* cls, double* t_entry_us, double* t_exit_us, int* stream_idx);
 void hgnn_timer_destroy(void* timer);
 int hgnn_net_forward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
                            const float* const* params, float* const* bn_running,
