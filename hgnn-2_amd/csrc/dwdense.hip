@@ -122,7 +122,6 @@ template <int FC, int MAXI>
 __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     WaveStamp stamp(a.stamps);
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int b = blockIdx.x;
     const int nmax = a.nmax, F = a.f;
     const int J = a.jt, j0 = 0, JA = a.jt;
     const int npad = (nmax + 31) / 32 * 32;
@@ -136,6 +135,9 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     float* Bmu = Rs + J * FC;       // [FC] BN mean, scale, and the BN of 0 (padded rows)
     float* Bsc = Bmu + FC;
     float* Bz = Bsc + FC;
+    // graphs b, b + gridDim.x, ...: the grid may be smaller than the batch (launch_fc), so the kernel holds
+    // fewer of the side stream's CUs beside the main stream's backward
+    for (int b = blockIdx.x; b < a.bs; b += gridDim.x) {
     const int off = a.node_off[b];
     const int nb = a.node_off[b + 1] - off;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -221,6 +223,8 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
         }
     }
     }
+    __syncthreads();  // the next graph's staging overwrites the LDS images
+    }
 }
 
 template <int FC, int MAXI>
@@ -235,16 +239,29 @@ static void allow_lds(size_t lds) {
     }
 }
 
+// Blocks of the dense dW (x): one per graph when HGNN_DWD_GRID=0; else at most this many, each walking
+// graphs b, b + grid, ...  The kernel runs on the side stream at two waves per SIMD (~225 registers): one
+// block per graph (512 at config 2) holds every SIMD's wave slots and blocks the main stream's BN-backward
+// statistics kernel until it ends (round-5 stamp timeline: 7-14 us of main-stream idle per node half).
+static int dwd_grid(int bs) {
+    static const int g = [] {
+        const char* e = getenv("HGNN_DWD_GRID");
+        return e ? atoi(e) : 256;
+    }();
+    return g <= 0 ? bs : std::min(bs, g);
+}
+
 template <int FC>
 static void launch_fc(const DwDenseArgs& a0, int maxi, int gy, size_t lds, hipStream_t s) {
     DwDenseArgs a = a0;
-    a.stamps = clock_stamps((long long)a0.bs * gy * 4);
+    const int gx = dwd_grid(a0.bs);
+    a.stamps = clock_stamps((long long)gx * gy * 4);
     allow_lds<FC, 1>(lds);
     allow_lds<FC, 3>(lds);
     allow_lds<FC, 5>(lds);
-    if (maxi <= 1) HGNN_KLAUNCH((k_dw_dense<FC, 1>), dim3(a.bs, gy), dim3(256), lds, s, a);
-    else if (maxi <= 3) HGNN_KLAUNCH((k_dw_dense<FC, 3>), dim3(a.bs, gy), dim3(256), lds, s, a);
-    else HGNN_KLAUNCH((k_dw_dense<FC, 5>), dim3(a.bs, gy), dim3(256), lds, s, a);
+    if (maxi <= 1) HGNN_KLAUNCH((k_dw_dense<FC, 1>), dim3(gx, gy), dim3(256), lds, s, a);
+    else if (maxi <= 3) HGNN_KLAUNCH((k_dw_dense<FC, 3>), dim3(gx, gy), dim3(256), lds, s, a);
+    else HGNN_KLAUNCH((k_dw_dense<FC, 5>), dim3(gx, gy), dim3(256), lds, s, a);
 }
 
 // Narrow inputs (F <= 16: layer 0's node features, the GNN_simple layers of config 1): the outer
