@@ -484,8 +484,15 @@ static int side_stream(hipStream_t main_s, SideStream** out) {
         }
         ss = SideStream{};
         HGNN_HOST_CHECK(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
-        for (int i = 0; i < 2; ++i) HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming));
-        for (int i = 0; i <= BWD_NBUF; ++i) HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming));
+        // fork / join events without the system-scope fence of a record (hipEventDisableSystemFence): the two
+        // streams are on one device, so the producing kernel's end-of-kernel release and the consumer's
+        // dispatch acquire already order the data, and the fence's cache writeback / invalidate only delays
+        // the main stream's next kernel -- 1.163-1.169 vs 1.193-1.197 ms per step in three alternating pairs
+        // (profiles/r05_ab_event_fence.txt); HGNN_EVENT_FENCE=1 restores the fenced records
+        static const bool fence = env_flag("HGNN_EVENT_FENCE", false);
+        const unsigned ef = hipEventDisableTiming | (fence ? 0u : hipEventDisableSystemFence);
+        for (int i = 0; i < 2; ++i) HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.fork[i], ef));
+        for (int i = 0; i <= BWD_NBUF; ++i) HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[i], ef));
         ss.dev = dev;
         HGNN_HOST_CHECK(hipSetDevice(cur));
     }
