@@ -725,15 +725,6 @@ int dw3_chunks(int r_cap, int o, int k) {
     // (tools/dw_lab.hip) 48 chunks x 5 tiles = 240 blocks ran 41.5 us (0.58 of the fp32 MFMA peak),
     // 56 x 5 = 280 blocks (a second partial round on 24 CUs) 55 us
     chunks = std::min(chunks, ceil_div(r_cap > 0 ? r_cap : 1, 64));
-    // narrow aggregates (layer 0: K = 13 / 271 at config 2) give a chunk so little work that the slab
-    // reduction's depth is the cost: at least 64 * 128 / K rows per chunk (K = 16: 512 rows, 64 chunks
-    // instead of 256; the last half's dW ends the backward's side stream, round-5 timeline)
-    static const bool narrow_cap = [] {
-        const char* e = getenv("HGNN_DW_NARROW_CAP");
-        return !e || e[0] != '0';
-    }();
-    if (narrow_cap && k < 128)
-        chunks = std::min(chunks, std::max(8, ceil_div(r_cap > 0 ? r_cap : 1, 64 * 128 / std::max(k, 1))));
     // a multiple of 8 keeps the XCD-aware order (launch_gemm3_dw); when rounding down would idle more
     // than a fifth of the target (config 4: 20 output tiles, 12 -> 8 chunks = 160 blocks on 256 CUs)
     // the exact count runs in the linear order instead
