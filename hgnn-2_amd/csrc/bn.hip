@@ -44,26 +44,10 @@ __global__ void __launch_bounds__(256) k_bn_finalize(BnFwdArgs a) {
     const int rows = *a.count;
     const int tiles = ceil_div(rows, 64);
     constexpr int U = 8;
-    double n = 0.0, s = 0.0;
-    for (int t0 = 0; t0 < tiles; t0 += 64 * U) {
-        float pn[U], pm[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int t = min(t0 + u * 64 + lane, max(tiles - 1, 0));
-            const float* p = a.part + ((long long)t * a.c + ch) * 3;
-            pn[u] = p[0];
-            pm[u] = p[1];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (t0 + u * 64 + lane < tiles) {
-                n += (double)pn[u];
-                s += (double)pn[u] * (double)pm[u];
-            }
-    }
-    const double N = wave_sum_d(n), S = wave_sum_d(s);
-    const double mean = N > 0.0 ? S / N : 0.0;
-    double q = 0.0;
+    // one pass: each lane merges its tiles' (count, mean, M2) into an fp64 (n, mean, M2) by Chan's update,
+    // then the wave merges the 64 triples the same way (DPP-free shuffles) -- a single round of partial loads
+    // instead of a mean pass and an M2 pass
+    double n = 0.0, mu = 0.0, m2 = 0.0;
     for (int t0 = 0; t0 < tiles; t0 += 64 * U) {
         float pn[U], pm[U], pq[U];
 #pragma unroll
@@ -76,12 +60,30 @@ __global__ void __launch_bounds__(256) k_bn_finalize(BnFwdArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (t0 + u * 64 + lane < tiles) {
-                const double dm = (double)pm[u] - mean;
-                q += (double)pq[u] + (double)pn[u] * dm * dm;
+            if (t0 + u * 64 + lane < tiles && pn[u] > 0.f) {
+                const double nb = (double)pn[u], nn = n + nb, d = (double)pm[u] - mu;
+                mu += d * (nb / nn);
+                m2 += (double)pq[u] + d * d * (n * nb / nn);
+                n = nn;
             }
     }
-    const double M2 = wave_sum_d(q);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(mu, o, 64), qb = __shfl_xor(m2, o, 64);
+        const double nn = n + nb;
+        if (nn > 0.0) {
+            // the same operation on both lanes of the pair: the operand with the smaller count (the lower
+            // lane on a tie) is "lo" on both, and the M2 terms are added commutatively
+            const double d = mb - mu;
+            const bool lo = n < nb || (n == nb && (lane & o) == 0);
+            const double mlo = lo ? mu : mb, mhi = lo ? mb : mu, nlo = lo ? n : nb;
+            const double mnew = mlo + (mhi - mlo) * ((nn - nlo) / nn);
+            m2 = m2 + qb + d * d * (n * nb / nn);
+            mu = mnew;
+        }
+        n = nn;
+    }
+    const double N = n, mean = mu, M2 = m2;
     if (lane == 0) {
         const double var = 1e-5 + (N > 0.0 ? M2 / N : 0.0);
         const float mf = (float)mean;
