@@ -82,31 +82,35 @@ __global__ void __launch_bounds__(256) k_dw_reduce2(const float* __restrict__ sl
 }
 
 // Slab sums with float4 columns (the default when the shapes allow): a wave sums 256 consecutive outputs of its
-// slab group (1 KB per slab row, coalesced), the four waves of a block take interleaved slab groups and
-// are combined in order through LDS; the bias gradients as in k_dw_reduce2.
-__global__ void __launch_bounds__(256) k_dw_reduce4(const float* __restrict__ slabs, const int* r_valid, int nz, int M,
+// slab group (1 KB per slab row, coalesced), the NW waves of a block take interleaved slab groups and
+// are combined in order through LDS; the bias gradients as in k_dw_reduce2.  NW = 16 for small outputs (the
+// narrow layer-0 dW: 2 048 outputs, 8 blocks, each wave 64 slabs deep at NW = 4 -- a latency chain at the end
+// of the backward's side stream), else 4.
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_dw_reduce4(const float* __restrict__ slabs, const int* r_valid, int nz, int M,
                                                     int MR, int N, int split, float* dw0, float* dw1,
                                                     const float* __restrict__ dbpart, float* db0, float* db1,
                                                     uint64_t* stamps) {
     WaveStamp stamp(stamps);
     const int total = MR * N, nwb = (total + 255) / 256;
     if ((int)blockIdx.x >= nwb) {
-        __shared__ double red[4];
+        __shared__ double red[NW];
         const int o = blockIdx.x - nwb;
         const int tv = ceil_div(*r_valid, 64);
         double s = 0.0;
-        for (int t = threadIdx.x; t < tv; t += 256) s += (double)dbpart[(long long)t * MR + o];
+        for (int t = threadIdx.x; t < tv; t += 64 * NW) s += (double)dbpart[(long long)t * MR + o];
         s = wave_sum_d(s);
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
         __syncthreads();
         if (threadIdx.x == 0) {
-            const double t = red[0] + red[1] + red[2] + red[3];
+            double t = 0.0;
+            for (int q = 0; q < NW; ++q) t += red[q];
             if (o < split) db0[o] = (float)t;
             else db1[o - split] = (float)t;
         }
         return;
     }
-    __shared__ float4 part[4][64];
+    __shared__ float4 part[NW][64];
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int idx = blockIdx.x * 256 + 4 * lane;  // first of this lane's four outputs (total % 4 == 0)
     const int rows = *r_valid;
@@ -115,13 +119,13 @@ __global__ void __launch_bounds__(256) k_dw_reduce4(const float* __restrict__ sl
     float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
     if (idx < total) {
         int z = g;
-        for (; z + 4 < zv; z += 8) {
+        for (; z + NW < zv; z += 2 * NW) {
             const float4 a = *reinterpret_cast<const float4*>(slabs + z * st + idx);
-            const float4 b = *reinterpret_cast<const float4*>(slabs + (z + 4) * st + idx);
+            const float4 b = *reinterpret_cast<const float4*>(slabs + (z + NW) * st + idx);
             s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
             s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
         }
-        for (; z < zv; z += 4) {
+        for (; z < zv; z += NW) {
             const float4 a = *reinterpret_cast<const float4*>(slabs + z * st + idx);
             s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
         }
@@ -131,7 +135,7 @@ __global__ void __launch_bounds__(256) k_dw_reduce4(const float* __restrict__ sl
     if (g == 0 && idx < total) {
         float4 t = part[0][lane];
 #pragma unroll
-        for (int q = 1; q < 4; ++q) {
+        for (int q = 1; q < NW; ++q) {
             const float4 v = part[q][lane];
             t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
         }
@@ -152,8 +156,13 @@ int launch_dw_reduce2(const float* slabs, const int* r_valid, int nz, int o, int
     // slab groups by the slab count: more groups when there are many slabs per output
     const int nb = dbpart ? o_real : 0;
     if (total % 4 == 0 && ((long long)o * k) % 4 == 0 && ((uintptr_t)slabs & 15) == 0) {
-        HGNN_KLAUNCH(k_dw_reduce4, dim3(ceil_div(total, 256) + nb), dim3(256), 0, s, slabs, r_valid, nz, o, o_real,
-                     k, split, dw0, dw1, dbpart, db0, db1, clock_stamps((long long)(ceil_div(total, 256) + nb) * 4));
+        const int nwb = ceil_div(total, 256);
+        if (nwb <= 64)
+            HGNN_KLAUNCH(k_dw_reduce4<16>, dim3(nwb + nb), dim3(1024), 0, s, slabs, r_valid, nz, o, o_real, k, split,
+                         dw0, dw1, dbpart, db0, db1, clock_stamps((long long)(nwb + nb) * 16));
+        else
+            HGNN_KLAUNCH(k_dw_reduce4<4>, dim3(nwb + nb), dim3(256), 0, s, slabs, r_valid, nz, o, o_real, k, split,
+                         dw0, dw1, dbpart, db0, db1, clock_stamps((long long)(nwb + nb) * 4));
     } else if (nz > 32) {
         HGNN_KLAUNCH(k_dw_reduce2<16>, dim3(ceil_div(total, 16) + nb), dim3(256), 0, s, slabs, r_valid, nz,
                            o, o_real, k, split, dw0, dw1, dbpart, db0, db1);
