@@ -822,6 +822,8 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     // each mid-backward join idles the main stream.)
     bool pending[BWD_NBUF] = {};
     int slot = 0, q = 0;
+    // HGNN_BWD_TAIL=0: the round-4 tail (the last half forks after its dA GEMM, dX unpacked after the join)
+    static const bool bwd_tail = env_flag("HGNN_BWD_TAIL", true);
     // The side stream also takes the dense operator gradient (W.requires_grad) of a node
     // half: it only accumulates into dW, so it leaves the dA -> aggregation-backward chain.
     // (Measured alternative, not kept: the gather half of the aggregation backward on a third
@@ -909,10 +911,14 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         // the side stream's dense dW reads a node half's dA: its own slot buffer; other halves share P.da
         const bool ndw_side = ndw && side;
         float* da = at<float>(ws, ndw_side && P.dak[slot] ? P.dak[slot] : P.da);
+        // the last half of the walk (no dense dW, which reads dA) forks before its dA GEMM: the side stream's
+        // dW + reduce is the step's tail there, nothing on the main stream follows to overlap it
+        const bool early = side && hi == 0 && !ndw && bwd_tail;
+        if (early) TRY(fork_dw(h, cap, tot, dyb, dbp, false, nullptr));
         TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2p, tot, cap, P.c2p, at<float>(ws, h.wt), P.c2p, h.k, da, h.kp, s));
         // dW starts once dA is done: two MFMA GEMMs side by side only slow each other,
         // dW beside the latency-bound dense-dW / aggregation-backward kernels does not
-        TRY(fork_dw(h, cap, tot, dyb, dbp, ndw, da));
+        if (!early) TRY(fork_dw(h, cap, tot, dyb, dbp, ndw, da));
         AggBwdArgs gab{}, pab{};
         if (ng) {
             gab.total_rows = tot;
@@ -953,10 +959,15 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         TRY(half_bwd(hi));
         TRY(mark(hi));
     }
-    if (side) {  // the side stream runs in order: its last work done means all of it is
-        HGNN_HOST_CHECK(hipEventRecord(side->join[BWD_NBUF], side->s));
-        HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[BWD_NBUF], 0));
-    }
+    auto join_side = [&]() -> int {  // the side stream runs in order: its last work done means all of it is
+        if (side) {
+            HGNN_HOST_CHECK(hipEventRecord(side->join[BWD_NBUF], side->s));
+            HGNN_HOST_CHECK(hipStreamWaitEvent(s, side->join[BWD_NBUF], 0));
+        }
+        return 0;
+    };
+    // dX reads only the main stream's aggregation gradients: unpacked before the join (HGNN_BWD_TAIL=0: after)
+    if (!bwd_tail) TRY(join_side());
     if (c->need_dx) {
         if (!dX) return HGNN_ERR_ARG;
         if (!init[0]) HGNN_HOST_CHECK(hipMemsetAsync(at<float>(ws, P.feats[0].grad), 0,
@@ -967,6 +978,7 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         else
             TL(HGNN_K_STRUCT, launch_unpack_nodes(at<float>(ws, P.feats[0].grad), c->bs, c->f_in, c->nmax, m, dX, s));
     }
+    if (bwd_tail) TRY(join_side());
     return 0;
 }
 
