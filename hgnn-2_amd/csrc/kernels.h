@@ -58,6 +58,7 @@ struct ExtractArgs {
     float* xo;
     float* xlo;
     uint64_t* stamps;  // the launch's stamp slot under a stamp-mode clock (common.h WaveStamp), else null
+    int dbg;           // diagnostics (HGNN_XR_DBG, k_extract_reg): 1 = stop after the loads, 2 = after the marks
 };
 int launch_extract(const ExtractArgs& a, hipStream_t s);
 

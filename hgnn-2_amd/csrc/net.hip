@@ -1368,6 +1368,30 @@ int hgnn_timer_launches(void* timer, int max, int* cls, double* t_entry_us, doub
     return t->used;
 }
 
+long long hgnn_timer_waves(void* timer, int launch, long long max, double* entry_us, double* exit_us) {
+    if (!timer || max < 0 || (max > 0 && (!entry_us || !exit_us))) return -HGNN_ERR_ARG;
+    Timer* t = static_cast<Timer*>(timer);
+    if (t->mode != HGNN_TIMER_STAMPS) return -HGNN_ERR_UNSUPPORTED;
+    if (launch < 0 || launch >= t->used) return -HGNN_ERR_ARG;
+    if (hipDeviceSynchronize() != hipSuccess) return -HGNN_ERR_HIP;
+    const int r = timer_read_stamps(t);
+    if (r) return -r;
+    uint64_t base = ~0ull;
+    for (int i = 0; i < t->used; ++i)
+        if (t->st_lo[i] && t->st_lo[i] < base) base = t->st_lo[i];
+    const long long nw = t->st_n[launch] / 2, n = nw < max ? nw : max;
+    if (n > 0) {
+        std::vector<uint64_t> h((size_t)(2 * n));
+        if (hipMemcpy(h.data(), t->st + t->st_off[launch], (size_t)(2 * n) * 8, hipMemcpyDeviceToHost) != hipSuccess)
+            return -HGNN_ERR_HIP;
+        for (long long w = 0; w < n; ++w) {
+            entry_us[w] = h[2 * w] ? (double)(h[2 * w] - base) * 1e-2 : -1.0;
+            exit_us[w] = h[2 * w + 1] ? (double)(h[2 * w + 1] - base) * 1e-2 : -1.0;
+        }
+    }
+    return nw;
+}
+
 void hgnn_timer_destroy(void* timer) {
     if (!timer) return;
     Timer* t = static_cast<Timer*>(timer);

@@ -366,6 +366,24 @@ __global__ void __launch_bounds__(X_THREADS) k_extract(ExtractArgs a) {
 constexpr int XL_THREADS = 512;
 
 __device__ __forceinline__ void lds_fill(float* __restrict__ dst, const float* __restrict__ src, int n) {
+    if ((reinterpret_cast<uintptr_t>(src) & 15) == 0 && (n & 3) == 0) {
+        // 16-B loads (the line-graph block of config 2: 3 675 float4, one round of 8 per thread)
+        constexpr int U = 8;
+        const int n4 = n >> 2;
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (int base = 0; base < n4; base += XL_THREADS * U) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = s4[min(base + u * XL_THREADS + (int)threadIdx.x, n4 - 1)];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = base + u * XL_THREADS + threadIdx.x;
+                if (i < n4) d4[i] = v[u];
+            }
+        }
+        return;
+    }
     constexpr int U = 16;
     for (int base = 0; base < n; base += XL_THREADS * U) {
         float v[U];
@@ -412,16 +430,37 @@ __device__ void lds_rows(const float* S0, const float* S1, int rows, int cols, i
     }
 }
 
-// Any nonzero of an LDS (R, C, NC) block outside [0, rr) x [0, rc) (NC = 1 per array for Pm / Pd).
+// Any nonzero of an LDS (R, C, NC) block outside [0, rr) x [0, rc) (NC = 1 per array for Pm / Pd): a wave per
+// row, lanes along the row -- rows past rr whole, live rows from column rc on.  (A flat sweep with the row and
+// column recovered by two integer divisions per element cost ~2 000 VALU per thread on the line-graph block.)
 __device__ void lds_validate(const float* S, int R, int C, int NC, int rr, int rc, uint32_t* err) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = XL_THREADS / 64;
+    const int row = C * NC, live = rc * NC;
     bool bad = false;
-    const int n = R * C * NC;
-    for (int i = threadIdx.x; i < n; i += XL_THREADS) {
-        const int r = i / (C * NC), c = (i / NC) % C;
-        if ((r >= rr || c >= rc) && S[i] != 0.f) bad = true;
-    }
-    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, (uint32_t)ERR_PAD_NONZERO);
+    for (int r = wv; r < R; r += nw)
+        for (int k = (r < rr ? live : 0) + lane; k < row; k += 64) bad |= S[r * row + k] != 0.f;
+    if (__any(bad) && lane == 0) atomicOr(err, (uint32_t)ERR_PAD_NONZERO);
 }
+
+// validate_mask's loads issued ahead of the LDS fill (n <= XL_THREADS: one per thread), checked after it
+struct MaskProbe {
+    float v = 0.f;
+    bool on = false;
+    __device__ void issue(const float* __restrict__ mask, int n, bool validate) {
+        on = validate && n <= XL_THREADS;
+        if (on && (int)threadIdx.x < n) v = mask[(long long)threadIdx.x * n];
+    }
+    __device__ void check(const float* __restrict__ mask, int n, int real, bool validate, uint32_t* err) const {
+        if (!validate) return;
+        if (!on) {
+            validate_mask(mask, n, real, err);
+            return;
+        }
+        const int i = threadIdx.x;
+        const bool bad = i < n && v != ((i < real && real > 0) ? 1.f : 0.f);
+        if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, (uint32_t)ERR_MASK);
+    }
+};
 
 template <int JT>
 __global__ void __launch_bounds__(XL_THREADS) k_extract_lds(ExtractArgs a) {
@@ -434,6 +473,9 @@ __global__ void __launch_bounds__(XL_THREADS) k_extract_lds(ExtractArgs a) {
     if (fam == 0) {
         const int e0 = a.meta.edge_off[b], eb = a.meta.edge_off[b + 1] - e0;
         const int n = emax * emax * JT;
+        const float* mk = a.mask_lg + (long long)b * emax * emax;
+        MaskProbe mp;
+        mp.issue(mk, emax, a.validate);
         lds_fill(S, a.WL + (long long)b * n, n);
         __syncthreads();
         const long long slot0 = (long long)b * emax * emax;
@@ -444,7 +486,7 @@ __global__ void __launch_bounds__(XL_THREADS) k_extract_lds(ExtractArgs a) {
                      a.entry_stride_w);
         if (a.validate) {
             lds_validate(S, emax, emax, JT, eb, eb, a.meta.err);
-            validate_mask(a.mask_lg + (long long)b * emax * emax, emax, eb, a.meta.err);
+            mp.check(mk, emax, eb, true, a.meta.err);
         }
         if (a.xlo)  // the packed edge input (k_pack_edges' work)
             for (int i = threadIdx.x; i < eb; i += XL_THREADS) a.xlo[e0 + i] = a.XL[(long long)b * emax + i];
@@ -459,6 +501,9 @@ __global__ void __launch_bounds__(XL_THREADS) k_extract_lds(ExtractArgs a) {
     float* SW = S;
     float* SM = S + nw_;
     float* SD = SM + np;
+    const float* mk = a.mask + (long long)b * nmax * nmax;
+    MaskProbe mp;
+    mp.issue(mk, nmax, a.validate);
     lds_fill(SW, a.W + (long long)b * nw_, nw_);
     if (a.dual) {
         lds_fill(SM, a.Pm + (long long)b * np, np);
@@ -472,7 +517,7 @@ __global__ void __launch_bounds__(XL_THREADS) k_extract_lds(ExtractArgs a) {
                  a.entry_stride_w);
     if (a.validate) {
         lds_validate(SW, nmax, nmax, JT, nb, nb, a.meta.err);
-        validate_mask(a.mask + (long long)b * nmax * nmax, nmax, nb, a.meta.err);
+        mp.check(mk, nmax, nb, true, a.meta.err);
     }
     if (!a.dual) return;
     const int e0 = a.meta.edge_off[b], eb = a.meta.edge_off[b + 1] - e0;
@@ -483,6 +528,263 @@ __global__ void __launch_bounds__(XL_THREADS) k_extract_lds(ExtractArgs a) {
         lds_validate(SM, nmax, emax, 1, nb, eb, a.meta.err);
         lds_validate(SD, nmax, emax, 1, nb, eb, a.meta.err);
     }
+}
+
+// ---- Register-staged extraction: one 512-thread block per graph takes all of the graph's dense operator blocks
+// (WL, W, Pm / Pd) into registers -- a wave per dense row, lanes along the row, every load of the block in flight
+// at once -- marks the live nonzeros in two LDS bitmaps (row-major and transposed), then writes every nonzero
+// entry straight to its place in both lists: the position is the count of set bits before it in its row (its
+// column) of the bitmap.  The lists are k_extract's, entry for entry (ascending columns per row, ascending rows
+// in a transposed row).  Padding is checked on the registers.  Against k_extract_lds: no 58.8-KB LDS copy of
+// the line-graph block, so the 512 blocks of config 2 are resident in one round (two per CU) -- the LDS kernel
+// ran its W / Pm / Pd blocks in a second round behind the line-graph blocks (per-wave stamps,
+// tools/wave_stats.py) -- and no flat LDS sweep for the padding check.  Shapes: a line-graph block of at most
+// 8 XR_MR_L rows of 256 floats, node blocks of at most 8 XR_MR_N rows of 128 floats (config 2: 70 x 210 and
+// 29 x 87 / 29 x 70); larger shapes take k_extract_lds / k_extract.
+constexpr int XR_THREADS = 512, XR_WAVES = XR_THREADS / 64, XR_MR_L = 9, XR_MCH_L = 4, XR_MR_N = 4, XR_MCH_N = 2;
+constexpr int XR_BITS = 2048;  // LDS words per block: bitmaps and their prefix counts
+
+struct XrList {  // one orientation's output: rows[row_packed0 + r] = {slot0 + r cap, count}, entries at slot
+    RowInfo* rows;
+    float* ent;
+    long long slot0;
+    int cap, row_packed0, col_packed0;
+};
+
+// A dense block of R x C elements, NC coefficients each: interleaved in s0 (W / WL: (r, c, j) at
+// s0[(r C + c) NC + j]) or, TWO, one in s0 and one in s1 (Pm / Pd: (r, c) at r C + c).  Live: [0, rr) x [0, rc).
+// LDS: the row-major bitmap [R][WR], the transposed one [C][WT], then their word prefix counts (same shapes).
+template <int NC, bool TWO, int MR, int MCH>
+struct XrBlock {
+    float v[MR][MCH];
+    float w[TWO ? MR : 1][TWO ? MCH : 1];
+    int R, C, rr, rc, L, WR, WT;
+    uint32_t* bits;
+    uint32_t* bitsT;
+    uint32_t* pre;   // [R][WR]: set bits of the row's words before this one
+    uint32_t* preT;  // [C][WT]
+
+    __device__ int words() const { return 2 * (R * WR + C * WT); }
+    __device__ void init(int R_, int C_, int rr_, int rc_, uint32_t* b) {
+        R = R_;
+        C = C_;
+        rr = rr_;
+        rc = rc_;
+        L = TWO ? C : C * NC;
+        WR = (C + 31) >> 5;
+        WT = (R + 31) >> 5;
+        bits = b;
+        bitsT = bits + R * WR;
+        pre = bitsT + C * WT;
+        preT = pre + R * WR;
+    }
+    // every load unconditional (clamped to a live address) and in flight before the first use
+    __device__ void load(const float* __restrict__ s0, const float* __restrict__ s1) {
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+        for (int i = 0; i < MR; ++i) {
+            const int rb = min(wv + XR_WAVES * i, R - 1) * L;
+#pragma unroll
+            for (int h = 0; h < MCH; ++h) {
+                const int o = rb + min(h * 64 + lane, L - 1);
+                v[i][h] = s0[o];
+                if constexpr (TWO) w[i][h] = s1[o];
+            }
+        }
+    }
+    __device__ bool nz(int i, int h) const {
+        if constexpr (TWO) return v[i][h] != 0.f || w[i][h] != 0.f;
+        return v[i][h] != 0.f;
+    }
+    // set the live nonzeros' bits; any nonzero outside the live region -> bad
+    __device__ void mark(bool& bad) const {
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+        for (int i = 0; i < MR; ++i) {
+            const int r = wv + XR_WAVES * i;
+            if (r >= R) break;
+#pragma unroll
+            for (int h = 0; h < MCH; ++h) {
+                const int k = h * 64 + lane, c = TWO ? k : k / NC;
+                if (k < L && nz(i, h)) {
+                    if (r < rr && c < rc) {
+                        atomicOr(&bits[r * WR + (c >> 5)], 1u << (c & 31));
+                        atomicOr(&bitsT[c * WT + (r >> 5)], 1u << (r & 31));
+                    } else {
+                        bad = true;
+                    }
+                }
+            }
+        }
+    }
+    // after the marks' barrier: the word prefix counts (a barrier follows before scatter)
+    __device__ void prefix() const {
+        for (int x = threadIdx.x; x < R * WR + C * WT; x += XR_THREADS) {
+            const bool t = x >= R * WR;
+            const int y = t ? x - R * WR : x, W = t ? WT : WR, q = y % W;
+            const uint32_t* bw = (t ? bitsT : bits) + (y - q);
+            uint32_t n = 0;
+            for (int z = 0; z < q; ++z) n += __popc(bw[z]);
+            (t ? preT : pre)[y] = n;
+        }
+    }
+    __device__ void scatter(const XrList& o, const XrList& t, int stride) const {
+        const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+        if (tid < rr) {
+            const int q = (tid + 1) * WR - 1;
+            o.rows[o.row_packed0 + tid] = RowInfo{(int)(o.slot0 + (long long)tid * o.cap), (int)(pre[q] + __popc(bits[q]))};
+        }
+        if (tid < rc) {
+            const int q = (tid + 1) * WT - 1;
+            t.rows[t.row_packed0 + tid] = RowInfo{(int)(t.slot0 + (long long)tid * t.cap), (int)(preT[q] + __popc(bitsT[q]))};
+        }
+        // per row: its elements' bitmap and prefix reads first (clamped, unconditional), then the positions and
+        // the stores (32-bit entry indices within the graph's lists: checked on the host)
+        float* const oe = o.ent + o.slot0 * stride;
+        float* const te = t.ent + t.slot0 * stride;
+#pragma unroll
+        for (int i = 0; i < MR; ++i) {
+            const int r = wv + XR_WAVES * i;
+            if (r >= rr) break;
+            uint32_t bw[MCH], bp[MCH], tw[MCH], tp[MCH];
+#pragma unroll
+            for (int h = 0; h < MCH; ++h) {
+                const int k = min(h * 64 + lane, L - 1), c = min(TWO ? k : k / NC, C - 1);
+                const int x = r * WR + (c >> 5), y = c * WT + (r >> 5);
+                bw[h] = bits[x];
+                bp[h] = pre[x];
+                tw[h] = bitsT[y];
+                tp[h] = preT[y];
+            }
+#pragma unroll
+            for (int h = 0; h < MCH; ++h) {
+                const int k = h * 64 + lane, c = TWO ? k : k / NC, j = TWO ? 0 : k - c * NC;
+                const uint32_t bit = 1u << (c & 31), rbit = 1u << (r & 31);
+                if (k < L && c < rc && (bw[h] & bit)) {
+                    const int pos = (int)(bp[h] + __popc(bw[h] & (bit - 1u)));
+                    const int tpos = (int)(tp[h] + __popc(tw[h] & (rbit - 1u)));
+                    float* e = oe + (r * o.cap + pos) * stride;
+                    float* et = te + (c * t.cap + tpos) * stride;
+                    if constexpr (TWO) {
+                        e[0] = __int_as_float(o.col_packed0 + c);
+                        e[1] = v[i][h];
+                        e[2] = w[i][h];
+                        et[0] = __int_as_float(t.col_packed0 + r);
+                        et[1] = v[i][h];
+                        et[2] = w[i][h];
+                    } else {
+                        if (j == 0) {
+                            e[0] = __int_as_float(o.col_packed0 + c);
+                            et[0] = __int_as_float(t.col_packed0 + r);
+                        }
+                        e[1 + j] = v[i][h];
+                        et[1 + j] = v[i][h];
+                    }
+                }
+            }
+        }
+    }
+};
+
+// (at most 128 VGPRs: two blocks per CU, so config 2's 512 blocks are resident in one round)
+template <int JT>
+__global__ void __launch_bounds__(XR_THREADS) __attribute__((amdgpu_waves_per_eu(4))) k_extract_reg(ExtractArgs a) {
+    WaveStamp stamp(a.stamps);
+    __shared__ uint32_t xb[XR_BITS];
+    const int b = blockIdx.x;
+    const int nmax = a.nmax, emax = a.emax;
+    const int n0 = a.meta.node_off[b], nb = a.meta.node_off[b + 1] - n0;
+    const int e0 = a.dual ? a.meta.edge_off[b] : 0, eb = a.dual ? a.meta.edge_off[b + 1] - e0 : 0;
+    const long long wblk = (long long)nmax * nmax * JT, lblk = (long long)emax * emax * JT,
+                    pblk = (long long)nmax * emax;
+    XrBlock<JT, false, XR_MR_L, XR_MCH_L> gl;
+    XrBlock<JT, false, XR_MR_N, XR_MCH_N> gw;
+    XrBlock<2, true, XR_MR_N, XR_MCH_N> gp;
+    gw.init(nmax, nmax, nb, nb, xb);
+    int used = gw.words();
+    if (a.dual) {
+        gl.init(emax, emax, eb, eb, xb + used);
+        used += gl.words();
+        gp.init(nmax, emax, nb, eb, xb + used);
+        used += gp.words();
+    }
+    for (int i = threadIdx.x; i < used; i += XR_THREADS) xb[i] = 0u;
+    __syncthreads();
+    const float* mkn = a.mask + (long long)b * nmax * nmax;
+    const float* mke = a.dual ? a.mask_lg + (long long)b * emax * emax : nullptr;
+    MaskProbe mpn, mpe;
+    mpn.issue(mkn, nmax, a.validate);
+    if (a.dual) {
+        mpe.issue(mke, emax, a.validate);
+        gl.load(a.WL + b * lblk, nullptr);
+        gp.load(a.Pm + b * pblk, a.Pd + b * pblk);
+    }
+    gw.load(a.W + b * wblk, nullptr);
+    // the packed inputs (k_pack_nodes / k_pack_edges' work) while the loads are in flight
+    if (a.xo)
+        for (int i = threadIdx.x; i < nb * a.f; i += XR_THREADS) {
+            const int n = i / a.f, c = i - n * a.f;
+            a.xo[(long long)(n0 + n) * a.f + c] = a.X[((long long)b * a.f + c) * nmax + n];
+        }
+    if (a.dual && a.xlo)
+        for (int i = threadIdx.x; i < eb; i += XR_THREADS) a.xlo[e0 + i] = a.XL[(long long)b * emax + i];
+    bool bad = false;
+    if (a.dbg == 1) {  // diagnostics: the loads only
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < XR_MR_L; ++i)
+#pragma unroll
+            for (int h = 0; h < XR_MCH_L; ++h) t += gl.v[i][h];
+#pragma unroll
+        for (int i = 0; i < XR_MR_N; ++i)
+#pragma unroll
+            for (int h = 0; h < XR_MCH_N; ++h) t += gw.v[i][h] + gp.v[i][h] + gp.w[i][h];
+        if (t == 1.2345f) atomicOr(a.meta.err, 0u);
+        return;
+    }
+    if (a.dual) {
+        gl.mark(bad);
+        gp.mark(bad);
+    }
+    gw.mark(bad);
+    __syncthreads();
+    if (a.dbg == 2) return;
+    gw.prefix();
+    if (a.dual) {
+        gl.prefix();
+        gp.prefix();
+    }
+    __syncthreads();
+    const long long sw = (long long)b * nmax * nmax;
+    gw.scatter(XrList{a.rows[S_W], a.entries[S_W], sw, nmax, n0, n0},
+               XrList{a.rows[S_WT], a.entries[S_WT], sw, nmax, n0, n0}, a.entry_stride_w);
+    if (a.dual) {
+        const long long sl = (long long)b * emax * emax, sp = (long long)b * nmax * emax;
+        gl.scatter(XrList{a.rows[S_WL], a.entries[S_WL], sl, emax, e0, e0},
+                   XrList{a.rows[S_WLT], a.entries[S_WLT], sl, emax, e0, e0}, a.entry_stride_w);
+        gp.scatter(XrList{a.rows[S_PN], a.entries[S_PN], sp, emax, n0, e0},
+                   XrList{a.rows[S_PE], a.entries[S_PE], sp, nmax, e0, n0}, 4);
+    }
+    if (a.validate) {
+        if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(a.meta.err, (uint32_t)ERR_PAD_NONZERO);
+        mpn.check(mkn, nmax, nb, true, a.meta.err);
+        if (a.dual) mpe.check(mke, emax, eb, true, a.meta.err);
+    }
+}
+
+// the register-staged extraction's shape limits (see k_extract_reg)
+static bool extract_reg_fits(const ExtractArgs& a) {
+    const int J = a.jtot;
+    if (a.nmax < 1 || a.nmax > XR_WAVES * XR_MR_N || a.nmax * J > 64 * XR_MCH_N) return false;
+    long long words = a.nmax * ((a.nmax + 31) / 32) * 2;
+    if (a.dual) {
+        if (a.emax < 1 || a.emax > XR_WAVES * XR_MR_L || a.emax * J > 64 * XR_MCH_L || a.emax > 64 * XR_MCH_N)
+            return false;
+        words += 2 * a.emax * ((a.emax + 31) / 32) + a.nmax * ((a.emax + 31) / 32) + a.emax * ((a.nmax + 31) / 32);
+    }
+    // (bitmaps and prefix counts; entry indices within one graph's lists in 32 bits)
+    const long long blk = (long long)std::max(a.nmax, a.emax) * std::max(a.nmax, a.emax) * std::max(a.entry_stride_w, 4);
+    return 2 * words <= XR_BITS && a.entry_stride_w >= 1 + J && blk < (1ll << 31);
 }
 
 // LDS bytes of the staged extraction (0: does not fit, use k_extract)
@@ -524,6 +826,30 @@ int launch_extract(const ExtractArgs& a, hipStream_t s) {
         const char* e = getenv("HGNN_EXTRACT_LDS");
         return !(e && e[0] == '0');
     }();
+    // HGNN_EXTRACT_REG=0: the LDS-staged kernel for the shapes the register-staged one takes
+    static const bool reg = [] {
+        const char* e = getenv("HGNN_EXTRACT_REG");
+        return !(e && e[0] == '0');
+    }();
+    if (staged && reg && a.kind0 == 0 && extract_reg_fits(a)) {
+        ExtractArgs as = a;
+        static const int dbg = [] {
+            const char* e = getenv("HGNN_XR_DBG");
+            return e ? atoi(e) : 0;
+        }();
+        // (diagnostics: a truncated launch ahead of the real one, which then runs as always)
+        for (int pass = dbg > 0 ? 0 : 1; pass < 2; ++pass) {
+            as.dbg = pass == 0 ? dbg : 0;
+            as.stamps = clock_stamps((long long)a.bs * XR_WAVES);
+            switch (a.jtot) {
+                case 3: HGNN_KLAUNCH(k_extract_reg<3>, dim3(a.bs), dim3(XR_THREADS), 0, s, as); break;
+                case 4: HGNN_KLAUNCH(k_extract_reg<4>, dim3(a.bs), dim3(XR_THREADS), 0, s, as); break;
+                default: return 2;  // (jtot > 4 never fits: 3 node rows of 128 floats)
+            }
+        }
+        HGNN_LAUNCH_CHECK();
+        return 0;
+    }
     const size_t lds = extract_lds_bytes(a);
     if (staged && lds > 0 && a.kind0 == 0) {
         switch (a.jtot) {

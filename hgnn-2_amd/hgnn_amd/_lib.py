@@ -92,6 +92,8 @@ SIGNATURES = {
     "hgnn_timer_destroy": ([_VP], None),
     "hgnn_timer_launches": ([_VP, _I, ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)], _I),
+    "hgnn_timer_waves": ([_VP, _I, ctypes.c_longlong, ctypes.POINTER(ctypes.c_double),
+                          ctypes.POINTER(ctypes.c_double)], ctypes.c_longlong),
     "hgnn_net_forward_timed": ([ctypes.POINTER(NetConfig), ctypes.POINTER(NetInputs), _VP, _VP, _VP, _VP, _VP,
                                 _VP], _I),
     "hgnn_net_backward_timed": ([ctypes.POINTER(NetConfig), ctypes.POINTER(NetInputs), _VP, _VP, _VP, _VP, _VP,

@@ -64,6 +64,16 @@ class KernelTimer:
             L.check(-n, "timer launches")
         return [(cls[i], t0[i], t1[i], sq[i]) for i in range(min(n, max_launches))]
 
+    def waves(self, launch, max_waves=1 << 20):
+        """Stamp mode: [(entry_us, exit_us)] of every wave of timed launch `launch` (enqueue order), in the
+        kernel's wave order (linear block id x waves per block + wave)."""
+        t0 = (ctypes.c_double * max_waves)()
+        t1 = (ctypes.c_double * max_waves)()
+        n = L.lib().hgnn_timer_waves(self.handle, launch, max_waves, t0, t1)
+        if n < 0:
+            L.check(-n, "timer waves")
+        return [(t0[i], t1[i]) for i in range(min(n, max_waves))]
+
     def close(self):
         if self.handle:
             L.lib().hgnn_timer_destroy(self.handle)

@@ -195,6 +195,11 @@ int hgnn_timer_elapsed(void* timer, int kernel_class, double* total_ms, int* lau
  * in order of first appearance.  Returns the number of launches (up to `max` written), or minus an
  * HGNN_ERR_* code. */
 int hgnn_timer_launches(void* timer, int max, int* cls, double* t_entry_us, double* t_exit_us, int* stream_idx);
+/* Stamp mode: the entry / exit times (us from the region's earliest stamp, -1: none) of every wave of timed
+ * launch `launch` (enqueue order), in the kernel's wave order (linear block id x waves per block + wave).
+ * Returns the launch's wave count (up to `max` written), or minus an HGNN_ERR_* code.  (Diagnostics:
+ * tools/wave_stats.py.) */
+long long hgnn_timer_waves(void* timer, int launch, long long max, double* entry_us, double* exit_us);
 void hgnn_timer_destroy(void* timer);
 int hgnn_net_forward_timed(const hgnn_net_config* cfg, const hgnn_net_inputs* in,
                            const float* const* params, float* const* bn_running,

@@ -226,6 +226,24 @@ def test_invalid_padding_and_mask_raise():
     mbad[i, n, 0] = 1.0
     with pytest.raises(RuntimeError, match="mask"):
         model([X, XL, W, WL, Pm, Pd], Nb, mbad, Eb, mask_lg)
+    # the line-graph block: a padded column of a live row, the last padded element; Pm / Pd padding;
+    # the line-graph mask
+    e = int(Eb[i])
+    for r, c, j in ((0, e, 1), (WL.shape[1] - 1, WL.shape[2] - 1, WL.shape[3] - 1)):
+        WLbad = WL.clone()
+        WLbad[i, r, c, j] = 0.5
+        with pytest.raises(RuntimeError, match="padding"):
+            model([X, XL, W, WLbad, Pm, Pd], Nb, mask, Eb, mask_lg)
+    for k in range(2):
+        P = (Pm, Pd)[k].clone()
+        P[i, 0, e] = 1.0  # a live node row, a padded edge column
+        args = [X, XL, W, WL, P, Pd] if k == 0 else [X, XL, W, WL, Pm, P]
+        with pytest.raises(RuntimeError, match="padding"):
+            model(args, Nb, mask, Eb, mask_lg)
+    mlbad = mask_lg.clone()
+    mlbad[i, e - 1, 0] = 0.0  # a live edge marked padded
+    with pytest.raises(RuntimeError, match="mask"):
+        model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mlbad)
     # a valid call still works afterwards
     model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
 
