@@ -134,7 +134,6 @@ int launch_bn_apply(const float* y, const int* total_rows, int cap_rows, int c, 
 }
 
 // ---------------------------------------------------------------- BN backward
-int bn_bwd_tiles(int cap_rows) { return ceil_div(cap_rows, 64); }
 
 // Per 64-row tile and channel: {sum g, sum g h, sum dz h, sum dz}, g = w dz, h = (y - mean) / std.
 __global__ void __launch_bounds__(256) k_bn_bwd_part(BnBwdArgs a) {
@@ -190,7 +189,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part(BnBwdArgs a) {
         red[3][threadIdx.x] = t2;
         __syncthreads();
         if (rg == 0 && ch < a.c) {
-            float* p = a.part + ((long long)tile * a.c + ch) * 4;
+            float* p = a.part + bn_bwd_part_index(ch, tile, bn_bwd_tiles(a.cap_rows));
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 float t = 0.f;
@@ -273,8 +272,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
             for (int q = 0; q < RG; ++q) t += f4c(red[j][q * L + l], comp);
             f4c(t4, j) = t;
         }
-        const long long idx = ((long long)tile * a.c + ch) * 4;
-        *reinterpret_cast<float4*>(a.part + idx) = t4;
+        *reinterpret_cast<float4*>(a.part + bn_bwd_part_index(ch, tile, bn_bwd_tiles(a.cap_rows))) = t4;
     }
 }
 
@@ -379,6 +377,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_fin(BnBwdArgs a) {
     const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (ch >= a.c) return;
     const int tiles = ceil_div(*a.total_rows, 64);
+    const int ntl = bn_bwd_tiles(a.cap_rows);  // the partials' tile stride
     constexpr int U = 8;
     double v[4] = {0.0, 0.0, 0.0, 0.0};
     for (int t0 = 0; t0 < tiles; t0 += 64 * U) {
@@ -386,7 +385,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_fin(BnBwdArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int t = min(t0 + u * 64 + lane, max(tiles - 1, 0));
-            pv[u] = *reinterpret_cast<const float4*>(a.part + ((long long)t * a.c + ch) * 4);
+            pv[u] = *reinterpret_cast<const float4*>(a.part + bn_bwd_part_index(ch, t, ntl));
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -1106,13 +1105,35 @@ __global__ void __launch_bounds__(RA_THREADS) k_readout_agg_bwd(ReadoutAggArgs a
         for (int j = 0; j < ns; ++j) CS[i * ns + j] = cs[j];
     }
     __syncthreads();
+    // a wave per row, lanes along the channels (float4 where C % 4 == 0: the row-major [rows][C] output of
+    // the executor always is); the flat (row, channel) loop's two integer divisions per element were most
+    // of this kernel's VALU
     const int acc = g ? a.g_acc : a.p_acc;
-    for (int i = threadIdx.x; i < nr * C; i += RA_THREADS) {
-        const int r = i / C, c = i % C;
-        float v = acc ? out[(long long)(r0 + r) * C + c] : 0.f;
-        for (int j = 0; j < ns; ++j) v = fmaf(CS[r * ns + j], R[j * C + c], v);
-        out[(long long)(r0 + r) * C + c] = v;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = RA_THREADS / 64;
+    if ((C & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+        for (int r = wv; r < nr; r += nw) {
+            float4* orow = reinterpret_cast<float4*>(out + (long long)(r0 + r) * C);
+            for (int c4 = lane; c4 < (C >> 2); c4 += 64) {
+                float4 v = acc ? orow[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int j = 0; j < ns; ++j) {
+                    const float w = CS[r * ns + j];
+                    const float4 q = *reinterpret_cast<const float4*>(R + j * C + 4 * c4);
+                    v.x = fmaf(w, q.x, v.x);
+                    v.y = fmaf(w, q.y, v.y);
+                    v.z = fmaf(w, q.z, v.z);
+                    v.w = fmaf(w, q.w, v.w);
+                }
+                orow[c4] = v;
+            }
+        }
+        return;
     }
+    for (int r = wv; r < nr; r += nw)
+        for (int c = lane; c < C; c += 64) {
+            float v = acc ? out[(long long)(r0 + r) * C + c] : 0.f;
+            for (int j = 0; j < ns; ++j) v = fmaf(CS[r * ns + j], R[j * C + c], v);
+            out[(long long)(r0 + r) * C + c] = v;
+        }
 }
 
 // dynamic LDS of the two readout-row kernels (beyond 64 KB allowed per kernel, up to the CU's 160 KB)
@@ -1191,9 +1212,14 @@ __global__ void __launch_bounds__(256) k_dw_readout(DwDenseArgs a) {
     __syncthreads();
     float* dWb = a.dW + (long long)b * nmax * nmax * J;
     const int per = nmax * J;
-    for (long long i = threadIdx.x; i < (long long)nmax * per; i += 256) {
-        const float u = U[i % per];
-        dWb[i] = a.accumulate ? dWb[i] + u : u;
+    // the same row u for every n: a thread per column t of the [n][per] block, walking the rows (no 64-bit
+    // modulo per element)
+    for (int t = threadIdx.x; t < per; t += 256) {
+        const float u = U[t];
+        for (int n = 0; n < nmax; ++n) {
+            float* q = dWb + (long long)n * per + t;
+            *q = a.accumulate ? *q + u : u;
+        }
     }
 }
 

@@ -308,7 +308,12 @@ struct BnBwdArgs {
 };
 // apply = 0: only the statistics (part + fin)
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply = 1);
-int bn_bwd_tiles(int cap_rows);
+__host__ __device__ inline int bn_bwd_tiles(int cap_rows) { return (cap_rows + 63) / 64; }
+// k_bn_bwd_part / part4 -> k_bn_bwd_fin partials: float4 {sum g, sum g h, sum dz h, sum dz} per (channel,
+// 64-row tile), channel-major [c][tiles] so the fin's per-channel loads are contiguous over the tiles
+__host__ __device__ inline long long bn_bwd_part_index(int ch, int tile, int tiles) {
+    return ((long long)ch * tiles + tile) * 4;
+}
 
 // dY of BN backward + ReLU for one element (batch_normalization.py:65-77 autograd):
 // g = w dz, h = (y - mean) / std, train: (g - m1 - h m2) / std with m1 = mean(g),
