@@ -44,46 +44,43 @@ __global__ void __launch_bounds__(256) k_bn_finalize(BnFwdArgs a) {
     const int rows = *a.count;
     const int tiles = ceil_div(rows, 64);
     constexpr int U = 8;
-    // one pass: each lane merges its tiles' (count, mean, M2) into an fp64 (n, mean, M2) by Chan's update,
-    // then the wave merges the 64 triples the same way (DPP-free shuffles) -- a single round of partial loads
-    // instead of a mean pass and an M2 pass
-    double n = 0.0, mu = 0.0, m2 = 0.0;
-    for (int t0 = 0; t0 < tiles; t0 += 64 * U) {
-        float pn[U], pm[U], pq[U];
+    // two passes over the tile partials (count, mean, M2) held in registers (one load round up to 512 tiles;
+    // beyond, the second pass reads them again): N and sum n m, then M2 = sum (q + n (m - mean)^2), all in
+    // fp64 with DPP wave totals (wave_total_d: no LDS round trips) -- the per-lane and per-wave Chan merges
+    // this replaced spent ~1.5 us in fp64 divisions and 36 ds_bpermute shuffles per wave
+    float pn[U], pm[U], pq[U];
+    auto load = [&](int t0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int t = min(t0 + u * 64 + lane, max(tiles - 1, 0));
             const float* p = a.part + ((long long)t * a.c + ch) * 3;
-            pn[u] = p[0];
-            pm[u] = p[1];
-            pq[u] = p[2];
+            const bool in = t0 + u * 64 + lane < tiles;
+            pn[u] = in ? p[0] : 0.f;
+            pm[u] = in ? p[1] : 0.f;
+            pq[u] = in ? p[2] : 0.f;
         }
+    };
+    double n = 0.0, sm = 0.0;
+    for (int t0 = 0; t0 < tiles; t0 += 64 * U) {
+        load(t0);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (t0 + u * 64 + lane < tiles && pn[u] > 0.f) {
-                const double nb = (double)pn[u], nn = n + nb, d = (double)pm[u] - mu;
-                mu += d * (nb / nn);
-                m2 += (double)pq[u] + d * d * (n * nb / nn);
-                n = nn;
-            }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(mu, o, 64), qb = __shfl_xor(m2, o, 64);
-        const double nn = n + nb;
-        if (nn > 0.0) {
-            // the same operation on both lanes of the pair: the operand with the smaller count (the lower
-            // lane on a tie) is "lo" on both, and the M2 terms are added commutatively
-            const double d = mb - mu;
-            const bool lo = n < nb || (n == nb && (lane & o) == 0);
-            const double mlo = lo ? mu : mb, mhi = lo ? mb : mu, nlo = lo ? n : nb;
-            const double mnew = mlo + (mhi - mlo) * ((nn - nlo) / nn);
-            m2 = m2 + qb + d * d * (n * nb / nn);
-            mu = mnew;
+        for (int u = 0; u < U; ++u) {
+            n += (double)pn[u];
+            sm = fma((double)pn[u], (double)pm[u], sm);
         }
-        n = nn;
     }
-    const double N = n, mean = mu, M2 = m2;
+    const double N = wave_total_d(n);
+    const double mean = N > 0.0 ? wave_total_d(sm) / N : 0.0;
+    double q = 0.0;
+    for (int t0 = 0; t0 < tiles; t0 += 64 * U) {
+        if (tiles > 64 * U) load(t0);  // one batch: still in registers
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double d = (double)pm[u] - mean;
+            q += (double)pq[u] + (double)pn[u] * d * d;
+        }
+    }
+    const double M2 = wave_total_d(q);
     if (lane == 0) {
         const double var = 1e-5 + (N > 0.0 ? M2 / N : 0.0);
         const float mf = (float)mean;
@@ -397,7 +394,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_fin(BnBwdArgs a) {
             }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = wave_sum_d(v[j]);
+    for (int j = 0; j < 4; ++j) v[j] = wave_total_d(v[j]);  // DPP tree, no LDS round trips
     if (lane == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) a.sums[ch * 4 + j] = (float)v[j];

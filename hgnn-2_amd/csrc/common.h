@@ -148,6 +148,26 @@ __device__ __forceinline__ float wave_total(float v) {
     v += dpp_moved<0x143, 0xC>(v);
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
+// wave_total's tree for a double (the two halves moved by the same DPP controls), uniform result
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_moved_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, ROWS, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_total_d(double v) {
+    v += dpp_moved_d<0xB1, 0xF>(v);
+    v += dpp_moved_d<0x4E, 0xF>(v);
+    v += dpp_moved_d<0x141, 0xF>(v);
+    v += dpp_moved_d<0x140, 0xF>(v);
+    v += dpp_moved_d<0x142, 0xA>(v);
+    v += dpp_moved_d<0x143, 0xC>(v);
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 // value of v in lane l (l wave-uniform)
 __device__ __forceinline__ float lane_value(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));

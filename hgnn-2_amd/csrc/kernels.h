@@ -213,10 +213,12 @@ __device__ __forceinline__ void repack_part(const RepackTable& t, int item, int 
         __syncthreads();
     }
     // WC as three bf16 planes (the split-bf16 forward GEMM's B operand), coalesced along k
+    // (32-bit element indices: 2d <= 1024 rows of at most a few thousand k; the 64-bit division per element
+    // these loops had was most of the launch's VALU)
     if (it.wc3) {
-        const long long n3 = (long long)c2 * it.ldc3;
-        for (long long e = (long long)yb * 256 + threadIdx.x; e < n3; e += (long long)t.y * 256) {
-            const int n = (int)(e / it.ldc3), k = (int)(e % it.ldc3);
+        const int n3 = c2 * it.ldc3;
+        for (int e = yb * 256 + (int)threadIdx.x; e < n3; e += t.y * 256) {
+            const int n = e / it.ldc3, k = e - n * it.ldc3;
             __bf16 a, b, c;
             split3(k < K ? W(n, k) : 0.f, a, b, c);
             it.wc3[e] = a;
@@ -225,13 +227,13 @@ __device__ __forceinline__ void repack_part(const RepackTable& t, int item, int 
         }
     }
     // WC (zero-padded to kp) and bc: coalesced along k
-    const long long nc = (long long)c2 * kp;
-    for (long long e = (long long)yb * 256 + threadIdx.x; e < nc + c2; e += (long long)t.y * 256) {
+    const int nc = c2 * kp;
+    for (int e = yb * 256 + (int)threadIdx.x; e < nc + c2; e += t.y * 256) {
         if (e < nc) {
-            const int n = (int)(e / kp), k = (int)(e % kp);
+            const int n = e / kp, k = e - n * kp;
             it.wc[e] = k < K ? W(n, k) : 0.f;
         } else {
-            const int n = (int)(e - nc);
+            const int n = e - nc;
             it.bc[n] = n < d ? it.bl[n] : it.br[n - d];
         }
     }
