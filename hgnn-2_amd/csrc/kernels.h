@@ -215,28 +215,55 @@ __device__ __forceinline__ void repack_part(const RepackTable& t, int item, int 
     // WC as three bf16 planes (the split-bf16 forward GEMM's B operand), coalesced along k
     // (32-bit element indices: 2d <= 1024 rows of at most a few thousand k; the 64-bit division per element
     // these loops had was most of the launch's VALU)
+    // 4 elements per thread per round, every load issued (clamped, unconditional) before the first store: one
+    // load per iteration made each block a chain of dependent round trips (~7 us per wave in the step)
+    auto Wc = [&](int n, int k) {  // W(n, k) with n, k clamped into range (a live address, masked after)
+        n = min(n, c2 - 1);
+        k = min(k, K - 1);
+        return n < d ? it.wl[(long long)n * K + k] : it.wr[(long long)(n - d) * K + k];
+    };
+    constexpr int RU = 4;
+    const int step = t.y * 256;
     if (it.wc3) {
         const int n3 = c2 * it.ldc3;
-        for (int e = yb * 256 + (int)threadIdx.x; e < n3; e += t.y * 256) {
-            const int n = e / it.ldc3, k = e - n * it.ldc3;
-            __bf16 a, b, c;
-            split3(k < K ? W(n, k) : 0.f, a, b, c);
-            it.wc3[e] = a;
-            it.wc3[n3 + e] = b;
-            it.wc3[2 * n3 + e] = c;
+        for (int e0 = yb * 256 + (int)threadIdx.x; e0 < n3; e0 += RU * step) {
+            float v[RU];
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                const int e = min(e0 + u * step, n3 - 1), n = e / it.ldc3, k = e - n * it.ldc3;
+                v[u] = Wc(n, k);
+            }
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                const int e = e0 + u * step;
+                if (e >= n3) break;
+                const int n = e / it.ldc3, k = e - n * it.ldc3;
+                __bf16 a, b, c;
+                split3(k < K ? v[u] : 0.f, a, b, c);
+                it.wc3[e] = a;
+                it.wc3[n3 + e] = b;
+                it.wc3[2 * n3 + e] = c;
+            }
         }
     }
     // WC (zero-padded to kp) and bc: coalesced along k
     const int nc = c2 * kp;
-    for (int e = yb * 256 + (int)threadIdx.x; e < nc + c2; e += t.y * 256) {
-        if (e < nc) {
+    for (int e0 = yb * 256 + (int)threadIdx.x; e0 < nc; e0 += RU * step) {
+        float v[RU];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            const int e = min(e0 + u * step, nc - 1), n = e / kp, k = e - n * kp;
+            v[u] = Wc(n, k);
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            const int e = e0 + u * step;
+            if (e >= nc) break;
             const int n = e / kp, k = e - n * kp;
-            it.wc[e] = k < K ? W(n, k) : 0.f;
-        } else {
-            const int n = e - nc;
-            it.bc[n] = n < d ? it.bl[n] : it.br[n - d];
+            it.wc[e] = k < K ? v[u] : 0.f;
         }
     }
+    for (int n = yb * 256 + (int)threadIdx.x; n < c2; n += step) it.bc[n] = n < d ? it.bl[n] : it.br[n - d];
 }
 
 // GEMM v3 (gemm3.hip): both operands k-contiguous ("NT"), used for the forward and dA.
