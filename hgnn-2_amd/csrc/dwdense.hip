@@ -135,6 +135,18 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
     float* Bmu = Rs + J * FC;       // [FC] BN mean, scale, and the BN of 0 (padded rows)
     float* Bsc = Bmu + FC;
     float* Bz = Bsc + FC;
+    // the input BN's per-channel constants do not depend on the graph: with one channel chunk (F <= FC),
+    // staged once per block instead of once per graph (one dependent round trip per graph saved)
+    const bool bn_once = a.pmean && F <= FC;
+    auto bn_consts = [&](int f0, int fc) {
+        for (int t = threadIdx.x; t < FC; t += 256) {
+            const int c = f0 + min(t, fc - 1);
+            Bmu[t] = a.pmean[c];
+            Bsc[t] = bn_scale(*a.pw, a.pstd[c]);
+            Bz[t] = bn_z(0.f, a.pmean[c], a.pstd[c], *a.pw, *a.pb);
+        }
+    };
+    if (bn_once) bn_consts(0, F);
     // graphs b, b + gridDim.x, ...: the grid may be smaller than the batch (launch_fc), so the kernel holds
     // fewer of the side stream's CUs beside the main stream's backward
     for (int b = blockIdx.x; b < a.bs; b += gridDim.x) {
@@ -169,13 +181,7 @@ __global__ void __launch_bounds__(256) k_dw_dense(DwDenseArgs a) {
                         r = fmaf(a.dout[b * a.dim_out + o], a.fcw[(long long)o * a.kfc + (j0 + j) * F + f0 + f], r);
                 Rs[t] = r;
             }
-        if (a.pmean)
-            for (int t = threadIdx.x; t < FC; t += 256) {
-                const int c = f0 + min(t, fc - 1);
-                Bmu[t] = a.pmean[c];
-                Bsc[t] = bn_scale(*a.pw, a.pstd[c]);
-                Bz[t] = bn_z(0.f, a.pmean[c], a.pstd[c], *a.pw, *a.pb);
-            }
+        if (a.pmean && !bn_once) bn_consts(f0, fc);
         __syncthreads();
         if (vec)
             dw_stage<FC, 4>(a, b, off, nb, npad, f0, fc, j0, J, Gs, Xs, GP, a.dout ? Rs : nullptr,
