@@ -175,6 +175,108 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
     }
 }
 
+// ---- dA on bf16 MFMA: Y[M][N] = A[M][K] . B[N][K]^T for a short reduction (K <= 32 NST: the 2d outputs of a
+// Conv1d pair, 128 at d = 64), A = dY (fp32, split at staging), B = WT's three bf16 planes (the repack's wt3).
+// k_gemm_bf3_fwd's tiles, LDS image and product order, but every stage's global loads are issued before the
+// first is used (clamped addresses, zeroed after, so no exec branch splits them): four stages of 12 MFMAs
+// per wave cannot hide a load round trip each, as the forward's one-stage-ahead prefetch asks.  Plain store.
+template <int NST>
+__global__ void __launch_bounds__(G_NT) k_gemm_bf3_da(const float* __restrict__ A, int lda,
+                                                      const __bf16* __restrict__ B, long long pb, int ldb,
+                                                      const int* __restrict__ m_valid, int m_cap, int N, int K,
+                                                      float* __restrict__ Y, int ldy, uint64_t* stamps) {
+    WaveStamp stamp(stamps);
+    __shared__ __attribute__((aligned(16))) char lds[2 * G_STAGE];
+    const int M = m_valid ? *m_valid : m_cap;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv >> 1, wn = wv & 1;
+    const int L = blockIdx.x + gridDim.x * blockIdx.y, jj = L >> 3;  // (k_gemm_bf3_fwd's XCD mapping)
+    const int by = jj % gridDim.y, bx = (L & 7) + 8 * (jj / gridDim.y);
+    const int m0 = bx * G_BM, n0 = by * G_BN;
+    if (m0 >= M) return;
+    const int arow = tid >> 2, ach = tid & 3, gm = m0 + arow;
+    const float* ap = A + (long long)min(gm, M - 1) * lda;
+    float4 ra[NST][2];
+    u32x4 rb[NST][3];
+#pragma unroll
+    for (int t = 0; t < NST; ++t) {
+        const int k = t * G_BK + 8 * ach;
+        ra[t][0] = *reinterpret_cast<const float4*>(ap + min(k, K - 4));
+        ra[t][1] = *reinterpret_cast<const float4*>(ap + min(k + 4, K - 4));
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int e = tid + G_NT * i, pl = e >> 8, row = (e & 255) >> 2, ch = e & 3;
+            const int kb = t * G_BK + 8 * ch, gn = min(n0 + row, N - 1);
+            rb[t][i] = *reinterpret_cast<const u32x4*>(B + pl * pb + (long long)gn * ldb + min(kb, ldb - 8));
+        }
+    }
+    auto store = [&](int buf, int t) {
+        char* st = lds + buf * G_STAGE;
+        const int k = t * G_BK + 8 * ach;
+        const bool v0 = gm < M && k < K, v1 = gm < M && k + 4 < K;
+        const float xv[8] = {v0 ? ra[t][0].x : 0.f, v0 ? ra[t][0].y : 0.f, v0 ? ra[t][0].z : 0.f,
+                             v0 ? ra[t][0].w : 0.f, v1 ? ra[t][1].x : 0.f, v1 ? ra[t][1].y : 0.f,
+                             v1 ? ra[t][1].z : 0.f, v1 ? ra[t][1].w : 0.f};
+        bf16x8 p0, p1, p2;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            __bf16 a, b, c;
+            split3(xv[e], a, b, c);
+            p0[e] = a;
+            p1[e] = b;
+            p2[e] = c;
+        }
+        *reinterpret_cast<bf16x8*>(st + swz(arow, ach)) = p0;
+        *reinterpret_cast<bf16x8*>(st + G_PLANE + swz(arow, ach)) = p1;
+        *reinterpret_cast<bf16x8*>(st + 2 * G_PLANE + swz(arow, ach)) = p2;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int e = tid + G_NT * i, pl = e >> 8, row = (e & 255) >> 2, ch = e & 3;
+            const bool ok = n0 + row < N && t * G_BK + 8 * ch < ldb;
+            const u32x4 z = {0u, 0u, 0u, 0u};
+            *reinterpret_cast<u32x4*>(st + (3 + pl) * G_PLANE + swz(row, ch)) = ok ? rb[t][i] : z;
+        }
+    };
+    f32x16 acc, tacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int r31 = lane & 31, h = lane >> 5;
+    const int frow = wm * 32 + r31, fcol = wn * 32 + r31;
+    store(0, 0);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < NST; ++t) {
+        const char* st = lds + (t & 1) * G_STAGE;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tacc[r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < G_BK / 16; ++s) {
+            const int ch = 2 * s + h;
+            bf16x8 a[3], b[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                a[p] = *reinterpret_cast<const bf16x8*>(st + p * G_PLANE + swz(frow, ch));
+                b[p] = *reinterpret_cast<const bf16x8*>(st + (3 + p) * G_PLANE + swz(fcol, ch));
+            }
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], tacc, 0, 0, 0);
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], tacc, 0, 0, 0);
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], tacc, 0, 0, 0);
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], tacc, 0, 0, 0);
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], tacc, 0, 0, 0);
+            tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], tacc, 0, 0, 0);
+        }
+        acc += tacc;
+        if (t + 1 < NST) store((t + 1) & 1, t + 1);
+        __syncthreads();
+    }
+    const int gn = n0 + wn * 32 + r31;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M && gn < N) Y[(long long)m * ldy + gn] = acc[r];
+    }
+}
+
 // ---- dW on bf16 MFMA: slabs[z][m][n] = sum_{r in chunk z} A[r][m] B[r][n] (k_gemm3_tn's contract: A = dY
 // [R][lda], m < M = 2d; B = the saved aggregate [R][ldb], n < N = kp; chunk z of dw3_kc(R, nz) rows), each
 // operand split into three bf16 planes at staging and the six products with i + j <= 4 summed on
@@ -314,6 +416,26 @@ int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const
     const dim3 g(ceil_div(o, 128), ceil_div(k, 128), nz);
     HGNN_KLAUNCH(k_gemm_bf3_tn<2>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz,
                  xcd && nz % 8 == 0 ? 1 : 0, clock_stamps((long long)g.x * g.y * g.z * (D_NT / 64)));
+    HGNN_LAUNCH_CHECK();
+    return 0;
+}
+
+int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
+                       int ldb, int n, float* y, int ldy, hipStream_t s) {
+    if (m_cap <= 0 || n <= 0) return 0;
+    if (k < 4 || k > 4 * G_BK || lda % 4 || k % 4 || ldb % 8 || pb % 8 || k > lda || bf3_ld(k) > ldb ||
+        (reinterpret_cast<uintptr_t>(a) & 15) || (reinterpret_cast<uintptr_t>(b) & 15))
+        return HGNN_ERR_UNSUPPORTED;
+    if ((long long)m_cap * lda * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    const int gx = ceil_div(ceil_div(m_cap, G_BM), 8) * 8;
+    const dim3 g(gx, ceil_div(n, G_BN));
+    uint64_t* st = clock_stamps((long long)g.x * g.y * (G_NT / 64));
+    switch (ceil_div(k, G_BK)) {
+        case 1: HGNN_KLAUNCH(k_gemm_bf3_da<1>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
+        case 2: HGNN_KLAUNCH(k_gemm_bf3_da<2>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
+        case 3: HGNN_KLAUNCH(k_gemm_bf3_da<3>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
+        default: HGNN_KLAUNCH(k_gemm_bf3_da<4>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
+    }
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -151,6 +151,10 @@ __host__ __device__ inline int bf3_ld(int k) { return (k + 15) / 16 * 16; }  // 
 // The forward Conv1d-pair GEMM on bf16 MFMA (three-way split, fp32 accuracy): Y = A . B^T + bias, ReLU
 // from column relu_from, BN partials per 64-row tile (as launch_gemm3_fwd); A fp32 [M][lda] (k < kp),
 // B three bf16 planes b + p pb [N][ldb] (ldb >= bf3_ld(k), zero beyond k)
+// The dA GEMM on bf16 MFMA (three-way split): Y[M][n] = A[M][k] . B^T for k <= 128 (A = dY fp32 [M][lda],
+// B = WT's three bf16 planes b + p pb [n][ldb], ldb >= bf3_ld(k), zero beyond k); HGNN_ERR_UNSUPPORTED otherwise
+int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
+                       int ldb, int n, float* y, int ldy, hipStream_t s);
 int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
                         int ldb, int n, const float* bias, int relu_from, float* y, int ldy, float* bn_part,
                         hipStream_t s);
@@ -169,6 +173,8 @@ struct RepackItem {
     int k, kp, ldt;
     __bf16* wc3;       // optional out: Wcat as three bf16 planes [3][2d][ldc3] (split3), zero beyond K
     int ldc3;
+    __bf16* wt3;       // optional out: WT as three bf16 planes [3][K][ldt3] (split3; the split-bf16 dA GEMM's B),
+    int ldt3;          // zero beyond 2d
 };
 constexpr int REPACK_MAX = 24;
 struct RepackTable {
@@ -209,6 +215,14 @@ __device__ __forceinline__ void repack_part(const RepackTable& t, int item, int 
         for (int rr = ty; rr < 32; rr += 8) {
             const int k = k0 + rr, n = n0 + tx;
             if (k < K && n < ldt) it.wt[(long long)k * ldt + n] = tile[tx][rr];
+            if (it.wt3 && k < K && n < it.ldt3) {  // (ldt3 = bf3_ld(ldt) <= the tiles' 32-column cover)
+                const long long e = (long long)k * it.ldt3 + n, pl = (long long)K * it.ldt3;
+                __bf16 a, b, c;
+                split3(tile[tx][rr], a, b, c);
+                it.wt3[e] = a;
+                it.wt3[pl + e] = b;
+                it.wt3[2 * pl + e] = c;
+            }
         }
         __syncthreads();
     }

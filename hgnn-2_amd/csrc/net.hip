@@ -41,6 +41,7 @@ struct Half {
     size_t a = 0, part = 0, mean = 0, stdv = 0;
     size_t wt = 0, wc = 0, bc = 0;  // repacked Conv1d-pair weights (repack.hip)
     size_t wc3 = 0;                 // Wcat as three bf16 planes [3][2d][bf3_ld(kp)] (split-bf16 forward GEMM)
+    size_t wt3 = 0;                 // WT as three bf16 planes [3][k][bf3_ld(c2p)] (split-bf16 dA GEMM)
 };
 
 // Buffer ring of the backward: a dY / bias-partial buffer (and, for the node halves whose dense dW the side
@@ -245,6 +246,7 @@ Program build_program(const hgnn_net_config* c) {
         h.wc = B.take((size_t)P.c2 * h.kp * sizeof(float));
         h.bc = B.take((size_t)P.c2 * sizeof(float));
         h.wc3 = B.take((size_t)3 * P.c2 * bf3_ld(h.kp) * 2);
+        h.wt3 = B.take((size_t)3 * h.k * bf3_ld(P.c2p) * 2);
         max_da = std::max(max_da, (size_t)cap * h.kp);
         max_slab = std::max(max_slab, dw3_slab_floats(cap, P.c2, h.k));
         max_cap = std::max(max_cap, cap);
@@ -507,6 +509,11 @@ static bool fwd_bf3(const Program& P) {
     static const bool on = env_flag("HGNN_FWD_BF3", true);
     return on && P.c2 % 64 == 0;
 }
+// the dA GEMM on the split-bf16 kernel (k_gemm_bf3_fwd with a plain-store epilogue, B = WT's planes)
+static bool da_bf3(const Program& P) {
+    static const bool on = env_flag("HGNN_DA_BF3", true);
+    return on && P.c2p <= 128;
+}
 
 int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_csr_batch* csr,
                 const float* const* prm, float* const* run, void* ws, float* out, hipStream_t s, Timer* tm) {
@@ -535,6 +542,10 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
             if (fwd_bf3(P)) {
                 it.wc3 = at<__bf16>(ws, h.wc3);
                 it.ldc3 = bf3_ld(h.kp);
+            }
+            if (da_bf3(P)) {
+                it.wt3 = at<__bf16>(ws, h.wt3);
+                it.ldt3 = bf3_ld(P.c2p);
             }
             if (rt.n == REPACK_MAX || hi + 1 == P.halves.size()) {
                 tables.push_back(rt);
@@ -915,7 +926,12 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         // dW + reduce is the step's tail there, nothing on the main stream follows to overlap it
         const bool early = side && hi == 0 && !ndw && bwd_tail;
         if (early) TRY(fork_dw(h, cap, tot, dyb, dbp, false, nullptr));
-        TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2p, tot, cap, P.c2p, at<float>(ws, h.wt), P.c2p, h.k, da, h.kp, s));
+        if (da_bf3(P))
+            TL(HGNN_K_GEMM_DA, launch_gemm_bf3_da(dyb, P.c2p, tot, cap, P.c2p, at<__bf16>(ws, h.wt3),
+                                                  (long long)h.k * bf3_ld(P.c2p), bf3_ld(P.c2p), h.k, da, h.kp, s));
+        else
+            TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2p, tot, cap, P.c2p, at<float>(ws, h.wt), P.c2p, h.k, da, h.kp,
+                                               s));
         // dW starts once dA is done: two MFMA GEMMs side by side only slow each other,
         // dW beside the latency-bound dense-dW / aggregation-backward kernels does not
         if (!early) TRY(fork_dw(h, cap, tot, dyb, dbp, ndw, da));
