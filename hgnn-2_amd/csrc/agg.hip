@@ -256,6 +256,158 @@ __global__ void __launch_bounds__(AGG_NT) k_agg_fwd(AggFwdArgs a) {
     }
 }
 
+// k_agg_fwd with RPW rows per wave (rows RPW w .. RPW w + RPW - 1): the row infos of all of them, then the first entry
+// chunk of all of them, are fetched before the first row's gathers, so RPW rows cost RPW + 2 dependent round
+// trips instead of 3 RPW.
+template <int JT, int CG, int CP, bool V, int RPW>
+__global__ void __launch_bounds__(AGG_NT) k_agg_fwd_rpw(AggFwdArgs a) {
+    WaveStamp stamp(a.stamps);
+    const int r0 = __builtin_amdgcn_readfirstlane((blockIdx.x * AGG_WV + (threadIdx.x >> 6)) * RPW);
+    const int lane = threadIdx.x & 63;
+    const int total = *a.total_rows;
+    if (r0 >= total) return;
+    constexpr int CGx = CG > 0 ? CG : 1, CPx = CP > 0 ? CP : 1, MX = JT > 3 ? JT - 3 : 1;
+    // The G and P chains (row info -> entry chunk -> feature gathers) run interleaved: both
+    // row infos, then both entry chunks, then the gathers of both lists in one batch, so a
+    // row costs ~3 dependent memory round trips instead of 6.
+    RowInfo rgk[RPW], rpk[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+        const int r = min(r0 + k, total - 1);  // (rows past the total: a live row, never stored)
+        rgk[k] = RowInfo{0, 0};
+        rpk[k] = RowInfo{0, 0};
+        if constexpr (CG > 0) rgk[k] = row_info(a.g.rows, r);
+        if constexpr (CP > 0) rpk[k] = row_info(a.p.rows, r);
+    }
+    LaneBn<CGx> bng;
+    LaneBn<CPx> bnp;
+    if constexpr (CG > 0) bng.init(a.gbn, a.cg, lane);
+    if constexpr (CP > 0) bnp.init(a.pbn, a.cp, lane);
+    const int stride = a.g.stride;
+    // the first 64-entry chunk of every row's lists
+    float4 mgk[RPW], mpk[RPW];
+    float mxk[RPW][MX];
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+        mgk[k] = mpk[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int ng = min(64, rgk[k].count), np = min(64, rpk[k].count);
+        if constexpr (CG > 0) {
+            mgk[k] = lane_entry(a.g.entries, stride, rgk[k].start, ng, lane);
+            if constexpr (JT > 3) {
+#pragma unroll
+                for (int j = 3; j < JT; ++j)
+                    mxk[k][j - 3] = lane < ng ? a.g.entries[(long long)(rgk[k].start + lane) * stride + 1 + j] : 0.f;
+            }
+        }
+        if constexpr (CP > 0) mpk[k] = lane_entry(a.p.entries, 4, rpk[k].start, np, lane);
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+    const int r = r0 + k;
+    if (r >= total) break;
+    const RowInfo rg = rgk[k], rp = rpk[k];
+    float* o = a.out + (long long)r * a.ldo;
+    float acc[JT][CGx], am[CPx], ad[CPx];
+#pragma unroll
+    for (int j = 0; j < JT; ++j)
+#pragma unroll
+        for (int i = 0; i < CGx; ++i) acc[j][i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPx; ++i) am[i] = ad[i] = 0.f;
+    const int nmax = max(rg.count, rp.count);
+    for (int e0 = 0; e0 < nmax; e0 += 64) {
+        const int ng = min(64, max(0, rg.count - e0)), np = min(64, max(0, rp.count - e0));
+        float4 mg = mgk[k], mp = mpk[k];
+        float mx[MX];
+#pragma unroll
+        for (int j = 0; j < MX; ++j) mx[j] = mxk[k][j];
+        if (e0 > 0) {
+            if constexpr (CG > 0) {
+                // JT <= 3: one float4 per entry; larger JT reads the extra coefficients below
+                mg = lane_entry(a.g.entries, stride, rg.start + e0, ng, lane);
+                if constexpr (JT > 3) {
+#pragma unroll
+                    for (int j = 3; j < JT; ++j)
+                        mx[j - 3] = lane < ng ? a.g.entries[(long long)(rg.start + e0 + lane) * stride + 1 + j] : 0.f;
+                }
+            }
+            if constexpr (CP > 0) mp = lane_entry(a.p.entries, 4, rp.start + e0, np, lane);
+        }
+        const int nn = max(ng, np);
+        for (int e = 0; e < nn; e += AGG_U) {
+            float xg[AGG_U][CGx], v[AGG_U][JT], xp[AGG_U][CPx], vm[AGG_U], vd[AGG_U];
+            if constexpr (CG > 0) {
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u) {
+                    // dead slots re-read the last live row with zero coefficients (no branch)
+                    const int eu = max(0, min(e + u, ng - 1));
+                    const int col = __builtin_amdgcn_readlane(__float_as_int(mg.x), eu);
+                    const bool live = e + u < ng;
+                    v[u][0] = live ? bcast(mg.y, eu) : 0.f;
+                    if constexpr (JT > 1) v[u][1] = live ? bcast(mg.z, eu) : 0.f;
+                    if constexpr (JT > 2) v[u][2] = live ? bcast(mg.w, eu) : 0.f;
+#pragma unroll
+                    for (int j = 3; j < JT; ++j) v[u][j] = live ? bcast(mx[j - 3], eu) : 0.f;
+                    if (ng > 0) load_row<CG, V>(a.xg + (long long)col * a.cg, a.cg, lane, xg[u]);
+                    else
+#pragma unroll
+                        for (int i = 0; i < CG; ++i) xg[u][i] = 0.f;
+                }
+            }
+            if constexpr (CP > 0) {
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u) {
+                    const int eu = max(0, min(e + u, np - 1));
+                    const int col = __builtin_amdgcn_readlane(__float_as_int(mp.x), eu);
+                    const bool live = e + u < np;
+                    vm[u] = live ? bcast(mp.y, eu) : 0.f;
+                    vd[u] = live ? bcast(mp.z, eu) : 0.f;
+                    if (np > 0) load_row<CP, V>(a.xp + (long long)col * a.cp, a.cp, lane, xp[u]);
+                    else
+#pragma unroll
+                        for (int i = 0; i < CP; ++i) xp[u][i] = 0.f;
+                }
+            }
+            if constexpr (CG > 0) {
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u) bng.apply(xg[u]);
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u)
+#pragma unroll
+                    for (int j = 0; j < JT; ++j)
+#pragma unroll
+                        for (int i = 0; i < CG; ++i) acc[j][i] = fmaf(v[u][j], xg[u][i], acc[j][i]);
+            }
+            if constexpr (CP > 0) {
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u) bnp.apply(xp[u]);
+#pragma unroll
+                for (int u = 0; u < AGG_U; ++u)
+#pragma unroll
+                    for (int i = 0; i < CP; ++i) {
+                        am[i] = fmaf(vm[u], xp[u][i], am[i]);
+                        ad[i] = fmaf(vd[u], xp[u][i], ad[i]);
+                    }
+            }
+        }
+    }
+    if constexpr (CG > 0) {
+#pragma unroll
+        for (int j = 0; j < JT; ++j) store_row<CG, V>(o + j * a.cg, a.cg, lane, acc[j]);
+    }
+    if constexpr (CP > 0) {
+        const int base = JT * a.cg;
+        store_row<CP, V>(o + base, a.cp, lane, am);
+        store_row<CP, V>(o + base + a.cp, a.cp, lane, ad);
+    }
+    // zero the row padding [K, ldo): the GEMMs run over the padded width
+    if (a.pad_from >= 0) {
+        const int kk = a.pad_from > 0 ? a.pad_from : JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
+        if (lane < a.ldo - kk) o[kk + lane] = 0.f;
+    }
+    }
+}
+
 static int cpl_of(int c) {
     if (c <= 0) return 0;
     if (c <= 64) return 1;
@@ -268,11 +420,30 @@ static int cpl_of(int c) {
 template <int JT, int CG, int CP>
 static void agg_fwd_v(const AggFwdArgs& a0, dim3 g, hipStream_t s) {
     AggFwdArgs a = a0;
-    a.stamps = clock_stamps((long long)g.x * AGG_WV);
     const int kk = JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
     const bool v = (CG == 0 || vec_ok(CG, a.cg, a.xg, {})) && (CP == 0 || vec_ok(CP, a.cp, a.xp, {})) &&
                    (CG == 0 || vec_ok(CG, a.cg, a.out, {a.ldo, (long long)kk})) &&
                    (CP == 0 || vec_ok(CP, a.cp, a.out, {a.ldo, (long long)JT * a.cg, (long long)a.cp}));
+    static const int rpw = [] {  // rows per wave: 1 (k_agg_fwd), 2 or 4 (k_agg_fwd_rpw; J_tot = 3 only)
+        const char* e = getenv("HGNN_AGG_RPW");
+        const int r = e ? atoi(e) : 2;
+        return r == 4 ? 4 : (r == 1 ? 1 : 2);
+    }();
+    if constexpr (JT == 3) {
+        if (rpw > 1) {
+            const dim3 g2(ceil_div(a.cap_rows, rpw * AGG_WV));
+            a.stamps = clock_stamps((long long)g2.x * AGG_WV);
+            if (rpw == 4) {
+                if (v) HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, true, 4>), g2, dim3(AGG_NT), 0, s, a);
+                else HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, false, 4>), g2, dim3(AGG_NT), 0, s, a);
+            } else {
+                if (v) HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, true, 2>), g2, dim3(AGG_NT), 0, s, a);
+                else HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, false, 2>), g2, dim3(AGG_NT), 0, s, a);
+            }
+            return;
+        }
+    }
+    a.stamps = clock_stamps((long long)g.x * AGG_WV);
     if (v) HGNN_KLAUNCH((k_agg_fwd<JT, CG, CP, true>), g, dim3(AGG_NT), 0, s, a);
     else HGNN_KLAUNCH((k_agg_fwd<JT, CG, CP, false>), g, dim3(AGG_NT), 0, s, a);
 }
