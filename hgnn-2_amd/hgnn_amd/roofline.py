@@ -14,7 +14,7 @@ from .net import expected_k
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_FP32_MFMA_TFS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak
 PEAK_BF16_MFMA_TFS = 16 * PEAK_FP32_MFMA_TFS  # dense bf16 MFMA: 16x the fp32 rate per clock (MI355X_MICROARCH.md)
-# the split-bf16 GEMMs (k_gemm_bf3_fwd, k_gemm_bf3_tn) run six bf16 products per fp32 product: their fp32
+# the split-bf16 GEMMs (k_gemm_bf3_fwd, k_gemm_bf3_da, k_gemm_bf3_tn) run six bf16 products per fp32 product: their fp32
 # algorithmic FLOPs are priced against a sixth of the bf16 peak
 PEAK_SPLIT_BF16_TFS = PEAK_BF16_MFMA_TFS / 6
 
@@ -147,7 +147,7 @@ CLASS_KERNELS = {
     K_READOUT: ("k_readout",),  # incl. k_readout_agg_bwd (net.hip times it in this class)
     K_BN_BWD: ("k_bn_bwd",),
     K_GEMM_DW: ("k_gemm3_tn", "k_gemm_dw", "k_gemm_bf3_tn"),
-    K_GEMM_DA: ("k_gemm3<", "k_gemm_da", "k_gemm5<"),
+    K_GEMM_DA: ("k_gemm3<", "k_gemm_da", "k_gemm5<", "k_gemm_bf3_da"),
     K_AGG_BWD: ("k_agg_bwd",),
     K_DW_DENSE: ("k_dw_dense",),
     K_DW_REDUCE: ("k_dw_reduce",),
@@ -167,11 +167,13 @@ def _in_class(kcls, name):
 
 
 def split_bf16(kcls, d):
-    """Whether the executor runs class kcls on the split-bf16 GEMMs at width d (net.hip fwd_bf3, gemm3.hip
-    launch_gemm3_dw; their switches HGNN_FWD_BF3 / HGNN_DW_BF3)."""
+    """Whether the executor runs class kcls on the split-bf16 GEMMs at width d (net.hip fwd_bf3 / da_bf3,
+    gemm3.hip launch_gemm3_dw; their switches HGNN_FWD_BF3 / HGNN_DA_BF3 / HGNN_DW_BF3)."""
     import os
     if kcls == K_GEMM_FWD:
         return (2 * d) % 64 == 0 and os.environ.get("HGNN_FWD_BF3", "1") != "0"
+    if kcls == K_GEMM_DA:
+        return (2 * d + 3) // 4 * 4 <= 128 and os.environ.get("HGNN_DA_BF3", "1") != "0"
     if kcls == K_GEMM_DW:
         return os.environ.get("HGNN_DW_BF3", "1") != "0"
     return False
