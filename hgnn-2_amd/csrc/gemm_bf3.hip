@@ -405,6 +405,126 @@ __global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn(const float* __restrict__ 
     }
 }
 
+// k_gemm_bf3_tn with a ring the compiler keeps: the loads unconditional (clamped row and column, the
+// out-of-range values zeroed at the split), no branch inside the unrolled stage group (the stages past the
+// chunk's last run on zeroed planes and add nothing), and each group of loads pinned where it is issued --
+// the conditional loads and the in-loop breaks of k_gemm_bf3_tn left a vmcnt(0) before every stage, so its
+// ring never had a load in flight across a stage.
+template <int PD>
+__global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn_ring(const float* __restrict__ A, int lda,
+                                                           const float* __restrict__ B, int ldb,
+                                                           float* __restrict__ slabs, int M, int N,
+                                                           const int* __restrict__ r_valid, int nz, int xcd_remap,
+                                                           uint64_t* stamps) {
+    WaveStamp stamp(stamps);
+    static_assert(PD >= 2, "a ring of at least two stages");
+    __shared__ __attribute__((aligned(16))) char lds[2 * D_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv >> 1, wn = wv & 1;
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (xcd_remap) {
+        const int T = gridDim.x * gridDim.y;
+        const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int j = L >> 3, t = j % T;
+        bz = (L & 7) + 8 * (j / T);
+        bx = t % gridDim.x;
+        by = t / gridDim.x;
+    }
+    const int m0 = bx * 128, n0 = by * 128;
+    const int R = *r_valid;
+    const int kchunk = dw3_kc(R, nz);
+    const int kbeg = bz * kchunk, kend = min(R, kbeg + kchunk);
+    if (kbeg >= kend) return;
+    const int col = tid & 127, rq = tid >> 7;
+    const bool am = m0 + col < M, bn = n0 + col < N;
+    const float* ap = A + min(m0 + col, M - 1);
+    const float* bp = B + min(n0 + col, N - 1);
+    float ra[PD][4], rb[PD][4];
+    auto load = [&](float (&xa)[4], float (&xb)[4], int k0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const long long gk = min(k0 + 4 * rq + i, kend - 1);
+            xa[i] = ap[gk * lda];
+            xb[i] = bp[gk * ldb];
+        }
+    };
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    auto store = [&](const float (&xa)[4], const float (&xb)[4], int buf, int k0) {
+        char* st = lds + buf * D_STAGE;
+        const int off = dswz(col, rq >> 1) + (rq & 1) * 8;
+        bf16x4 p[3], q[3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool in = k0 + 4 * rq + i < kend;
+            __bf16 x, y, z;
+            split3(in && am ? xa[i] : 0.f, x, y, z);
+            p[0][i] = x;
+            p[1][i] = y;
+            p[2][i] = z;
+            split3(in && bn ? xb[i] : 0.f, x, y, z);
+            q[0][i] = x;
+            q[1][i] = y;
+            q[2][i] = z;
+        }
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+            *reinterpret_cast<bf16x4*>(st + pl * D_PLANE + off) = p[pl];
+            *reinterpret_cast<bf16x4*>(st + (3 + pl) * D_PLANE + off) = q[pl];
+        }
+    };
+    f32x16 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const int nt = (kend - kbeg + D_BK - 1) / D_BK;
+    const int r31 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int u = 0; u < PD; ++u) load(ra[u], rb[u], kbeg + u * D_BK);
+    __builtin_amdgcn_sched_barrier(0);
+    store(ra[0], rb[0], 0, kbeg);
+    __syncthreads();
+    for (int t0 = 0; t0 < nt; t0 += PD) {
+#pragma unroll
+        for (int u = 0; u < PD; ++u) {
+            const int t = t0 + u;
+            const char* st = lds + (t & 1) * D_STAGE;
+            bf16x8 a[3], b[2][3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                a[pl] = *reinterpret_cast<const bf16x8*>(st + pl * D_PLANE + dswz(wm * 32 + r31, h));
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    b[j][pl] = *reinterpret_cast<const bf16x8*>(st + (3 + pl) * D_PLANE + dswz(wn * 64 + j * 32 + r31, h));
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[j][1], acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][2], acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[j][0], acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][1], acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[j][0], acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][0], acc[j], 0, 0, 0);
+            }
+            const int un = (u + 1) % PD;  // the slot holding stage t + 1
+            store(ra[un], rb[un], (t + 1) & 1, kbeg + (t + 1) * D_BK);
+            load(ra[u], rb[u], kbeg + (t + PD) * D_BK);  // slot u (stage t, staged) takes stage t + PD
+            __builtin_amdgcn_sched_barrier(0);
+            __syncthreads();
+        }
+    }
+    float* out = slabs + (long long)bz * M * N;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int gn = n0 + wn * 64 + j * 32 + r31;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int gm = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (gm < M && gn < N) out[(long long)gm * N + gn] = acc[j][r];
+        }
+    }
+}
+
 }  // namespace
 
 int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o,
@@ -414,8 +534,19 @@ int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const
     if ((long long)r_cap * (lda > lddy ? lda : lddy) >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     // ring depth 2: step times 1.300-1.302 ms against 1.306-1.314 (4) and 1.313-1.323 (6), alternating runs
     const dim3 g(ceil_div(o, 128), ceil_div(k, 128), nz);
-    HGNN_KLAUNCH(k_gemm_bf3_tn<2>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz,
-                 xcd && nz % 8 == 0 ? 1 : 0, clock_stamps((long long)g.x * g.y * g.z * (D_NT / 64)));
+    static const int ring = [] {  // HGNN_DW_RING: 0 = k_gemm_bf3_tn<2>, 2..4 = k_gemm_bf3_tn_ring<depth>
+        const char* e = getenv("HGNN_DW_RING");
+        const int v = e ? atoi(e) : 4;
+        return v == 0 ? 0 : (v < 2 ? 2 : (v > 4 ? 4 : v));
+    }();
+    uint64_t* st = clock_stamps((long long)g.x * g.y * g.z * (D_NT / 64));
+    const int xr = xcd && nz % 8 == 0 ? 1 : 0;
+    switch (ring) {
+        case 0: HGNN_KLAUNCH(k_gemm_bf3_tn<2>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr, st); break;
+        case 2: HGNN_KLAUNCH(k_gemm_bf3_tn_ring<2>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr, st); break;
+        case 3: HGNN_KLAUNCH(k_gemm_bf3_tn_ring<3>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr, st); break;
+        default: HGNN_KLAUNCH(k_gemm_bf3_tn_ring<4>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr, st); break;
+    }
     HGNN_LAUNCH_CHECK();
     return 0;
 }
