@@ -137,10 +137,11 @@ int launch_agg_bwd_pair(const AggBwdArgs& ga, const AggBwdArgs& pa, hipStream_t 
 // ---------------------------------------------------------------- GEMM (gemm3.hip, gemm_bf3.hip, repack.hip)
 // fp32 x as three bf16 parts x1 + x2 + x3 (residual below 2^-26 |x|): the operand form of the split-bf16
 // GEMM (gemm_bf3.hip).  Non-finite inputs: x = +-Inf (or |x| above the bf16 maximum, which rounds x1 to Inf)
-// gives x2 = Inf - Inf = NaN, so a split-bf16 GEMM (the forward at 2d % 64 == 0, every dW GEMM) returns NaN
-// where an fp32 GEMM returns Inf; finite inputs below the bf16 maximum (~3.4e38) are unaffected.  Not
-// guarded in the split: a select per element costs ~3 VALU in the staging loop these GEMMs are bound by
-// (round 5: 32 v_cmp + 110 v_cndmask per 24 MFMAs); HGNN_FWD_BF3=0 / HGNN_DW_BF3=0 select the fp32 GEMMs.
+// gives x2 = Inf - Inf = NaN, so a split-bf16 GEMM (the forward at 2d % 64 == 0, the dA at 2d <= 128, every
+// dW GEMM) returns NaN where an fp32 GEMM returns Inf; finite inputs below the bf16 maximum (~3.4e38) are
+// unaffected.  Not guarded in the split: a select per element costs ~3 VALU in the staging loop these GEMMs
+// are bound by (round 5: 32 v_cmp + 110 v_cndmask per 24 MFMAs); HGNN_FWD_BF3=0 / HGNN_DA_BF3=0 /
+// HGNN_DW_BF3=0 select the fp32 GEMMs.
 __device__ __forceinline__ void split3(float x, __bf16& a, __bf16& b, __bf16& c) {
     a = (__bf16)x;
     const float r = x - (float)a;
