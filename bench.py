@@ -46,8 +46,14 @@ def parse():
     ap.add_argument("--d", "--dim", dest="d", type=int, default=64)
     ap.add_argument("--layers", type=int, default=5)
     ap.add_argument("--order", type=int, default=2)
-    ap.add_argument("--settle-s", type=float, default=1.0,
-                    help="untimed steps for this many seconds before the warmup steps (clock ramp)")
+    ap.add_argument("--settle-s", type=float, default=1.5,
+                    help="untimed steps for this many seconds (after 40 warm-up / sampling steps) before the "
+                         "warmup steps (clock ramp)")
+    ap.add_argument("--force-dp", type=int, default=0,
+                    help="at --gpus 1: form an RCCL (nccl) process group of world size 1 and run the per-layer "
+                         "bucketed all-reduce anyway (exercises the N > 1 communication path on one GPU)")
+    ap.add_argument("--attribution", type=int, default=1,
+                    help="host-enqueue and GPU-busy time per step, each over a region of its own")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-bs", type=int, default=128,
                     help="graphs per step of the CPU baseline's timed protocol (bounded sample)")
@@ -203,6 +209,7 @@ def main():
     backend = os.environ.get("HGNN_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
+    force_dp = world == 1 and bool(args.force_dp)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -210,6 +217,10 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    elif force_dp:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                **({"device_id": torch.device("cuda", local)} if backend == "nccl" else {}))
     dev = torch.device("cuda", local)
 
     from hgnn_amd import roofline as RF
@@ -227,7 +238,8 @@ def main():
     from hgnn_amd.dp import GradAllReduce, LayerBucketAllReduce
     # N > 1: per-layer gradient buckets reduced on a communication stream while the executor's
     # backward is still running (its per-layer events), BN running statistics averaged
-    allreduce = LayerBucketAllReduce(model) if world > 1 and not args.graph else GradAllReduce(params)
+    allreduce = (LayerBucketAllReduce(model, force=force_dp) if (world > 1 or force_dp) and not args.graph
+                 else GradAllReduce(params))
     last_out = [None]
 
     def compute():
@@ -250,26 +262,33 @@ def main():
         allreduce()  # no-op at N = 1
         return loss
 
-    # settle: untimed steps for --settle-s seconds before the W warmup steps, so a fresh box's
-    # clocks have ramped before anything is timed (the first run on a box was up to 30 % slow
-    # in A/B runs with only the W steps ahead of it)
+    # warm-up, then settle by wall time (review r05 #1): WARM untimed steps first (one-time costs: module
+    # loads, the caching allocator, the executor's program cache -- on a fresh box the first steps take
+    # ~25 ms each, so a step time sampled over them sized the settle far too short), then the step time
+    # sampled over SAMPLE more steps sizes a count of untimed steps covering --settle-s seconds, so a fresh
+    # box's clocks have ramped before anything is timed.  A step count, not a deadline: every rank must
+    # run the same number of steps (their all-reduces pair up), so the count is maxed over the ranks.
+    WARM, SAMPLE = 20, 20
     settle_steps = 0
+    settle_sample_ms = None
     if args.settle_s > 0:
-        # a step count, not a deadline: every rank must run the same number of steps (their
-        # all-reduces pair up), so the count from 10 timed steps is maxed over the ranks
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(10):
+        for _ in range(WARM):
             step()
         torch.cuda.synchronize()
-        n = int(args.settle_s / max((time.perf_counter() - t0) / 10, 1e-5))
+        t0 = time.perf_counter()
+        for _ in range(SAMPLE):
+            step()
+        torch.cuda.synchronize()
+        per = max((time.perf_counter() - t0) / SAMPLE, 1e-5)
+        settle_sample_ms = round(per * 1e3, 4)
+        n = int(args.settle_s / per) + 1
         if world > 1:
             t = torch.tensor([n], dtype=torch.int64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             n = int(t.item())
         for _ in range(n):
             step()
-        settle_steps = 10 + n
+        settle_steps = WARM + SAMPLE + n
         torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
@@ -350,6 +369,7 @@ def main():
         dist.all_reduce(e)
         rank_ms = [round(float(v) * 1e3 / args.steps, 4) for v in e.cpu()]
         elapsed = float(e.max().item())
+    if world > 1 or force_dp:
         if isinstance(allreduce, LayerBucketAllReduce):
             # the per-step gradient all-reduce (HIP events on the communication stream) over a
             # separate region of the same steps, so `value` carries no event records
@@ -364,6 +384,55 @@ def main():
                 dist.all_reduce(c, op=dist.ReduceOp.MAX)
                 comm["allreduce_span_ms_max_rank"] = round(float(c[0]), 4)
                 comm["allreduce_exposed_ms_max_rank"] = round(float(c[1]), 4)
+
+    # attribution (review r05 #1), each over a region of its own after the `value` region: the host's
+    # enqueue time per step (perf_counter around the steps, no synchronisation inside: the executor never
+    # waits on the GPU, so this is the host's cost while the GPU still runs), and the GPU's busy time per
+    # step: the union of every stamped executor launch span (all streams; in-kernel s_memrealtime stamps,
+    # nothing added to the streams; torch's loss kernels and memsets are not stamped and count as idle)
+    attribution = None
+    if args.attribution and graph is None:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        th = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        tw = time.perf_counter() - t0
+        nb = 5
+        tmb = KernelTimer(400 * nb, range(RF.N_CLASSES), mode=TIMER_STAMPS, stamp_words=(1 << 22) * nb)
+        with tmb:
+            for _ in range(nb):
+                step()
+            torch.cuda.synchronize()
+        lau = tmb.launches(400 * nb)
+        tmb.close()
+        busy, span = [], []
+        per_step = len(lau) // nb if lau else 0
+        for i in range(nb if per_step else 0):
+            iv = sorted((e0, e1) for _, e0, e1, _ in lau[i * per_step:(i + 1) * per_step])
+            tot, cs, ce = 0.0, iv[0][0], iv[0][1]
+            for e0, e1 in iv[1:]:
+                if e0 > ce:
+                    tot += ce - cs
+                    cs, ce = e0, e1
+                else:
+                    ce = max(ce, e1)
+            tot += ce - cs
+            busy.append(tot)
+            span.append(iv[-1][1] - iv[0][0] if iv else 0.0)
+        import statistics as _st
+        attribution = {
+            "host_enqueue_ms_per_step": round(th * 1e3 / args.steps, 4),
+            "wall_ms_per_step": round(tw * 1e3 / args.steps, 4),
+            "gpu_busy_ms_per_step": round(_st.median(busy) / 1e3, 4) if busy else None,
+            "gpu_span_ms_per_step": round(_st.median(span) / 1e3, 4) if span else None,
+            "stamped_launches_per_step": per_step,
+            "settle_sample_ms_per_step": settle_sample_ms,
+            "note": ("host_enqueue: perf_counter over the enqueue of --steps steps without synchronisation; "
+                     "gpu_busy: union of the stamped executor launch spans of one step (median of 5 steps, "
+                     "all streams), gpu_span: first entry to last exit of the step's stamped launches"),
+        }
 
     # every timed class over its own region of args.steps eager steps, after the `value` region (event
     # records cost ~10 us each: 1.90 vs 1.72 ms per step measured on one box; events captured into a
@@ -460,10 +529,11 @@ def main():
             "graphs_per_gpu": args.bs,
             "global_batch": args.bs * world,
             "parallelism": f"dp{world}",
-            "collective": ("rccl" if backend == "nccl" else backend) if world > 1 else None,
+            "collective": ("rccl" if backend == "nccl" else backend) if (world > 1 or force_dp) else None,
         },
         "rank_ms_per_step": rank_ms,
         "comm": comm,
+        "attribution": attribution,
         "roofline": roof,
         "roofline_hbm": roof_hbm,
         "roofline_fwd": roof_fwd,
@@ -485,7 +555,7 @@ def main():
         ok = int(f.item())
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if world > 1 or force_dp:
         dist.destroy_process_group()
     if not ok:
         sys.exit("bench: a rank produced non-finite outputs")

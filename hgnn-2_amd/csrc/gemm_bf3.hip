@@ -532,7 +532,8 @@ int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const
     if (r_cap <= 0) return 0;
     if (nz <= 0) return HGNN_ERR_ARG;
     if ((long long)r_cap * (lda > lddy ? lda : lddy) >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
-    // ring depth 2: step times 1.300-1.302 ms against 1.306-1.314 (4) and 1.313-1.323 (6), alternating runs
+    // ring depth 4 (k_gemm_bf3_tn_ring<4>, round 5: 1.1038 vs 1.1146 ms median over eight alternating pairs against
+    // k_gemm_bf3_tn<2>; depth 3 bimodal, depth 2 slower -- DESIGN.md §8 round 5)
     const dim3 g(ceil_div(o, 128), ceil_div(k, 128), nz);
     static const int ring = [] {  // HGNN_DW_RING: 0 = k_gemm_bf3_tn<2>, 2..4 = k_gemm_bf3_tn_ring<depth>
         const char* e = getenv("HGNN_DW_RING");

@@ -412,6 +412,8 @@ struct Timer {
     std::vector<double> st_ms;  // per launch, filled on the first read after a region
     std::vector<uint64_t> st_lo, st_hi;  // per launch: first entry / last exit stamp (10 ns ticks)
     bool st_read = false;
+    int rd_used = -1;         // used / st_used at the last read: a read is reused only while neither moved
+    long long rd_st_used = -1;
 };
 
 struct ClockScope {  // t_clock for the launches of one TL call
@@ -494,7 +496,11 @@ static int side_stream(hipStream_t main_s, SideStream** out) {
         static const bool fence = env_flag("HGNN_EVENT_FENCE", false);
         const unsigned ef = hipEventDisableTiming | (fence ? 0u : hipEventDisableSystemFence);
         for (int i = 0; i < 2; ++i) HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.fork[i], ef));
-        for (int i = 0; i <= BWD_NBUF; ++i) HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[i], ef));
+        for (int i = 0; i < BWD_NBUF; ++i) HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[i], ef));
+        // the end-of-backward join hands the side stream's final dW / bias gradients to the caller's stream,
+        // whose next consumer may be a D2H copy (gloo DP) or a peer: that record keeps the system-scope
+        // release (once per step)
+        HGNN_HOST_CHECK(hipEventCreateWithFlags(&ss.join[BWD_NBUF], hipEventDisableTiming));
         ss.dev = dev;
         HGNN_HOST_CHECK(hipSetDevice(cur));
     }
@@ -1306,7 +1312,7 @@ void hgnn_timer_reset(void* timer) {
 
 // Stamp mode: a launch's time = max over its waves' exit stamps - min over their entry stamps (100 MHz).
 static int timer_read_stamps(Timer* t) {
-    if (t->st_read) return HGNN_OK;
+    if (t->st_read && t->rd_used == t->used && t->rd_st_used == t->st_used) return HGNN_OK;
     if (hipDeviceSynchronize() != hipSuccess) return HGNN_ERR_HIP;
     std::vector<uint64_t> h((size_t)t->st_used);
     if (t->st_used && hipMemcpy(h.data(), t->st, (size_t)t->st_used * 8, hipMemcpyDeviceToHost) != hipSuccess)
@@ -1326,6 +1332,8 @@ static int timer_read_stamps(Timer* t) {
         t->st_hi[i] = hi;
     }
     t->st_read = true;
+    t->rd_used = t->used;
+    t->rd_st_used = t->st_used;
     return HGNN_OK;
 }
 

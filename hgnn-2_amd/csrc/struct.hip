@@ -775,6 +775,7 @@ __global__ void __launch_bounds__(XR_THREADS) __attribute__((amdgpu_waves_per_eu
 // the register-staged extraction's shape limits (see k_extract_reg)
 static bool extract_reg_fits(const ExtractArgs& a) {
     const int J = a.jtot;
+    if (J < 3 || J > 4) return false;  // k_extract_reg is instantiated for J_tot 3 and 4 only
     if (a.nmax < 1 || a.nmax > XR_WAVES * XR_MR_N || a.nmax * J > 64 * XR_MCH_N) return false;
     long long words = a.nmax * ((a.nmax + 31) / 32) * 2;
     if (a.dual) {
@@ -844,7 +845,7 @@ int launch_extract(const ExtractArgs& a, hipStream_t s) {
             switch (a.jtot) {
                 case 3: HGNN_KLAUNCH(k_extract_reg<3>, dim3(a.bs), dim3(XR_THREADS), 0, s, as); break;
                 case 4: HGNN_KLAUNCH(k_extract_reg<4>, dim3(a.bs), dim3(XR_THREADS), 0, s, as); break;
-                default: return 2;  // (jtot > 4 never fits: 3 node rows of 128 floats)
+                default: return 2;  // (extract_reg_fits admits J_tot 3 and 4 only)
             }
         }
         HGNN_LAUNCH_CHECK();

@@ -140,8 +140,11 @@ class LayerBucketAllReduce:
     gradients into the flat buffer and all-reduces it in one collective after the backward.
     """
 
-    def __init__(self, model, group=None, sync_running=True):
+    def __init__(self, model, group=None, sync_running=True, force=False):
         self.model = model
+        # force: run the bucketed collectives even in a group of one rank (an RCCL group of world size 1 on a
+        # one-GPU box exercises the communication stream, the per-layer events and the RCCL kernels)
+        self.force = force
         self.group = group
         self.sync_running = sync_running
         spec = model._spec(next(model.parameters()).device)
@@ -210,7 +213,7 @@ class LayerBucketAllReduce:
                     v.copy_(p.grad)
             p.grad = v
         self.fresh = False
-        if world == 1:
+        if world == 1 and not self.force:
             return
         run = running_stats(self.model) if self.n_run else []
         if run and sum(t.numel() for t in run) != self.n_run:

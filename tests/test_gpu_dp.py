@@ -217,3 +217,63 @@ def test_world8_config4_global_batch_4096_d128():
     graphs, shards, oracle, got = _run_world(world, d, nl, ng, timeout=600)
     assert max(len(s) for s in shards) - min(len(s) for s in shards) <= 16
     _check_world(world, nl, shards, oracle, got, ng)
+
+
+def _nccl_world1_worker(port, q):
+    """One rank in an RCCL ("nccl") process group of world size 1: the plain step's gradients, then the same
+    step with LayerBucketAllReduce forced on (communication stream, per-layer executor events, the RCCL
+    all-reduce kernels) -- a sum over one rank and a division by 1 leave every gradient bit unchanged."""
+    os.environ.setdefault("HGNN_STRICT", "1")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        _paths()
+        import fixture_util as fu
+        from hgnn_amd.dp import LayerBucketAllReduce, running_stats
+        from models.gnns.model_mnb import GNN_lg
+        graphs, _ = _shards(1, 64)
+        X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = [t.cuda() for t in _batch(graphs)]
+        model = GNN_lg(0, D, L, 5, 1, 1, ORDER).cuda()
+        fu.det_init(model, WSEED)
+        out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+        torch.nn.MSELoss()(out, T).backward()
+        plain = {k: p.grad.detach().clone() for k, p in model.named_parameters()}
+        run_plain = [t.clone() for t in running_stats(model)]
+        dp = LayerBucketAllReduce(model, force=True)
+        res = {"backend": dist.get_backend()}
+        for step in range(2):
+            model.zero_grad(set_to_none=True)
+            out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+            torch.nn.MSELoss()(out, T).backward()
+            dp.timing = step == 1
+            dp()
+        torch.cuda.synchronize()
+        res["comm"] = dp.timing_summary()
+        res["flat_is_grad"] = all(p.grad.data_ptr() == v.data_ptr() for p, v in zip(dp.params, dp.views))
+        res["bitwise"] = {k: bool(torch.equal(p.grad, plain[k])) for k, p in model.named_parameters()}
+        # the running statistics went through the collective too (after two more training forwards)
+        res["running_finite"] = all(bool(torch.isfinite(t).all()) for t in running_stats(model))
+        res["running_moved"] = any(not torch.equal(a, b) for a, b in zip(running_stats(model), run_plain))
+        q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_world1_bucketed_allreduce_bitwise():
+    """The RCCL branch executed on hardware (review r05 #7): an "nccl" process group of world size 1 with the
+    per-layer buckets forced on; every gradient bitwise equal to the step without DP."""
+    import multiprocessing as mp
+    ctx = mp.get_context("forkserver")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_nccl_world1_worker, args=(_free_port(), q))
+    pr.start()
+    res = q.get(timeout=240)
+    pr.join(timeout=120)
+    assert pr.exitcode == 0
+    assert res["backend"] == "nccl"
+    assert res["flat_is_grad"]
+    assert all(res["bitwise"].values()), [k for k, v in res["bitwise"].items() if not v]
+    assert res["running_finite"] and res["running_moved"]
+    assert res["comm"] is not None and res["comm"]["buckets"] == L - 1

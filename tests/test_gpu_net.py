@@ -460,3 +460,45 @@ def test_large_J_vs_oracle_fp64(J):
     for g, r in ((Xg.grad, X64.grad), (Wg.grad, W64.grad)):
         err = (g.cpu().double() - r).abs().max().item()
         assert err <= 1e-4 * max(1.0, r.abs().max().item()), err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("J,n", [(3, 20), (4, 18), (5, 16)])
+def test_gnn_simple_small_graphs_jtot_beyond_4(J, n):
+    """J_tot = J + 2 = 5..7 on graphs small enough for the register-staged extraction's size bounds
+    (nmax * J_tot <= 128: ADVICE r05 -- k_extract_reg has J_tot 3 / 4 instances only, the other J_tot must
+    take the LDS / global extraction): GNN_simple (d = 8, L = 3, X and W requiring grad) on 16 sparse
+    SBM-n graphs against the fp64 oracle, outputs on the two-leg policy, every gradient, dX and dW."""
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_simple
+    L, d = 3, 8
+    b = _batch(dg.sbm_dataset(16, n=n, seed=70 + J, p_in=0.2, p_out=0.03), J)
+    model = GNN_simple(0, d, L, 5, 1, J).cuda()
+    fu.det_init(model, 700 + J)
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = [t.cpu() for t in b]
+    assert W.shape[3] == J + 2 and W.shape[1] * (J + 2) <= 128
+
+    def oracle(dtype, grads):
+        p = {k: v.detach().cpu().to(dtype).requires_grad_(grads) for k, v in model.state_dict().items()}
+        Xo = X.to(dtype).requires_grad_(grads)
+        Wo = W.to(dtype).requires_grad_(grads)
+        o = R.gnn_simple(p, [Xo, Wo], Nb, mask.to(dtype), L, R.bn_states(L, 2 * d, "simple", dtype), True)
+        if grads:
+            torch.nn.MSELoss()(o, T.to(dtype)).backward()
+        return o.detach(), p, Xo, Wo
+
+    ref64, p64, X64, W64 = oracle(torch.float64, True)
+    with torch.no_grad():
+        ref32 = oracle(torch.float32, False)[0]
+    Xg, Wg = X.cuda().requires_grad_(True), W.cuda().requires_grad_(True)
+    out = model([Xg, Wg], Nb.cuda(), mask.cuda())
+    torch.nn.MSELoss()(out, T.cuda()).backward()
+    o = PP.outputs_two_leg(out, ref32, ref64)
+    assert o["pass"], o
+    gmax = max(v.grad.abs().max().item() for v in p64.values())
+    for k, prm in model.named_parameters():
+        err = (prm.grad.cpu().double() - p64[k].grad).abs()
+        assert torch.all(err <= 1e-4 * gmax + 1e-5 * p64[k].grad.abs()), (k, err.max().item(), gmax)
+    for g, r in ((Xg.grad, X64.grad), (Wg.grad, W64.grad)):
+        err = (g.cpu().double() - r).abs().max().item()
+        assert err <= 1e-4 * max(1.0, r.abs().max().item()), err
