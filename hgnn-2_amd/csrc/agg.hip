@@ -141,7 +141,20 @@ struct LaneBn {
     }
 };
 
-template <int JT, int CG, int CP, bool V>
+// Diagonal I / D mode (AggFwdArgs::j0 = 2): the row's entries of one 64-entry chunk (lane e: entry e, m = (col,
+// v_0, v_1, ..)) -- the diagonal entry's (v_0, v_1) go to diag[r]; an off-diagonal entry with v_0 or v_1 nonzero
+// is an operator the GEMMs' diagonal form cannot take (ERR_DIAG_ID).  found: a diagonal entry was met (uniform).
+__device__ __forceinline__ void diag_scan(const AggFwdArgs& a, int r, float4 m, int n, int lane, bool& found) {
+    const bool live = lane < n;
+    const int col = __float_as_int(m.x);
+    const bool on = live && col == r;
+    if (on) a.diag[r] = make_float2(m.y, m.z);
+    if (__ballot(on)) found = true;
+    const bool bad = live && col != r && (m.y != 0.f || m.z != 0.f);
+    if (__ballot(bad) && lane == 0) atomicOr(a.err, ERR_DIAG_ID);
+}
+
+template <int JT, int CG, int CP, bool V, int J0>
 __global__ void __launch_bounds__(AGG_NT) k_agg_fwd(AggFwdArgs a) {
     WaveStamp stamp(a.stamps);
     const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * AGG_WV + (threadIdx.x >> 6));
@@ -168,6 +181,7 @@ __global__ void __launch_bounds__(AGG_NT) k_agg_fwd(AggFwdArgs a) {
     if constexpr (CP > 0) bnp.init(a.pbn, a.cp, lane);
     const int stride = a.g.stride;
     const int nmax = max(rg.count, rp.count);
+    bool dfound = false;
     for (int e0 = 0; e0 < nmax; e0 += 64) {
         const int ng = min(64, max(0, rg.count - e0)), np = min(64, max(0, rp.count - e0));
         float4 mg = make_float4(0.f, 0.f, 0.f, 0.f), mp = mg;
@@ -180,6 +194,8 @@ __global__ void __launch_bounds__(AGG_NT) k_agg_fwd(AggFwdArgs a) {
                 for (int j = 3; j < JT; ++j)
                     mx[j - 3] = lane < ng ? a.g.entries[(long long)(rg.start + e0 + lane) * stride + 1 + j] : 0.f;
             }
+            if constexpr (J0 > 0)
+                if (a.diag) diag_scan(a, r, mg, ng, lane, dfound);
         }
         if constexpr (CP > 0) mp = lane_entry(a.p.entries, 4, rp.start + e0, np, lane);
         const int nn = max(ng, np);
@@ -223,7 +239,7 @@ __global__ void __launch_bounds__(AGG_NT) k_agg_fwd(AggFwdArgs a) {
 #pragma unroll
                 for (int u = 0; u < AGG_U; ++u)
 #pragma unroll
-                    for (int j = 0; j < JT; ++j)
+                    for (int j = J0; j < JT; ++j)
 #pragma unroll
                         for (int i = 0; i < CG; ++i) acc[j][i] = fmaf(v[u][j], xg[u][i], acc[j][i]);
             }
@@ -242,16 +258,18 @@ __global__ void __launch_bounds__(AGG_NT) k_agg_fwd(AggFwdArgs a) {
     }
     if constexpr (CG > 0) {
 #pragma unroll
-        for (int j = 0; j < JT; ++j) store_row<CG, V>(o + j * a.cg, a.cg, lane, acc[j]);
+        for (int j = J0; j < JT; ++j) store_row<CG, V>(o + (j - J0) * a.cg, a.cg, lane, acc[j]);
+        if constexpr (J0 > 0)
+            if (a.diag && !dfound && lane == 0) a.diag[r] = make_float2(0.f, 0.f);
     }
     if constexpr (CP > 0) {
-        const int base = JT * a.cg;
+        const int base = (JT - J0) * a.cg;
         store_row<CP, V>(o + base, a.cp, lane, am);
         store_row<CP, V>(o + base + a.cp, a.cp, lane, ad);
     }
     // zero the row padding [K, ldo): the GEMMs run over the padded width
     if (a.pad_from >= 0) {
-        const int kk = a.pad_from > 0 ? a.pad_from : JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
+        const int kk = a.pad_from > 0 ? a.pad_from : (JT - J0) * a.cg + (CP > 0 ? 2 * a.cp : 0);
         if (lane < a.ldo - kk) o[kk + lane] = 0.f;
     }
 }
@@ -259,7 +277,7 @@ __global__ void __launch_bounds__(AGG_NT) k_agg_fwd(AggFwdArgs a) {
 // k_agg_fwd with RPW rows per wave (rows RPW w .. RPW w + RPW - 1): the row infos of all of them, then the first entry
 // chunk of all of them, are fetched before the first row's gathers, so RPW rows cost RPW + 2 dependent round
 // trips instead of 3 RPW.
-template <int JT, int CG, int CP, bool V, int RPW>
+template <int JT, int CG, int CP, bool V, int RPW, int J0>
 __global__ void __launch_bounds__(AGG_NT) k_agg_fwd_rpw(AggFwdArgs a) {
     WaveStamp stamp(a.stamps);
     const int r0 = __builtin_amdgcn_readfirstlane((blockIdx.x * AGG_WV + (threadIdx.x >> 6)) * RPW);
@@ -315,6 +333,7 @@ __global__ void __launch_bounds__(AGG_NT) k_agg_fwd_rpw(AggFwdArgs a) {
 #pragma unroll
     for (int i = 0; i < CPx; ++i) am[i] = ad[i] = 0.f;
     const int nmax = max(rg.count, rp.count);
+    bool dfound = false;
     for (int e0 = 0; e0 < nmax; e0 += 64) {
         const int ng = min(64, max(0, rg.count - e0)), np = min(64, max(0, rp.count - e0));
         float4 mg = mgk[k], mp = mpk[k];
@@ -333,6 +352,8 @@ __global__ void __launch_bounds__(AGG_NT) k_agg_fwd_rpw(AggFwdArgs a) {
             }
             if constexpr (CP > 0) mp = lane_entry(a.p.entries, 4, rp.start + e0, np, lane);
         }
+        if constexpr (J0 > 0 && CG > 0)
+            if (a.diag) diag_scan(a, r, mg, ng, lane, dfound);
         const int nn = max(ng, np);
         for (int e = 0; e < nn; e += AGG_U) {
             float xg[AGG_U][CGx], v[AGG_U][JT], xp[AGG_U][CPx], vm[AGG_U], vd[AGG_U];
@@ -374,7 +395,7 @@ __global__ void __launch_bounds__(AGG_NT) k_agg_fwd_rpw(AggFwdArgs a) {
 #pragma unroll
                 for (int u = 0; u < AGG_U; ++u)
 #pragma unroll
-                    for (int j = 0; j < JT; ++j)
+                    for (int j = J0; j < JT; ++j)
 #pragma unroll
                         for (int i = 0; i < CG; ++i) acc[j][i] = fmaf(v[u][j], xg[u][i], acc[j][i]);
             }
@@ -393,16 +414,18 @@ __global__ void __launch_bounds__(AGG_NT) k_agg_fwd_rpw(AggFwdArgs a) {
     }
     if constexpr (CG > 0) {
 #pragma unroll
-        for (int j = 0; j < JT; ++j) store_row<CG, V>(o + j * a.cg, a.cg, lane, acc[j]);
+        for (int j = J0; j < JT; ++j) store_row<CG, V>(o + (j - J0) * a.cg, a.cg, lane, acc[j]);
+        if constexpr (J0 > 0)
+            if (a.diag && !dfound && lane == 0) a.diag[r] = make_float2(0.f, 0.f);
     }
     if constexpr (CP > 0) {
-        const int base = JT * a.cg;
+        const int base = (JT - J0) * a.cg;
         store_row<CP, V>(o + base, a.cp, lane, am);
         store_row<CP, V>(o + base + a.cp, a.cp, lane, ad);
     }
     // zero the row padding [K, ldo): the GEMMs run over the padded width
     if (a.pad_from >= 0) {
-        const int kk = a.pad_from > 0 ? a.pad_from : JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
+        const int kk = a.pad_from > 0 ? a.pad_from : (JT - J0) * a.cg + (CP > 0 ? 2 * a.cp : 0);
         if (lane < a.ldo - kk) o[kk + lane] = 0.f;
     }
     }
@@ -417,13 +440,13 @@ static int cpl_of(int c) {
     return -1;
 }
 
-template <int JT, int CG, int CP>
+template <int JT, int CG, int CP, int J0>
 static void agg_fwd_v(const AggFwdArgs& a0, dim3 g, hipStream_t s) {
     AggFwdArgs a = a0;
-    const int kk = JT * a.cg + (CP > 0 ? 2 * a.cp : 0);
+    const int kk = (JT - J0) * a.cg + (CP > 0 ? 2 * a.cp : 0);
     const bool v = (CG == 0 || vec_ok(CG, a.cg, a.xg, {})) && (CP == 0 || vec_ok(CP, a.cp, a.xp, {})) &&
                    (CG == 0 || vec_ok(CG, a.cg, a.out, {a.ldo, (long long)kk})) &&
-                   (CP == 0 || vec_ok(CP, a.cp, a.out, {a.ldo, (long long)JT * a.cg, (long long)a.cp}));
+                   (CP == 0 || vec_ok(CP, a.cp, a.out, {a.ldo, (long long)(JT - J0) * a.cg, (long long)a.cp}));
     static const int rpw = [] {  // rows per wave: 1 (k_agg_fwd), 2 or 4 (k_agg_fwd_rpw; J_tot = 3 only)
         const char* e = getenv("HGNN_AGG_RPW");
         const int r = e ? atoi(e) : 2;
@@ -434,30 +457,47 @@ static void agg_fwd_v(const AggFwdArgs& a0, dim3 g, hipStream_t s) {
             const dim3 g2(ceil_div(a.cap_rows, rpw * AGG_WV));
             a.stamps = clock_stamps((long long)g2.x * AGG_WV);
             if (rpw == 4) {
-                if (v) HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, true, 4>), g2, dim3(AGG_NT), 0, s, a);
-                else HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, false, 4>), g2, dim3(AGG_NT), 0, s, a);
+                if (v) HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, true, 4, J0>), g2, dim3(AGG_NT), 0, s, a);
+                else HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, false, 4, J0>), g2, dim3(AGG_NT), 0, s, a);
             } else {
-                if (v) HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, true, 2>), g2, dim3(AGG_NT), 0, s, a);
-                else HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, false, 2>), g2, dim3(AGG_NT), 0, s, a);
+                if (v) HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, true, 2, J0>), g2, dim3(AGG_NT), 0, s, a);
+                else HGNN_KLAUNCH((k_agg_fwd_rpw<JT, CG, CP, false, 2, J0>), g2, dim3(AGG_NT), 0, s, a);
             }
             return;
         }
     }
     a.stamps = clock_stamps((long long)g.x * AGG_WV);
-    if (v) HGNN_KLAUNCH((k_agg_fwd<JT, CG, CP, true>), g, dim3(AGG_NT), 0, s, a);
-    else HGNN_KLAUNCH((k_agg_fwd<JT, CG, CP, false>), g, dim3(AGG_NT), 0, s, a);
+    if (v) HGNN_KLAUNCH((k_agg_fwd<JT, CG, CP, true, J0>), g, dim3(AGG_NT), 0, s, a);
+    else HGNN_KLAUNCH((k_agg_fwd<JT, CG, CP, false, J0>), g, dim3(AGG_NT), 0, s, a);
+}
+
+template <int JT, int CG, int CP>
+static int agg_fwd_j0(const AggFwdArgs& a, dim3 g, hipStream_t s) {
+    // the diagonal I / D form is built for the layer widths the executor gives it: G and P inputs of the
+    // same 2d <= 256 channels (or no P part, GNN_simple)
+    if (a.j0 == 2) {
+        if constexpr (CG > 0 && CG <= 4 && (CP == 0 || CP == CG)) {
+            agg_fwd_v<JT, CG, CP, 2>(a, g, s);
+            return 0;
+        }
+        return 2;
+    }
+    agg_fwd_v<JT, CG, CP, 0>(a, g, s);
+    return 0;
 }
 
 template <int JT, int CG>
 static int agg_fwd_cp(const AggFwdArgs& a, dim3 g, hipStream_t s) {
+    int r = 0;
     switch (cpl_of(a.xp ? a.cp : 0)) {
-        case 0: agg_fwd_v<JT, CG, 0>(a, g, s); break;
-        case 1: agg_fwd_v<JT, CG, 1>(a, g, s); break;
-        case 2: agg_fwd_v<JT, CG, 2>(a, g, s); break;
-        case 4: agg_fwd_v<JT, CG, 4>(a, g, s); break;
-        case 8: agg_fwd_v<JT, CG, 8>(a, g, s); break;
+        case 0: r = agg_fwd_j0<JT, CG, 0>(a, g, s); break;
+        case 1: r = agg_fwd_j0<JT, CG, 1>(a, g, s); break;
+        case 2: r = agg_fwd_j0<JT, CG, 2>(a, g, s); break;
+        case 4: r = agg_fwd_j0<JT, CG, 4>(a, g, s); break;
+        case 8: r = agg_fwd_j0<JT, CG, 8>(a, g, s); break;
         default: return 2;
     }
+    if (r) return r;
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -478,6 +518,7 @@ static int agg_fwd_cg(const AggFwdArgs& a, dim3 g, hipStream_t s) {
 
 int launch_agg_fwd(const AggFwdArgs& a, hipStream_t s) {
     if (a.cap_rows <= 0) return 0;
+    if (a.j0 != 0 && (a.j0 != 2 || !a.xg || (a.diag && !a.err))) return HGNN_ERR_ARG;
     const dim3 g(ceil_div(a.cap_rows, AGG_WV));
     switch (a.jtot) {
         case 3: return agg_fwd_cg<3>(a, g, s);

@@ -118,6 +118,7 @@ enum : uint32_t {
     ERR_CCN_SELFLOOP = 1u << 3,  // CCN adjacency without self loop (chi_ii absent)
     ERR_CCN_DEGREE = 1u << 4,    // CCN degree above the compiled bound
     ERR_CCN_ASYM = 1u << 5,      // CCN adjacency pattern not symmetric
+    ERR_DIAG_ID = 1u << 6,       // operator slice 0 or 1 (I, D) with an off-diagonal entry (diagonal I / D mode)
 };
 
 __device__ __forceinline__ float wave_sum(float v) {

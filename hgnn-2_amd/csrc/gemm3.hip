@@ -735,20 +735,26 @@ int dw3_chunks(int r_cap, int o, int k) {
 
 size_t dw3_slab_floats(int r_cap, int o, int k) { return (size_t)dw3_chunks(r_cap, o, k) * o * k; }
 
+bool dw_bf3_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("HGNN_DW_BF3");
+        return !e || e[0] != '0';
+    }();
+    return on;
+}
+
 // slabs[z][o][k] = sum_{r in chunk z} dY[r, o] A[r, k]
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
-                    int nz, float* slabs, hipStream_t s) {
+                    int nz, float* slabs, hipStream_t s, const DiagIdArgs* id) {
     if (r_cap <= 0) return 0;
     if (nz <= 0) return HGNN_ERR_ARG;
     static const bool xcd = [] {
         const char* e = getenv("HGNN_DW_XCD");
         return !e || e[0] != '0';
     }();
-    static const bool bf3 = [] {
-        const char* e = getenv("HGNN_DW_BF3");
-        return !e || e[0] != '0';
-    }();
-    if (bf3) return launch_gemm_bf3_dw(dy, lddy, a, lda, r_valid, r_cap, o, k, nz, slabs, xcd, s);
+    const bool bf3 = dw_bf3_enabled();
+    if (bf3) return launch_gemm_bf3_dw(dy, lddy, a, lda, r_valid, r_cap, o, k, nz, slabs, xcd, s, id);
+    if (id) return HGNN_ERR_UNSUPPORTED;  // the diagonal I / D columns: the split-bf16 kernel only
     HGNN_KLAUNCH((k_gemm3_tn<128, 128, 32, 4, 2>), dim3(ceil_div(o, 128), ceil_div(k, 128), nz), dim3(512), 0, s,
                        dy, lddy, a, lda, slabs, o, k, r_valid, nz, xcd && nz % 8 == 0 ? 1 : 0);
     HGNN_LAUNCH_CHECK();

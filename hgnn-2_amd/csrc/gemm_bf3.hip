@@ -29,14 +29,16 @@ constexpr int G_STAGE = 6 * G_PLANE;                  // A planes, then B planes
 
 __device__ __forceinline__ int swz(int row, int ch) { return row * G_ROWB + 16 * (ch ^ ((row >> 2) & 3)); }
 
+template <bool ID>
 __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__ A, int lda,
                                                        const __bf16* __restrict__ B, long long pb, int ldb,
                                                        const int* __restrict__ m_valid, int m_cap, int N, int K,
                                                        float* __restrict__ Y, int ldy, const float* __restrict__ bias,
                                                        int relu_from, float* __restrict__ bn_part,
-                                                       uint64_t* stamps) {
+                                                       uint64_t* stamps, DiagIdArgs id) {
     WaveStamp stamp(stamps);
     __shared__ __attribute__((aligned(16))) char lds[2 * G_STAGE];
+    __shared__ float bn_mu[256], bn_sc[256];  // diagonal I / D columns: BN of x per channel
     const int M = m_valid ? *m_valid : m_cap;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv >> 1, wn = wv & 1;
@@ -49,13 +51,34 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
     // staging: A -- 64 rows x 4 chunks of 8 k, one chunk (two float4) per thread, split into the three
     // planes; B -- 3 planes x 64 rows x 4 chunks of 16 B, three per thread
     const int arow = tid >> 2, ach = tid & 3;
+    // diagonal I / D columns (DiagIdArgs): logical k < kx read x (BN applied at the store, times the row's v_0 /
+    // v_1); kx is a multiple of G_BK, so a stage is wholly of one kind
+    const int kx = ID ? 2 * id.c : 0;
+    float2 dg = make_float2(0.f, 0.f);
+    float bnb = 0.f;
+    if constexpr (ID) {
+        for (int c = tid; c < id.c; c += G_NT) {
+            const float w = *id.bn.w;
+            bn_mu[c] = id.bn.mean[c];
+            bn_sc[c] = bn_scale(w, id.bn.std[c]);
+        }
+        bnb = *id.bn.b;
+        if (m0 + arow < M) dg = id.diag[m0 + arow];  // rows past M: coefficient 0, the operand 0
+    }
     float4 ra[2];
     u32x4 rb[3];
     auto load = [&](int k0) {
         const int k = k0 + 8 * ach, gm = m0 + arow;
-        const float* ap = A + (long long)gm * lda + k;
-        ra[0] = (gm < M && k < K) ? *reinterpret_cast<const float4*>(ap) : make_float4(0.f, 0.f, 0.f, 0.f);
-        ra[1] = (gm < M && k + 4 < K) ? *reinterpret_cast<const float4*>(ap + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ID && k0 < kx) {
+            const int ch = k - (k >= id.c ? id.c : 0);
+            const float* xp = id.x + (long long)gm * id.ldx + ch;
+            ra[0] = gm < M ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
+            ra[1] = gm < M ? *reinterpret_cast<const float4*>(xp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+            const float* ap = A + (long long)gm * lda + (k - kx);
+            ra[0] = (gm < M && k < K) ? *reinterpret_cast<const float4*>(ap) : make_float4(0.f, 0.f, 0.f, 0.f);
+            ra[1] = (gm < M && k + 4 < K) ? *reinterpret_cast<const float4*>(ap + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const int e = tid + G_NT * i, pl = e >> 8, row = (e & 255) >> 2, ch = e & 3;
@@ -64,9 +87,15 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
                                          : u32x4{0u, 0u, 0u, 0u};
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, int k0) {
         char* st = lds + buf * G_STAGE;
-        const float xv[8] = {ra[0].x, ra[0].y, ra[0].z, ra[0].w, ra[1].x, ra[1].y, ra[1].z, ra[1].w};
+        float xv[8] = {ra[0].x, ra[0].y, ra[0].z, ra[0].w, ra[1].x, ra[1].y, ra[1].z, ra[1].w};
+        if (ID && k0 < kx) {  // v_j(r) * BN(x): the aggregation's fmaf(v_j, x̂, 0) of the diagonal entry
+            const int k = k0 + 8 * ach, hi = k >= id.c, ch = k - (hi ? id.c : 0);
+            const float v = hi ? dg.y : dg.x;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[e] = fmaf(v, bn_z_s(xv[e], bn_mu[ch + e], bn_sc[ch + e], bnb), 0.f);
+        }
         bf16x8 p0, p1, p2;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -91,8 +120,9 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
     const int nt = (K + G_BK - 1) / G_BK;
     const int r31 = lane & 31, h = lane >> 5;
     const int frow = wm * 32 + r31, fcol = wn * 32 + r31;
+    if constexpr (ID) __syncthreads();  // the BN table
     load(0);
-    store(0);
+    store(0, 0);
     __syncthreads();
     if (nt > 1) load(G_BK);
     for (int t = 0; t < nt; ++t) {
@@ -118,7 +148,7 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
         }
         acc += tacc;  // per-stage partial sums added to acc (fma chains of G_BK terms, as the fp32 GEMMs)
         if (t + 1 < nt) {
-            store((t + 1) & 1);
+            store((t + 1) & 1, (t + 1) * G_BK);
             if (t + 2 < nt) load((t + 2) * G_BK);
         }
         __syncthreads();
@@ -290,166 +320,52 @@ constexpr int D_BK = 16, D_NT = 512, D_ROWB = D_BK * 2, D_PLANE = 128 * D_ROWB, 
 
 __device__ __forceinline__ int dswz(int m, int ch) { return m * D_ROWB + 16 * (ch ^ ((m >> 3) & 1)); }
 
-template <int PD>
-__global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn(const float* __restrict__ A, int lda,
-                                                      const float* __restrict__ B, int ldb,
-                                                      float* __restrict__ slabs, int M, int N,
-                                                      const int* __restrict__ r_valid, int nz, int xcd_remap,
-                                                      uint64_t* stamps) {
-    WaveStamp stamp(stamps);
-    static_assert(PD >= 2, "a ring of at least two stages");
-    __shared__ __attribute__((aligned(16))) char lds[2 * D_STAGE];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int wm = wv >> 1, wn = wv & 1;
-    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    if (xcd_remap) {  // k_gemm3_tn's order: the output tiles of one row chunk on one XCD
-        const int T = gridDim.x * gridDim.y;
-        const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-        const int j = L >> 3, t = j % T;
-        bz = (L & 7) + 8 * (j / T);
-        bx = t % gridDim.x;
-        by = t / gridDim.x;
-    }
-    const int m0 = bx * 128, n0 = by * 128;
-    const int R = *r_valid;
-    const int kchunk = dw3_kc(R, nz);
-    const int kbeg = bz * kchunk, kend = min(R, kbeg + kchunk);
-    if (kbeg >= kend) return;  // the reduce only sums the chunks that hold rows
-    const int col = tid & 127, rq = tid >> 7;
-    const bool am = m0 + col < M, bn = n0 + col < N;
-    const float* ap = A + m0 + col;
-    const float* bp = B + n0 + col;
-    float ra[PD][4], rb[PD][4];
-    auto load = [&](float (&xa)[4], float (&xb)[4], int k0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int gk = k0 + 4 * rq + i;
-            xa[i] = (gk < kend && am) ? ap[(long long)gk * lda] : 0.f;
-            xb[i] = (gk < kend && bn) ? bp[(long long)gk * ldb] : 0.f;
-        }
-    };
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    auto store = [&](const float (&xa)[4], const float (&xb)[4], int buf) {
-        char* st = lds + buf * D_STAGE;
-        const int off = dswz(col, rq >> 1) + (rq & 1) * 8;
-        bf16x4 p[3], q[3];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            __bf16 x, y, z;
-            split3(xa[i], x, y, z);
-            p[0][i] = x;
-            p[1][i] = y;
-            p[2][i] = z;
-            split3(xb[i], x, y, z);
-            q[0][i] = x;
-            q[1][i] = y;
-            q[2][i] = z;
-        }
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-            *reinterpret_cast<bf16x4*>(st + pl * D_PLANE + off) = p[pl];
-            *reinterpret_cast<bf16x4*>(st + (3 + pl) * D_PLANE + off) = q[pl];
-        }
-    };
-    f32x16 acc[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-    const int nt = (kend - kbeg + D_BK - 1) / D_BK;
-    const int r31 = lane & 31, h = lane >> 5;
-#pragma unroll
-    for (int u = 0; u < PD; ++u) load(ra[u], rb[u], kbeg + u * D_BK);
-    store(ra[0], rb[0], 0);
-    __syncthreads();
-    for (int t0 = 0; t0 < nt; t0 += PD) {
-#pragma unroll
-        for (int u = 0; u < PD; ++u) {
-            const int t = t0 + u;
-            if (t >= nt) break;
-            const char* st = lds + (t & 1) * D_STAGE;
-            bf16x8 a[3], b[2][3];
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
-                a[pl] = *reinterpret_cast<const bf16x8*>(st + pl * D_PLANE + dswz(wm * 32 + r31, h));
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    b[j][pl] = *reinterpret_cast<const bf16x8*>(st + (3 + pl) * D_PLANE + dswz(wn * 64 + j * 32 + r31, h));
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {  // the six terms with i + j <= 4, the small ones first
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[j][1], acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][2], acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[j][0], acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][1], acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[j][0], acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][0], acc[j], 0, 0, 0);
-            }
-            if (t + 1 < nt) {
-                const int un = (u + 1) % PD;  // the slot holding stage t + 1
-                store(ra[un], rb[un], (t + 1) & 1);
-                load(ra[u], rb[u], kbeg + (t + PD) * D_BK);  // slot u (stage t, staged) takes stage t + PD
-            }
-            __syncthreads();
-        }
-    }
-    float* out = slabs + (long long)bz * M * N;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int gn = n0 + wn * 64 + j * 32 + r31;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int gm = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (gm < M && gn < N) out[(long long)gm * N + gn] = acc[j][r];
-        }
-    }
-}
-
-// k_gemm_bf3_tn with a ring the compiler keeps: the loads unconditional (clamped row and column, the
+// The ring (round 5; the first form, k_gemm_bf3_tn, was retired in round 6): the loads unconditional (clamped row and column, the
 // out-of-range values zeroed at the split), no branch inside the unrolled stage group (the stages past the
 // chunk's last run on zeroed planes and add nothing), and each group of loads pinned where it is issued --
-// the conditional loads and the in-loop breaks of k_gemm_bf3_tn left a vmcnt(0) before every stage, so its
+// the conditional loads and the in-loop breaks of the first form left a vmcnt(0) before every stage, so its
 // ring never had a load in flight across a stage.
-template <int PD>
-__global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn_ring(const float* __restrict__ A, int lda,
-                                                           const float* __restrict__ B, int ldb,
-                                                           float* __restrict__ slabs, int M, int N,
-                                                           const int* __restrict__ r_valid, int nz, int xcd_remap,
-                                                           uint64_t* stamps) {
-    WaveStamp stamp(stamps);
-    static_assert(PD >= 2, "a ring of at least two stages");
-    __shared__ __attribute__((aligned(16))) char lds[2 * D_STAGE];
+// VIRT: the block's 128 output columns are diagonal I / D columns (DiagIdArgs; n0 < kx, kx a multiple of 128):
+// the B operand is v_j(r) * BN(x[r][ch]) built at the split from x and the row's diag coefficient, loaded by the
+// same ring; otherwise B is the aggregate's column n - kx.
+template <int PD, bool VIRT>
+__device__ __forceinline__ void dw_ring_body(char* lds, const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                             int ldb, float* __restrict__ slabs, int M, int N, int m0, int n0, int bz,
+                                             int kbeg, int kend, const DiagIdArgs& id, int kx) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv >> 1, wn = wv & 1;
-    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    if (xcd_remap) {
-        const int T = gridDim.x * gridDim.y;
-        const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-        const int j = L >> 3, t = j % T;
-        bz = (L & 7) + 8 * (j / T);
-        bx = t % gridDim.x;
-        by = t / gridDim.x;
-    }
-    const int m0 = bx * 128, n0 = by * 128;
-    const int R = *r_valid;
-    const int kchunk = dw3_kc(R, nz);
-    const int kbeg = bz * kchunk, kend = min(R, kbeg + kchunk);
-    if (kbeg >= kend) return;
     const int col = tid & 127, rq = tid >> 7;
-    const bool am = m0 + col < M, bn = n0 + col < N;
+    const int n = n0 + col;
+    const bool am = m0 + col < M, bn = n < N;
     const float* ap = A + min(m0 + col, M - 1);
-    const float* bp = B + min(n0 + col, N - 1);
-    float ra[PD][4], rb[PD][4];
-    auto load = [&](float (&xa)[4], float (&xb)[4], int k0) {
+    const float* bp;
+    const float* cp = nullptr;  // VIRT: the row's coefficient (v_0 or v_1 of diag[r])
+    long long ldbb = ldb;
+    float mu = 0.f, sc = 1.f, bb = 0.f;
+    if constexpr (VIRT) {
+        const int hi = n >= id.c, ch = n - (hi ? id.c : 0);
+        bp = id.x + ch;
+        ldbb = id.ldx;
+        cp = reinterpret_cast<const float*>(id.diag) + hi;
+        mu = id.bn.mean[ch];
+        sc = bn_scale(*id.bn.w, id.bn.std[ch]);
+        bb = *id.bn.b;
+    } else {
+        bp = B + min(n, N - 1) - kx;
+    }
+    constexpr int NC = VIRT ? 4 : 1;
+    float ra[PD][4], rb[PD][4], rc[PD][NC];
+    auto load = [&](float (&xa)[4], float (&xb)[4], float (&xc)[NC], int k0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const long long gk = min(k0 + 4 * rq + i, kend - 1);
             xa[i] = ap[gk * lda];
-            xb[i] = bp[gk * ldb];
+            xb[i] = bp[gk * ldbb];
+            if constexpr (VIRT) xc[i] = cp[2 * gk];
         }
     };
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    auto store = [&](const float (&xa)[4], const float (&xb)[4], int buf, int k0) {
+    auto store = [&](const float (&xa)[4], const float (&xb)[4], const float (&xc)[NC], int buf, int k0) {
         char* st = lds + buf * D_STAGE;
         const int off = dswz(col, rq >> 1) + (rq & 1) * 8;
         bf16x4 p[3], q[3];
@@ -461,7 +377,9 @@ __global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn_ring(const float* __restri
             p[0][i] = x;
             p[1][i] = y;
             p[2][i] = z;
-            split3(in && bn ? xb[i] : 0.f, x, y, z);
+            float bv = xb[i];
+            if constexpr (VIRT) bv = fmaf(xc[i], bn_z_s(bv, mu, sc, bb), 0.f);  // the aggregation's value
+            split3(in && bn ? bv : 0.f, x, y, z);
             q[0][i] = x;
             q[1][i] = y;
             q[2][i] = z;
@@ -480,9 +398,9 @@ __global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn_ring(const float* __restri
     const int nt = (kend - kbeg + D_BK - 1) / D_BK;
     const int r31 = lane & 31, h = lane >> 5;
 #pragma unroll
-    for (int u = 0; u < PD; ++u) load(ra[u], rb[u], kbeg + u * D_BK);
+    for (int u = 0; u < PD; ++u) load(ra[u], rb[u], rc[u], kbeg + u * D_BK);
     __builtin_amdgcn_sched_barrier(0);
-    store(ra[0], rb[0], 0, kbeg);
+    store(ra[0], rb[0], rc[0], 0, kbeg);
     __syncthreads();
     for (int t0 = 0; t0 < nt; t0 += PD) {
 #pragma unroll
@@ -507,8 +425,8 @@ __global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn_ring(const float* __restri
                 acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][0], acc[j], 0, 0, 0);
             }
             const int un = (u + 1) % PD;  // the slot holding stage t + 1
-            store(ra[un], rb[un], (t + 1) & 1, kbeg + (t + 1) * D_BK);
-            load(ra[u], rb[u], kbeg + (t + PD) * D_BK);  // slot u (stage t, staged) takes stage t + PD
+            store(ra[un], rb[un], rc[un], (t + 1) & 1, kbeg + (t + 1) * D_BK);
+            load(ra[u], rb[u], rc[u], kbeg + (t + PD) * D_BK);  // slot u (stage t, staged) takes stage t + PD
             __builtin_amdgcn_sched_barrier(0);
             __syncthreads();
         }
@@ -525,29 +443,79 @@ __global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn_ring(const float* __restri
     }
 }
 
+template <int PD, bool ID>
+__global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn_ring(const float* __restrict__ A, int lda,
+                                                           const float* __restrict__ B, int ldb,
+                                                           float* __restrict__ slabs, int M, int N,
+                                                           const int* __restrict__ r_valid, int nz, int xcd_remap,
+                                                           uint64_t* stamps, DiagIdArgs id) {
+    WaveStamp stamp(stamps);
+    static_assert(PD >= 2, "a ring of at least two stages");
+    __shared__ __attribute__((aligned(16))) char lds[2 * D_STAGE];
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (xcd_remap) {
+        const int T = gridDim.x * gridDim.y;
+        const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int j = L >> 3, t = j % T;
+        bz = (L & 7) + 8 * (j / T);
+        bx = t % gridDim.x;
+        by = t / gridDim.x;
+    }
+    const int m0 = bx * 128, n0 = by * 128;
+    const int R = *r_valid;
+    const int kchunk = dw3_kc(R, nz);
+    const int kbeg = bz * kchunk, kend = min(R, kbeg + kchunk);
+    if (kbeg >= kend) return;
+    const int kx = ID ? 2 * id.c : 0;
+    if constexpr (ID) {
+        if (n0 < kx) {
+            dw_ring_body<(PD > 3 ? PD - 1 : PD), true>(lds, A, lda, B, ldb, slabs, M, N, m0, n0, bz, kbeg, kend, id, kx);
+            return;
+        }
+    }
+    dw_ring_body<PD, false>(lds, A, lda, B, ldb, slabs, M, N, m0, n0, bz, kbeg, kend, id, kx);
+}
+
+// the diagonal I / D columns' contract (DiagIdArgs): 2c a multiple of 32, c <= 256, float4-aligned x rows
+bool diag_id_ok(const DiagIdArgs* id, int k) {
+    return id->x && id->diag && id->bn.mean && id->bn.std && id->bn.w && id->bn.b && id->c > 0 && id->c <= 256 &&
+           (2 * id->c) % 32 == 0 && id->ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(id->x) & 15) == 0 &&
+           2 * id->c < k;
+}
+
 }  // namespace
 
 int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o,
-                       int k, int nz, float* slabs, int xcd, hipStream_t s) {
+                       int k, int nz, float* slabs, int xcd, hipStream_t s, const DiagIdArgs* id) {
     if (r_cap <= 0) return 0;
     if (nz <= 0) return HGNN_ERR_ARG;
     if ((long long)r_cap * (lda > lddy ? lda : lddy) >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    // diagonal I / D columns: whole 128-column output tiles (kx a multiple of 128), the ring kernel
+    if (id && (!diag_id_ok(id, k) || (2 * id->c) % 128 || (long long)r_cap * id->ldx >= (1ll << 31)))
+        return HGNN_ERR_UNSUPPORTED;
+    const DiagIdArgs none{};
+    const DiagIdArgs ida = id ? *id : none;
     // ring depth 4 (k_gemm_bf3_tn_ring<4>, round 5: 1.1038 vs 1.1146 ms median over eight alternating pairs against
-    // k_gemm_bf3_tn<2>; depth 3 bimodal, depth 2 slower -- DESIGN.md §8 round 5)
+    // the retired unringed form; depth 3 bimodal, depth 2 slower -- DESIGN.md §8 round 5)
     const dim3 g(ceil_div(o, 128), ceil_div(k, 128), nz);
-    static const int ring = [] {  // HGNN_DW_RING: 0 = k_gemm_bf3_tn<2>, 2..4 = k_gemm_bf3_tn_ring<depth>
+    static const int ring = [] {  // HGNN_DW_RING: 2..4 = k_gemm_bf3_tn_ring<depth>
         const char* e = getenv("HGNN_DW_RING");
         const int v = e ? atoi(e) : 4;
-        return v == 0 ? 0 : (v < 2 ? 2 : (v > 4 ? 4 : v));
+        return v < 2 ? 2 : (v > 4 ? 4 : v);
     }();
     uint64_t* st = clock_stamps((long long)g.x * g.y * g.z * (D_NT / 64));
     const int xr = xcd && nz % 8 == 0 ? 1 : 0;
-    switch (ring) {
-        case 0: HGNN_KLAUNCH(k_gemm_bf3_tn<2>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr, st); break;
-        case 2: HGNN_KLAUNCH(k_gemm_bf3_tn_ring<2>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr, st); break;
-        case 3: HGNN_KLAUNCH(k_gemm_bf3_tn_ring<3>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr, st); break;
-        default: HGNN_KLAUNCH(k_gemm_bf3_tn_ring<4>, g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr, st); break;
+#define HGNN_DW_RING_LAUNCH(D, I) \
+    HGNN_KLAUNCH((k_gemm_bf3_tn_ring<D, I>), g, dim3(D_NT), 0, s, dy, lddy, a, lda, slabs, o, k, r_valid, nz, xr, st, ida)
+    switch (ring * 2 + (id ? 1 : 0)) {
+        case 4: HGNN_DW_RING_LAUNCH(2, false); break;
+        case 5: HGNN_DW_RING_LAUNCH(2, true); break;
+        case 6: HGNN_DW_RING_LAUNCH(3, false); break;
+        case 7: HGNN_DW_RING_LAUNCH(3, true); break;
+        case 9: HGNN_DW_RING_LAUNCH(4, true); break;
+        default: HGNN_DW_RING_LAUNCH(4, false); break;
     }
+#undef HGNN_DW_RING_LAUNCH
     HGNN_LAUNCH_CHECK();
     return 0;
 }
@@ -574,16 +542,24 @@ int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, i
 
 int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
                         int ldb, int n, const float* bias, int relu_from, float* y, int ldy, float* bn_part,
-                        hipStream_t s) {
+                        hipStream_t s, const DiagIdArgs* id) {
     if (m_cap <= 0 || n <= 0) return 0;
-    if (lda % 4 || k % 4 || ldb % 8 || pb % 8 || k > lda || bf3_ld(k) > ldb || (reinterpret_cast<uintptr_t>(a) & 15) ||
-        (reinterpret_cast<uintptr_t>(b) & 15))
+    const int kx = id ? 2 * id->c : 0;
+    if (id && !diag_id_ok(id, k)) return HGNN_ERR_UNSUPPORTED;
+    if (lda % 4 || k % 4 || ldb % 8 || pb % 8 || k - kx > lda || bf3_ld(k) > ldb ||
+        (reinterpret_cast<uintptr_t>(a) & 15) || (reinterpret_cast<uintptr_t>(b) & 15))
         return HGNN_ERR_UNSUPPORTED;
     if ((long long)m_cap * lda * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    if (id && (long long)m_cap * id->ldx * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     const int gx = ceil_div(ceil_div(m_cap, G_BM), 8) * 8;
     const dim3 g(gx, ceil_div(n, G_BN));
-    HGNN_KLAUNCH(k_gemm_bf3_fwd, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, bias, relu_from,
-                 bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)));
+    const DiagIdArgs none{};
+    if (id)
+        HGNN_KLAUNCH(k_gemm_bf3_fwd<true>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, bias,
+                     relu_from, bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)), *id);
+    else
+        HGNN_KLAUNCH(k_gemm_bf3_fwd<false>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, bias,
+                     relu_from, bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)), none);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -108,6 +108,14 @@ struct AggFwdArgs {
     // the row's zero padding [pad_from, ldo): 0 = after the parts this launch writes, -1 = none
     // (a G-only launch beside a P-only one, which writes the padding)
     int pad_from;
+    // j0 = 2 ("diagonal I / D"): slices 0 and 1 of G (graph_operators' I and D, functions/operators.py:19-23)
+    // are not aggregated -- the Conv1d GEMMs read x itself and scale it per row (gemm_bf3.hip) -- so the G part
+    // holds slices 2 .. jtot - 1 at (j - 2) * cg and P starts at (jtot - 2) * cg.  diag (optional): per row
+    // the diagonal entry's (v_0, v_1), (0, 0) for a row without one; an entry off the diagonal with v_0 or v_1
+    // nonzero ORs ERR_DIAG_ID into err
+    int j0;
+    float2* diag;
+    uint32_t* err;
     uint64_t* stamps;  // set by the launch under a stamp-mode clock (common.h WaveStamp), else null
 };
 int launch_agg_fwd(const AggFwdArgs& a, hipStream_t s);
@@ -154,14 +162,28 @@ __host__ __device__ inline int bf3_ld(int k) { return (k + 15) / 16 * 16; }  // 
 // B three bf16 planes b + p pb [N][ldb] (ldb >= bf3_ld(k), zero beyond k)
 // The dA GEMM on bf16 MFMA (three-way split): Y[M][n] = A[M][k] . B^T for k <= 128 (A = dY fp32 [M][lda],
 // B = WT's three bf16 planes b + p pb [n][ldb], ldb >= bf3_ld(k), zero beyond k); HGNN_ERR_UNSUPPORTED otherwise
+// The diagonal I / D operand columns of the Conv1d GEMMs (AggFwdArgs::j0 = 2): the logical operand of a half is
+// [v_0(r) x̂_r | v_1(r) x̂_r | aggregate of slices 2.. and P], x̂ = BN(x) of the half's G input applied on load --
+// the values the full aggregation stores in its I and D columns, bit for bit (fmaf(v, x̂, 0) per element, as
+// the aggregation's first live FMA), so the GEMMs see the same operand.  kx = 2c leading logical columns come
+// from x; the rest from the aggregate (its column k - kx).  kx = 0: no such columns (the operand is the
+// aggregate alone).
+struct DiagIdArgs {
+    const float* x;        // the G input of the half, pre-BN y [rows][ldx]
+    int ldx, c;            // c channels: kx = 2c (a multiple of 32 and c <= 256 where set)
+    const float2* diag;    // per row (v_0, v_1) of the diagonal entry (AggFwdArgs::diag)
+    BnView bn;             // BN of the producer of x (mean != null)
+};
 int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
                        int ldb, int n, float* y, int ldy, hipStream_t s);
+// (id: the diagonal I / D columns, k counts them; null = none)
 int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
                         int ldb, int n, const float* bias, int relu_from, float* y, int ldy, float* bn_part,
-                        hipStream_t s);
-// The dW GEMM (launch_gemm3_dw's contract) on bf16 MFMA through the same three-way split
+                        hipStream_t s, const DiagIdArgs* id = nullptr);
+// The dW GEMM (launch_gemm3_dw's contract) on bf16 MFMA through the same three-way split (id: as the forward's,
+// for the aggregate operand)
 int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o,
-                       int k, int nz, float* slabs, int xcd, hipStream_t s);
+                       int k, int nz, float* slabs, int xcd, hipStream_t s, const DiagIdArgs* id = nullptr);
 
 struct RepackItem {
     const float* wl;   // linear conv weight (d, K)
@@ -295,6 +317,7 @@ int launch_gemm3_da(const float* dy, int lddy, const int* m_valid, int m_cap, in
 // the output tiles); the kernels derive the chunk length from the device row count, so every chunk
 // holds rows whatever the batch's fill of its capacity
 int dw3_chunks(int r_cap, int o, int k);
+bool dw_bf3_enabled();  // the dW GEMM on split-bf16 MFMA (HGNN_DW_BF3 != 0)
 __host__ __device__ inline int dw3_kc(int rows, int nz) {
     int kc = (rows + nz - 1) / nz;
     kc = (kc + 31) / 32 * 32;
@@ -302,7 +325,7 @@ __host__ __device__ inline int dw3_kc(int rows, int nz) {
 }
 size_t dw3_slab_floats(int r_cap, int o, int k);
 int launch_gemm3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o, int k,
-                    int nz, float* slabs, hipStream_t s);
+                    int nz, float* slabs, hipStream_t s, const DiagIdArgs* id = nullptr);
 // slabs [z][o][k] -> dW (rows [0, split) -> dw0, [split, o_real) -> dw1; rows >= o_real are the
 // zero padding of an odd 2d); bias grads from the BN-backward per-tile column sums of dY
 // (dbpart [tiles][o_real])

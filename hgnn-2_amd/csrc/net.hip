@@ -37,7 +37,9 @@ struct Half {
     int out, bn;
     int pw_lin, pb_lin, pw_relu, pb_relu, pbn_w, pbn_b;
     int relu_from;
-    int kp;  // row stride of the aggregate / dA buffers (k rounded up to 4: the GEMMs' float4 k)
+    int kp;  // row stride of the dA buffer and logical width of the GEMM operand (k rounded up to 4: float4 k)
+    bool id = false;  // diagonal I / D columns (AggFwdArgs::j0 = 2): the aggregate holds slices 2.. and P only
+    int kpa = 0;      // row stride of the aggregate buffer: kp, or kp - 2 cg with id
     size_t a = 0, part = 0, mean = 0, stdv = 0;
     size_t wt = 0, wc = 0, bc = 0;  // repacked Conv1d-pair weights (repack.hip)
     size_t wc3 = 0;                 // Wcat as three bf16 planes [3][2d][bf3_ld(kp)] (split-bf16 forward GEMM)
@@ -57,6 +59,7 @@ struct Program {
     std::vector<Half> halves;
     int last_gin = -1, last_pin = -1, k_last = 0, p_fcw = 0, p_fcb = 0;
     size_t a_last = 0, colsum = 0;
+    size_t diag_n = 0, diag_e = 0;  // per row (v_0, v_1) of the diagonal operator entry (diagonal I / D mode)
     size_t node_off = 0, edge_off = 0, totals = 0, err = 0;
     size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
     int entry_stride_w = 4;
@@ -94,6 +97,27 @@ static bool env_flag(const char* name, bool dflt) {
     const char* e = getenv(name);
     if (!e || !e[0]) return dflt;
     return e[0] != '0';
+}
+
+// The forward Conv1d-pair GEMM on bf16 MFMA with three-way split operands (gemm_bf3.hip: fp32 accuracy,
+// 2.7x fewer MFMA cycles); HGNN_FWD_BF3=0: the fp32 MFMA kernels (launch_gemm3_fwd).  Line-graph networks
+// with 2d % 64 == 0 (the kernel's 64-column tiles).
+static bool fwd_bf3_c2(int c2) {
+    static const bool on = env_flag("HGNN_FWD_BF3", true);
+    return on && c2 % 64 == 0;
+}
+// Diagonal I / D columns (round 6; HGNN_DIAG_ID=1: on, off by default -- measured 1.110 vs 1.105 ms per step in three
+// of three alternating pairs at config 2: the aggregation lost 5 us per step, the forward and dW GEMMs' staging
+// gained 11 and 14): graph_operators' slices 0 and 1 are I and diag(D)
+// (functions/operators.py:19-23), so the aggregate's I / D column blocks are x̂ and D_r x̂ -- two of the five
+// column blocks of a line-graph half at J = 1, written by the aggregation and read by the forward and dW GEMMs.
+// In this mode the aggregation stores only slices 2.. and P (plus each row's diagonal coefficients) and the two
+// split-bf16 GEMMs build the I / D columns from the half's input x̂ as they stage it (DiagIdArgs), the same
+// values bit for bit.  For the halves whose G input is a BN'd layer output of 2d <= 256 channels (not the
+// raw inputs of layer 0), with the split-bf16 forward and dW GEMMs.
+static bool diag_id_on(int c2) {
+    static const bool on = env_flag("HGNN_DIAG_ID", false);
+    return on && fwd_bf3_c2(c2) && dw_bf3_enabled() && c2 <= 256;
 }
 
 Program build_program(const hgnn_net_config* c) {
@@ -199,6 +223,11 @@ Program build_program(const hgnn_net_config* c) {
             in_n = out_n;
         }
     }
+    for (Half& h : P.halves) {
+        bool prod = false;
+        for (const Half& o : P.halves) prod = prod || o.out == h.gin;
+        h.id = diag_id_on(P.c2) && prod && h.cg == P.c2 && (h.pin < 0 || h.cp == P.c2);
+    }
     P.last_gin = in_n;
     P.last_pin = lg ? in_e : -1;
     P.k_last = P.jt * P.feats[in_n].c + (lg ? 2 * P.feats[in_e].c : 0);
@@ -238,7 +267,8 @@ Program build_program(const hgnn_net_config* c) {
     for (auto& h : P.halves) {
         const int cap = h.edge ? P.cap_e : P.cap_n;
         h.kp = (h.k + 3) / 4 * 4;
-        h.a = B.take((size_t)cap * h.kp * sizeof(float));
+        h.kpa = h.id ? h.kp - 2 * h.cg : h.kp;
+        h.a = B.take((size_t)cap * h.kpa * sizeof(float));
         h.part = B.take((size_t)gemm_fwd_tiles_m(cap) * P.c2 * 3 * sizeof(float));
         h.mean = B.take(P.c2 * sizeof(float));
         h.stdv = B.take(P.c2 * sizeof(float));
@@ -263,6 +293,8 @@ Program build_program(const hgnn_net_config* c) {
         }
         if (na) P.dak[i] = B.take(na * sizeof(float));
     }
+    P.diag_n = B.take((size_t)P.cap_n * sizeof(float2));
+    if (lg) P.diag_e = B.take((size_t)P.cap_e * sizeof(float2));
     P.a_last = B.take((size_t)P.cap_n * P.k_last * sizeof(float));
     P.colsum = B.take((size_t)c->bs * P.k_last * sizeof(float));
     max_da = std::max(max_da, (size_t)P.cap_n * P.k_last);
@@ -333,6 +365,19 @@ BnView feat_bn(const Program& P, void* ws, const float* const* prm, int f) {
     v.w = prm[h->pbn_w];
     v.b = prm[h->pbn_b];
     return v;
+}
+
+// The diagonal I / D operand of a half's GEMMs (DiagIdArgs): its G input (pre-BN y, BN on load) and the row
+// coefficients of its kind
+DiagIdArgs diag_id_args(const Program& P, void* ws, const float* const* prm, const Half& h) {
+    DiagIdArgs d{};
+    if (!h.id) return d;
+    d.x = feat_src(P, ws, h.gin);
+    d.ldx = P.feats[h.gin].c;
+    d.c = h.cg;
+    d.diag = at<float2>(ws, h.edge ? P.diag_e : P.diag_n);
+    d.bn = feat_bn(P, ws, prm, h.gin);
+    return d;
 }
 
 // Where a call's batch structure lives: the workspace (filled by the device
@@ -508,13 +553,7 @@ static int side_stream(hipStream_t main_s, SideStream** out) {
     return 0;
 }
 
-// The forward Conv1d-pair GEMM on bf16 MFMA with three-way split operands (gemm_bf3.hip: fp32 accuracy,
-// 2.7x fewer MFMA cycles); HGNN_FWD_BF3=0: the fp32 MFMA kernels (launch_gemm3_fwd).  Line-graph networks
-// with 2d % 64 == 0 (the kernel's 64-column tiles).
-static bool fwd_bf3(const Program& P) {
-    static const bool on = env_flag("HGNN_FWD_BF3", true);
-    return on && P.c2 % 64 == 0;
-}
+static bool fwd_bf3(const Program& P) { return fwd_bf3_c2(P.c2); }
 // the dA GEMM on the split-bf16 kernel (k_gemm_bf3_fwd with a plain-store epilogue, B = WT's planes)
 static bool da_bf3(const Program& P) {
     static const bool on = env_flag("HGNN_DA_BF3", true);
@@ -620,14 +659,26 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
             ag.cp = h.cp;
         }
         ag.out = at<float>(ws, h.a);
-        ag.ldo = h.kp;
+        ag.ldo = h.kpa;
+        if (h.id) {
+            ag.j0 = 2;
+            // the first diagonal-I / D half of its kind records the rows' diagonal coefficients
+            bool first = true;
+            for (int q = 0; q < hi; ++q) first = first && !(P.halves[q].id && P.halves[q].edge == h.edge);
+            if (first) {
+                ag.diag = at<float2>(ws, h.edge ? P.diag_e : P.diag_n);
+                ag.err = m.err;
+            }
+        }
         TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
 
+        const DiagIdArgs ida = diag_id_args(P, ws, prm, h);
         if (fwd_bf3(P))
-            TL(HGNN_K_GEMM_FWD, launch_gemm_bf3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<__bf16>(ws, h.wc3),
+            TL(HGNN_K_GEMM_FWD, launch_gemm_bf3_fwd(at<float>(ws, h.a), h.kpa, tot, cap, h.kp, at<__bf16>(ws, h.wc3),
                                                     (long long)P.c2 * bf3_ld(h.kp), bf3_ld(h.kp), P.c2,
                                                     at<float>(ws, h.bc), h.relu_from, at<float>(ws, P.feats[h.out].y),
-                                                    P.c2, c->training ? at<float>(ws, h.part) : nullptr, s));
+                                                    P.c2, c->training ? at<float>(ws, h.part) : nullptr, s,
+                                                    h.id ? &ida : nullptr));
         else
             TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<float>(ws, h.wc), h.kp,
                                                  P.c2, at<float>(ws, h.bc), h.relu_from,
@@ -863,8 +914,9 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
             if (ndw_side) TL(HGNN_K_DW_DENSE, dw_dense(h.gin, dab, h.kp, false, 1));
             // dY rows have stride c2p; the dW GEMM's float4 loads along the 2d outputs read the zero
             // padding of an odd 2d and store only the 2d real rows of each slab
-            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(dyb, P.c2p, at<float>(ws, h.a), h.kp, tot, cap, P.c2, h.k, nz,
-                                               at<float>(ws, P.slabs), s));
+            const DiagIdArgs ida = diag_id_args(P, ws, prm, h);
+            TL(HGNN_K_GEMM_DW, launch_gemm3_dw(dyb, P.c2p, at<float>(ws, h.a), h.kpa, tot, cap, P.c2, h.k, nz,
+                                               at<float>(ws, P.slabs), s, h.id ? &ida : nullptr));
             TL(HGNN_K_DW_REDUCE, launch_dw_reduce2(at<float>(ws, P.slabs), tot, nz, P.c2, P.c2, h.k, P.d,
                                                    grads[h.pw_lin], grads[h.pw_relu], dbp, grads[h.pb_lin],
                                                    grads[h.pb_relu], s));

@@ -27,6 +27,9 @@ DEVERR = {
     0x8: "CCN adjacency without a self loop (chi_ii undefined, functions/utils_ccn.py:137-140)",
     0x10: "CCN vertex degree above the compiled bound (1024 for CCN-1D, 256 for CCN-2D)",
     0x20: "CCN adjacency pattern is not symmetric (the batched CCN backward needs A_ij > 0 <=> A_ji > 0)",
+    0x40: ("operator slice 0 or 1 (graph_operators' I and D, functions/operators.py:19-23) holds an off-diagonal "
+           "entry; the executor takes these two slices as diagonal -- HGNN_DIAG_ID=0 aggregates them as general "
+           "slices"),
 }
 
 

@@ -50,18 +50,32 @@ def lg_halves(order, f_in, d, n_layers, jt):
     return out, k_last
 
 
+def diag_id(cg, cp, d):
+    """Whether the executor builds a half's I / D operand columns in its GEMMs instead of aggregating them (net.hip
+    diag_id_on: HGNN_DIAG_ID=1 (off by default), the split-bf16 forward and dW GEMMs, 2d % 64 == 0, 2d <= 256; halves whose G input
+    is a layer output of 2d channels)."""
+    import os
+    c2 = 2 * d
+    on = (os.environ.get("HGNN_DIAG_ID", "0") == "1" and split_bf16(K_GEMM_FWD, d) and split_bf16(K_GEMM_DW, d)
+          and c2 <= 256)
+    return on and cg == c2 and cp in (0, c2)
+
+
 def class_work(kcls, counts, order, f_in, d, n_layers, jt=3):
-    """(flops, bytes) of one training step for kernel class kcls (sum over its launches)."""
+    """(flops, bytes) of one training step for kernel class kcls (sum over its launches).  With the diagonal I / D
+    columns (diag_id) the aggregate a half stores is k - 2 cg wide and its GEMMs read the half's input (cg wide)
+    for the other 2 cg operand columns."""
     halves, k_last = lg_halves(order, f_in, d, n_layers, jt)
     c2 = 2 * d
     rows = lambda edge: counts["edges"] if edge else counts["nodes"]  # noqa: E731
     nnz_g = lambda edge: counts["nnz_wl"] if edge else counts["nnz_w"]  # noqa: E731
+    opnd = lambda k, cg, cp: (k - cg) if diag_id(cg, cp, d) else k  # noqa: E731  (operand columns read per row)
     fl = by = 0.0
     if kcls == K_GEMM_FWD:
         for edge, k, cg, cp in halves:
             r = rows(edge)
             fl += 2.0 * r * k * c2
-            by += 4.0 * (r * k + r * c2 + c2 * (k + 1))
+            by += 4.0 * (r * opnd(k, cg, cp) + r * c2 + c2 * (k + 1))
     elif kcls == K_GEMM_DA:
         for edge, k, cg, cp in halves:
             r = rows(edge)
@@ -71,16 +85,17 @@ def class_work(kcls, counts, order, f_in, d, n_layers, jt=3):
         for edge, k, cg, cp in halves:
             r = rows(edge)
             fl += 2.0 * r * c2 * k
-            by += 4.0 * (r * c2 + r * k + c2 * k)
+            by += 4.0 * (r * c2 + r * opnd(k, cg, cp) + c2 * k)
     elif kcls in (K_AGG_FWD, K_AGG_BWD):
         # the last layer's forward aggregation is a k_agg_fwd launch; its backward is the readout class
         # (k_readout_agg_bwd: the readout gradient R_b broadcast per graph, no [rows][K] dA read)
         items = [(e, k, cg, cp) for e, k, cg, cp in halves] + ([(False, k_last, c2, c2)] if kcls == K_AGG_FWD else [])
-        for edge, k, cg, cp in items:
+        for i, (edge, k, cg, cp) in enumerate(items):
             r, ro = rows(edge), rows(not edge)
+            cut = kcls == K_AGG_FWD and i < len(halves) and diag_id(cg, cp, d)
             s_bytes = 8.0 * (r + r) + 16.0 * (nnz_g(edge) + counts["nnz_p"])
-            by += 4.0 * (r * k + r * cg + ro * cp) + s_bytes
-            fl += 2.0 * (nnz_g(edge) * jt * cg + 2 * counts["nnz_p"] * cp)
+            by += 4.0 * (r * (k - 2 * cg if cut else k) + r * cg + ro * cp) + s_bytes
+            fl += 2.0 * (nnz_g(edge) * (jt - 2 if cut else jt) * cg + 2 * counts["nnz_p"] * cp)
     elif kcls == K_BN_FWD:
         for edge, k, cg, cp in halves:
             by += 4.0 * 2 * rows(edge) * c2
@@ -103,9 +118,10 @@ def agg_requested_bytes(kcls, counts, order, f_in, d, n_layers, jt=3):
     nnz_g = lambda edge: counts["nnz_wl"] if edge else counts["nnz_w"]  # noqa: E731
     by = 0.0
     if kcls == K_AGG_FWD:
-        for edge, k, cg, cp in halves + [(False, k_last, c2, c2)]:
+        for i, (edge, k, cg, cp) in enumerate(halves + [(False, k_last, c2, c2)]):
             r = rows(edge)
-            by += 4.0 * (nnz_g(edge) * cg + counts["nnz_p"] * cp + r * k) + 8.0 * 2 * r + 16.0 * (
+            kw = k - 2 * cg if i < len(halves) and diag_id(cg, cp, d) else k
+            by += 4.0 * (nnz_g(edge) * cg + counts["nnz_p"] * cp + r * kw) + 8.0 * 2 * r + 16.0 * (
                 nnz_g(edge) + counts["nnz_p"])
     elif kcls == K_AGG_BWD:
         for edge, k, cg, cp in halves:

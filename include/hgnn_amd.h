@@ -63,6 +63,7 @@ extern "C" {
 #define HGNN_DEVERR_CCN_SELFLOOP 0x8u /* CCN adjacency lacks a self loop        */
 #define HGNN_DEVERR_CCN_DEGREE 0x10u  /* CCN degree above the compiled bound    */
 #define HGNN_DEVERR_CCN_ASYM 0x20u    /* CCN adjacency pattern not symmetric    */
+#define HGNN_DEVERR_DIAG_ID 0x40u     /* operator slice 0 / 1 (I, D) not diagonal */
 
 int hgnn_abi_version(void);
 const char* hgnn_status_string(int status);

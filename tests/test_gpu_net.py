@@ -7,6 +7,8 @@ properties at the benchmark size.  Tolerances (SURVEY.md §8 c):
   gradients |d| <= 1e-4 * max_global|g| + 1e-5 |g|   (global floor: cv2/cv4 bias grads are 0)
 """
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -502,3 +504,38 @@ def test_gnn_simple_small_graphs_jtot_beyond_4(J, n):
     for g, r in ((Xg.grad, X64.grad), (Wg.grad, W64.grad)):
         err = (g.cpu().double() - r).abs().max().item()
         assert err <= 1e-4 * max(1.0, r.abs().max().item()), err
+
+
+def test_offdiagonal_identity_or_degree_slice_raises():
+    """The diagonal I / D columns (HGNN_DIAG_ID=1; d = 32: 2d = 64, the split-bf16 GEMMs) take operator slices 0
+    and 1 as graph_operators' I and diag(D) (functions/operators.py:19-23); an off-diagonal entry in either slice
+    of W or WL is reported (HGNN_DEVERR_DIAG_ID) instead of being dropped, and a valid call works afterwards.  The
+    switch is read once per process: a child process runs the case."""
+    import subprocess
+    import sys
+    env = dict(os.environ, HGNN_DIAG_ID="1", HGNN_STRICT="1")
+    r = subprocess.run([sys.executable, "-c", "import test_gpu_net as T; T._offdiag_case()"], env=env,
+                       cwd=os.path.dirname(os.path.abspath(__file__)), capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "offdiag ok" in r.stdout
+
+
+def _offdiag_case():
+    import hgnn_amd.datagen as dg
+    from models.gnns.model_mnb import GNN_lg
+    graphs = dg.qm9_shape_dataset(8, seed=5)
+    model = GNN_lg(0, 32, 3, 5, 1, 1, 2).cuda()
+    X, W, T, XL, WL, Pm, Pd, mask, mask_lg, Nb, Eb = _cuda(_batch(graphs))
+    for j in (0, 1):
+        Wbad = W.clone()
+        Wbad[0, 0, 1, j] = 0.25  # inside graph 0's real block, off the diagonal
+        with pytest.raises(RuntimeError, match="off-diagonal"):
+            model([X, XL, Wbad, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+        e = int(Eb[0])
+        WLbad = WL.clone()
+        WLbad[0, 0, e - 1, j] = 0.25
+        with pytest.raises(RuntimeError, match="off-diagonal"):
+            model([X, XL, W, WLbad, Pm, Pd], Nb, mask, Eb, mask_lg)
+    out = model([X, XL, W, WL, Pm, Pd], Nb, mask, Eb, mask_lg)
+    assert torch.isfinite(out).all()
+    print("offdiag ok")
