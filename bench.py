@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--force-dp", type=int, default=0,
                     help="at --gpus 1: form an RCCL (nccl) process group of world size 1 and run the per-layer "
                          "bucketed all-reduce anyway (exercises the N > 1 communication path on one GPU)")
+    ap.add_argument("--dp-single", type=int, default=0,
+                    help="N > 1: one all-reduce of the whole gradient buffer after the backward instead of per-layer "
+                         "buckets overlapped with it")
     ap.add_argument("--attribution", type=int, default=1,
                     help="host-enqueue and GPU-busy time per step, each over a region of its own")
     ap.add_argument("--cpu-baseline", type=int, default=1)
@@ -238,7 +241,8 @@ def main():
     from hgnn_amd.dp import GradAllReduce, LayerBucketAllReduce
     # N > 1: per-layer gradient buckets reduced on a communication stream while the executor's
     # backward is still running (its per-layer events), BN running statistics averaged
-    allreduce = (LayerBucketAllReduce(model, force=force_dp) if (world > 1 or force_dp) and not args.graph
+    allreduce = (LayerBucketAllReduce(model, force=force_dp, single=bool(args.dp_single))
+                 if (world > 1 or force_dp) and not args.graph
                  else GradAllReduce(params))
     last_out = [None]
 

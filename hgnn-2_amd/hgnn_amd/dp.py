@@ -140,8 +140,11 @@ class LayerBucketAllReduce:
     gradients into the flat buffer and all-reduces it in one collective after the backward.
     """
 
-    def __init__(self, model, group=None, sync_running=True, force=False):
+    def __init__(self, model, group=None, sync_running=True, force=False, single=False):
         self.model = model
+        # single: one collective over the whole buffer after the backward instead of one per layer (fewer host-side
+        # collective calls; no overlap with the backward)
+        self.single = single
         # force: run the bucketed collectives even in a group of one rank (an RCCL group of world size 1 on a
         # one-GPU box exercises the communication stream, the per-layer events and the RCCL kernels)
         self.force = force
@@ -242,7 +245,11 @@ class LayerBucketAllReduce:
             if run:
                 torch._foreach_copy_(self._tail_views(run), run)
         cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
-        if fresh or cur is None:
+        if self.single and cur is not None and not fresh:
+            # one collective on the caller's stream, after the backward it follows in stream order
+            pack_running()
+            dist.all_reduce(self.flat, op=op, group=self.group)
+        elif fresh or cur is None:
             # no per-layer events this step: one collective over the whole buffer after the backward
             if cur is not None:
                 self.comm.wait_stream(cur)

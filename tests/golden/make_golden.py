@@ -119,6 +119,25 @@ def gen_operators(out):
     print(f"operators: {len(graphs)} graphs, {time.time() - t0:.1f}s")
 
 
+def gen_operators_hij(out):
+    """J = 3, 4, 5 operators (slices up to A^16 / AL^16) of the QM9-shape graphs the large-J GPU tests use
+    (tests/test_gpu_net.py::test_large_J_vs_oracle_fp64: qm9_shape_dataset(32, seed=40 + J)), as the reference's
+    graph_operators (functions/operators.py:25-29, fp32 torch.matmul powers) computes them on this CPU: pins the
+    operator bits the network tests feed to the GPU (J >= 4 powers leave fp32's exact range, so their rounding
+    depends on the matmul's summation order)."""
+    t0 = time.time()
+    rec = {}
+    for J in (3, 4, 5):
+        graphs = dg.qm9_shape_dataset(32, seed=40 + J)
+        rec.update({f"J{J}.{k}": v for k, v in fu.pack_graphs(graphs).items()})
+        for k, (X, A, _t) in enumerate(graphs):
+            W, WL, Pm, Pd = r_ops.graph_operators([X, A], J, True)
+            rec[f"J{J}.W_{k}"] = W.numpy()
+            rec[f"J{J}.WL_{k}"] = WL.numpy()
+    np.savez_compressed(os.path.join(out, "operators_hij.npz"), **rec)
+    print(f"operators_hij: {time.time() - t0:.1f}s")
+
+
 def instances(graphs, J=1):
     data = []
     for X, A, t in graphs:

@@ -187,3 +187,34 @@ def _real_weight_check():
                 d = (WL[:, :, 3].double() - WLr[:, :, 3].double()).abs()
                 assert (d <= (ALa @ ALa) * M * 2.0 ** -24).all()
     return n_diff
+
+
+def test_high_j_operators_vs_reference_fixture():
+    """J = 3, 4, 5 operators against the reference's own graph_operators output (tests/golden/operators_hij.npz,
+    functions/operators.py:25-29, fp32 torch.matmul powers on the fixture machine's BLAS).  J = 3 (A^4) stays in
+    fp32's exact range for these weights: bit-exact.  J >= 4 (A^8, A^16) leaves it, so the reference's bits depend
+    on its BLAS's summation order; the builder rounds each power once from an fp64 accumulation (the correctly
+    rounded square of its fp32 input).  Measured: J = 4 differs in 27 of 407 220 entries (26 by 1 ulp, one by 2);
+    J = 5 (A^16, squared from the already rounded A^8) in 8 556 of 652 267, by 1-6 ulp.  The restated
+    oracle (oracle/ref_mnb.py, torch.matmul like the reference) is bit-exact at every J."""
+    import os
+
+    import fixture_util as fu
+    from functions.operators import graph_operators
+    GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    z = np.load(os.path.join(GOLD, "operators_hij.npz"))
+    for J, max_diff, max_ulp in ((3, 0, 0), (4, 64, 2), (5, 12000, 8)):
+        gs = fu.unpack_graphs(z, f"J{J}.")
+        nd = 0
+        for k, (X, A, _t) in enumerate(gs):
+            W, WL, _, _ = graph_operators([X, A], J, True)
+            Wo, WLo, _, _ = R.graph_operators([X, A], J, True)
+            for got, orc, key in ((W, Wo, f"J{J}.W_{k}"), (WL, WLo, f"J{J}.WL_{k}")):
+                ref = torch.from_numpy(z[key])
+                assert torch.equal(orc, ref), (J, key)
+                d = got != ref
+                nd += int(d.sum())
+                if d.any():
+                    ulps = (got[d].view(torch.int32).long() - ref[d].view(torch.int32).long()).abs()
+                    assert int(ulps.max()) <= max_ulp, (J, key, int(ulps.max()))
+        assert nd <= max_diff, (J, nd)

@@ -120,7 +120,11 @@ def test_gnn_simple_j2_vs_oracle():
     # outputs reach |y| = 412 here (SBM-50, A^2 slice): measured |gpu - ref64| = 1.33e-3 against the
     # reference fp32's own 5.2e-4 (3.2e-6 vs 1.3e-6 relative), inside the first leg (1e-5 relative) but
     # 2.6x the reference's error, so the fp64 leg is held at 3x here (re-measured round 5: 1.34x the
-    # strict 2x bound, profiles/r05_parity_margins.jsonl -- this relaxation stays)
+    # strict 2x bound, profiles/r05_parity_margins.jsonl).  Where it enters (round 6,
+    # tools/parity_order_spread.py -> profiles/r06_parity_order_spread.txt): the reference's OWN fp32 error on
+    # these graphs moves 0.53x-3.07x (median 1.08x) with a mere relabelling of the nodes -- the same function,
+    # only the order of the graph_oper / BN sums changed -- 3 of 12 relabellings above 2x: the summation order
+    # of the aggregation sets it, not a kernel, so the 3x leg stays
     _check(model, b, 6, 0, kind="simple", factor=3.0)
 
 
