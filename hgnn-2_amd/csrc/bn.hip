@@ -42,6 +42,31 @@ __global__ void __launch_bounds__(256) k_bn_finalize(BnFwdArgs a) {
         return;
     }
     const int rows = *a.count;
+    if (a.acc) {
+        // the forward GEMM's fp64 atomic sums (copies summed in copy order): mean = S / N, var = Q / N - mean^2 in fp64
+        // (every y^2 exact in fp64, the sums carry ~1e-16 relative), then the same rounding to float as below
+        if (lane == 0) {
+            double S = 0.0, Q = 0.0;
+#pragma unroll
+            for (int q = 0; q < BN_ACC_COPIES; ++q) {
+                S += a.acc[((long long)q * 2 + 0) * a.c + ch];
+                Q += a.acc[((long long)q * 2 + 1) * a.c + ch];
+            }
+            const double N = (double)rows;
+            const double mean = N > 0.0 ? S / N : 0.0;
+            const double var = 1e-5 + (N > 0.0 ? fmax(Q / N - mean * mean, 0.0) : 0.0);
+            const float mf = (float)mean;
+            const float sf = (float)sqrt(var);
+            a.mean[ch] = mf;
+            a.std[ch] = sf;
+            if (a.run_mean) {
+                const float m1 = 1.0f - a.momentum;
+                a.run_mean[ch] = __fadd_rn(__fmul_rn(m1, mf), __fmul_rn(a.momentum, a.run_mean[ch]));
+                a.run_std[ch] = __fadd_rn(__fmul_rn(m1, sf), __fmul_rn(a.momentum, a.run_std[ch]));
+            }
+        }
+        return;
+    }
     const int tiles = ceil_div(rows, 64);
     constexpr int U = 8;
     // two passes over the tile partials (count, mean, M2) held in registers (one load round up to 512 tiles;
@@ -269,8 +294,25 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
             for (int q = 0; q < RG; ++q) t += f4c(red[j][q * L + l], comp);
             f4c(t4, j) = t;
         }
-        *reinterpret_cast<float4*>(a.part + bn_bwd_part_index(ch, tile, bn_bwd_tiles(a.cap_rows))) = t4;
+        if (a.acc64) {
+            // the tile's four sums into copy tile % BN_ACC_COPIES, [copy][j][c]: a wave's lanes add 64 consecutive
+            // doubles (no-return atomics, performed at the memory side; the kernel boundary orders them for apply4)
+            double* dst = a.acc64 + (long long)(tile % BN_ACC_COPIES) * 4 * a.c + ch;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) atomicAdd(dst + (long long)j * a.c, (double)f4c(t4, j));
+        } else {
+            *reinterpret_cast<float4*>(a.part + bn_bwd_part_index(ch, tile, bn_bwd_tiles(a.cap_rows))) = t4;
+        }
     }
+}
+
+// The per-channel statistics of the atomic path: the BN_ACC_COPIES copies of stat j summed in copy order (fixed), as
+// k_bn_bwd_fin rounds its fp64 total to the float it stores
+__device__ __forceinline__ float bn_acc_stat(const double* acc, int c, int j, int ch) {
+    double v = 0.0;
+#pragma unroll
+    for (int q = 0; q < BN_ACC_COPIES; ++q) v += acc[((long long)q * 4 + j) * c + ch];
+    return (float)v;
 }
 
 __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
@@ -278,12 +320,26 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
     const int total = *a.total_rows;
     const float wv = *a.w;
     const float inv_n = total > 0 ? 1.0f / (float)total : 0.f;
+    // atomic path: the statistics m1 / m2 of every channel from the accumulator copies, once per block into LDS
+    __shared__ float sm12[2][1024];
+    if (a.acc64) {
+        for (int ch = threadIdx.x; ch < a.c; ch += blockDim.x) {
+            sm12[0][ch] = bn_acc_stat(a.acc64, a.c, 0, ch);
+            sm12[1][ch] = bn_acc_stat(a.acc64, a.c, 1, ch);
+        }
+        // the next half's accumulators (its part4 runs after this kernel): zeroed for it
+        if (a.acc64_zero)
+            for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < bn_acc_doubles(a.c);
+                 i += (long long)gridDim.x * blockDim.x)
+                a.acc64_zero[i] = 0.0;
+        __syncthreads();
+    }
     if (blockIdx.x == 0) {
         __shared__ double redd[4];
         double t1 = 0.0, t2 = 0.0;
         for (int ch = threadIdx.x; ch < a.c; ch += blockDim.x) {
-            t1 += (double)a.sums[ch * 4 + 2];
-            t2 += (double)a.sums[ch * 4 + 3];
+            t1 += (double)(a.acc64 ? bn_acc_stat(a.acc64, a.c, 2, ch) : a.sums[ch * 4 + 2]);
+            t2 += (double)(a.acc64 ? bn_acc_stat(a.acc64, a.c, 3, ch) : a.sums[ch * 4 + 3]);
         }
         const double T1 = block_sum_d(t1, redd);
         const double T2 = block_sum_d(t2, redd);
@@ -307,8 +363,8 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
             const int ch = 4 * lane + i;
             mu[i] = a.mean[ch];
             isd[i] = 1.0f / a.std[ch];
-            m1[i] = a.sums[ch * 4 + 0] * inv_n;
-            m2[i] = a.sums[ch * 4 + 1] * inv_n;
+            m1[i] = (a.acc64 ? sm12[0][ch] : a.sums[ch * 4 + 0]) * inv_n;
+            m2[i] = (a.acc64 ? sm12[1][ch] : a.sums[ch * 4 + 1]) * inv_n;
             relu[i] = ch >= a.relu_from;
         }
         auto one = [&](long long i, float4 yv, float4 dz) {
@@ -909,6 +965,13 @@ static void bn2_launch(const BnBwdArgs& a, hipStream_t s) {
 
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     const int tiles = bn_bwd_tiles(a.cap_rows);
+    // the paths without the atomic statistics still hand the next half a zeroed accumulator region
+    const bool acc_path = a.acc64 && bn_vec4(a) && (a.ldy == 0 || a.ldy == a.c) && apply && a.c <= 1024 &&
+                          !(bn2_enabled() && ceil_div(a.cap_rows, BN2_ROWS) <= 192 && (a.c == 4 || a.c == 8 || a.c == 16)) &&
+                          !(bn2_wide_enabled() && ceil_div(a.cap_rows, BN2_ROWS) <= 192 &&
+                            (a.c == 64 || a.c == 128 || a.c == 256));
+    if (a.acc64_zero && !acc_path)
+        HGNN_HOST_CHECK(hipMemsetAsync(a.acc64_zero, 0, (size_t)bn_acc_doubles(a.c) * sizeof(double), s));
     if (a.ldy != 0 && a.ldy < a.c) return HGNN_ERR_ARG;
     // a padded dY stride is written by the scalar apply only
     const bool v4 = bn_vec4(a) && (a.ldy == 0 || a.ldy == a.c);
@@ -932,15 +995,23 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
         return 0;
     }
     BnBwdArgs as = a;  // a stamp slot per launch (stamp-mode clock only)
+    // the atomic statistics (acc64): part4 -> apply4, no k_bn_bwd_fin
+    const bool acc = a.acc64 && v4 && apply && a.c <= 1024;
+    if (!acc) {
+        as.acc64 = nullptr;
+        as.acc64_zero = nullptr;
+    }
     if (tiles > 0) {
         as.stamps = v4 ? clock_stamps((long long)tiles * 4) : nullptr;
         if (v4) HGNN_KLAUNCH(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, as);
         else HGNN_KLAUNCH(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
     }
     HGNN_LAUNCH_CHECK();
-    as.stamps = clock_stamps((long long)ceil_div(a.c, 4) * 4);
-    HGNN_KLAUNCH(k_bn_bwd_fin, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, as);
-    HGNN_LAUNCH_CHECK();
+    if (!acc) {
+        as.stamps = clock_stamps((long long)ceil_div(a.c, 4) * 4);
+        HGNN_KLAUNCH(k_bn_bwd_fin, dim3(ceil_div(a.c, 4)), dim3(256), 0, s, as);
+        HGNN_LAUNCH_CHECK();
+    }
     if (!apply) return 0;
     as.stamps = v4 ? clock_stamps((long long)(tiles > 0 ? tiles : 1) * 4) : nullptr;
     if (v4) HGNN_KLAUNCH(k_bn_bwd_apply4, dim3(tiles > 0 ? tiles : 1), dim3(256), 0, s, as);

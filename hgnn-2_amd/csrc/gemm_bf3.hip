@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
                                                        const int* __restrict__ m_valid, int m_cap, int N, int K,
                                                        float* __restrict__ Y, int ldy, const float* __restrict__ bias,
                                                        int relu_from, float* __restrict__ bn_part,
-                                                       uint64_t* stamps, DiagIdArgs id) {
+                                                       uint64_t* stamps, DiagIdArgs id, double* __restrict__ bn_acc) {
     WaveStamp stamp(stamps);
     __shared__ __attribute__((aligned(16))) char lds[2 * G_STAGE];
     __shared__ float bn_mu[256], bn_sc[256];  // diagonal I / D columns: BN of x per channel
@@ -161,6 +161,7 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
     const bool relu = gn >= relu_from;
     float sm = 0.f;
     int cnt = 0;
+    double s1 = 0.0, s2 = 0.0;  // bn_acc: fp64 sums of y and y^2 (each y^2 exact in fp64)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int gm = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -171,7 +172,29 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
             if (gn < N) Y[(long long)gm * ldy + gn] = v;
             sm += v;
             ++cnt;
+            if (bn_acc) {
+                s1 += (double)v;
+                s2 = fma((double)v, (double)v, s2);
+            }
         }
+    }
+    if (bn_acc) {
+        // the tile's column sums: the two 32-lane halves (shuffle), the two row halves of the block (LDS), then one
+        // no-return fp64 atomic per column and statistic into copy bx % BN_ACC_COPIES (spreads the adders)
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        double* redd = reinterpret_cast<double*>(lds);  // free: the main loop ended with a barrier
+        if (lane < 32 && wm == 1) {
+            redd[col] = s1;
+            redd[G_BN + col] = s2;
+        }
+        __syncthreads();
+        if (lane < 32 && wm == 0 && gn < N) {
+            double* dst = bn_acc + (long long)(bx % BN_ACC_COPIES) * 2 * N + gn;
+            atomicAdd(dst, s1 + redd[col]);
+            atomicAdd(dst + N, s2 + redd[G_BN + col]);
+        }
+        return;
     }
     if (!bn_part) return;
     sm += __shfl_xor(sm, 32, 64);
@@ -542,7 +565,7 @@ int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, i
 
 int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
                         int ldb, int n, const float* bias, int relu_from, float* y, int ldy, float* bn_part,
-                        hipStream_t s, const DiagIdArgs* id) {
+                        hipStream_t s, const DiagIdArgs* id, double* bn_acc) {
     if (m_cap <= 0 || n <= 0) return 0;
     const int kx = id ? 2 * id->c : 0;
     if (id && !diag_id_ok(id, k)) return HGNN_ERR_UNSUPPORTED;
@@ -556,10 +579,10 @@ int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, 
     const DiagIdArgs none{};
     if (id)
         HGNN_KLAUNCH(k_gemm_bf3_fwd<true>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, bias,
-                     relu_from, bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)), *id);
+                     relu_from, bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)), *id, bn_acc);
     else
         HGNN_KLAUNCH(k_gemm_bf3_fwd<false>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, bias,
-                     relu_from, bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)), none);
+                     relu_from, bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)), none, bn_acc);
     HGNN_LAUNCH_CHECK();
     return 0;
 }

@@ -28,6 +28,8 @@ struct BatchMeta {
     int* edge_off;   // (bs + 1) packed edge row offsets
     int* totals;     // [0] = total nodes, [1] = total edge slots
     uint32_t* err;   // validation bits (ERR_*)
+    double* zero64 = nullptr;  // optional: a region the first kernel of the forward zeroes (k_plan block 0)
+    int zero64_n = 0;          //   (the BN-backward statistics accumulators, BnBwdArgs::acc64)
 };
 
 struct RepackTable;
@@ -177,9 +179,11 @@ struct DiagIdArgs {
 int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
                        int ldb, int n, float* y, int ldy, hipStream_t s);
 // (id: the diagonal I / D columns, k counts them; null = none)
+// (bn_acc: the BN statistics as fp64 atomic sums [BN_ACC_COPIES][2][n] (sum y, sum y^2, zero on entry) instead of the
+// per-tile partials bn_part)
 int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
                         int ldb, int n, const float* bias, int relu_from, float* y, int ldy, float* bn_part,
-                        hipStream_t s, const DiagIdArgs* id = nullptr);
+                        hipStream_t s, const DiagIdArgs* id = nullptr, double* bn_acc = nullptr);
 // The dW GEMM (launch_gemm3_dw's contract) on bf16 MFMA through the same three-way split (id: as the forward's,
 // for the aggregate operand)
 int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const int* r_valid, int r_cap, int o,
@@ -334,6 +338,8 @@ int launch_dw_reduce2(const float* slabs, const int* r_valid, int nz, int o, int
 
 // ---------------------------------------------------------------- BN
 struct BnFwdArgs {
+    const double* acc;     // optional: the forward GEMM's fp64 atomic sums [BN_ACC_COPIES][2][c] (sum y, sum y^2); else
+                           // part
     const float* part;     // [tiles][c][3]
     int tiles, c;
     const int* count;      // device: total real rows (sum N_batch / E_batch)
@@ -371,8 +377,16 @@ struct BnBwdArgs {
     float* dw;             // scalar out
     float* db;             // scalar out
     float* dbpart;         // optional out: per-64-row-tile column sums of dy [tiles][c]
+    // optional (the float4 part4 / apply4 path): the statistics go by fp64 atomics into acc64 (BN_ACC_COPIES copies
+    // [copy][4][c], zero on entry; copy = tile % BN_ACC_COPIES spreads the adders) instead of per-tile partials
+    // summed by k_bn_bwd_fin -- apply4 reads the copies in a fixed order -- and apply4 zeroes acc64_zero (the next
+    // half's region) for the call after it.  Other paths zero acc64_zero with a memset.
+    double* acc64;
+    double* acc64_zero;
     uint64_t* stamps;  // the launch's stamp slot under a stamp-mode clock (common.h WaveStamp), else null
 };
+constexpr int BN_ACC_COPIES = 8;
+__host__ __device__ inline long long bn_acc_doubles(int c) { return (long long)BN_ACC_COPIES * 4 * c; }
 // apply = 0: only the statistics (part + fin)
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply = 1);
 __host__ __device__ inline int bn_bwd_tiles(int cap_rows) { return (cap_rows + 63) / 64; }

@@ -43,6 +43,7 @@ struct Half {
     size_t a = 0, part = 0, mean = 0, stdv = 0;
     size_t wt = 0, wc = 0, bc = 0;  // repacked Conv1d-pair weights (repack.hip)
     size_t wc3 = 0;                 // Wcat as three bf16 planes [3][2d][bf3_ld(kp)] (split-bf16 forward GEMM)
+    size_t bnf = 0;                 // the forward GEMM's BN sums by fp64 atomics [BN_ACC_COPIES][2][2d] (HGNN_BN_ACC)
     size_t wt3 = 0;                 // WT as three bf16 planes [3][k][bf3_ld(c2p)] (split-bf16 dA GEMM)
 };
 
@@ -64,6 +65,8 @@ struct Program {
     size_t rows[S_COUNT] = {}, ent[S_COUNT] = {};
     int entry_stride_w = 4;
     size_t da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0;
+    size_t bnb_acc[2] = {};  // BN-backward statistics accumulators (BnBwdArgs::acc64), ping-pong over the walk
+    size_t acc_end = 0;      // end of the accumulator run (bnb_acc[0] .. the halves' bnf)
     int nbuf = 0;  // ring length: min(halves, BWD_NBUF)
     size_t dyk[BWD_NBUF] = {}, dbk[BWD_NBUF] = {}, dak[BWD_NBUF] = {};
     size_t bytes = 0;
@@ -301,6 +304,11 @@ Program build_program(const hgnn_net_config* c) {
     P.da = B.take(max_da * sizeof(float));  // dA of the halves the side stream does not read, and the readout's
     P.slabs = B.take(max_slab * sizeof(float));
     P.bnb_part = B.take((size_t)bn_bwd_tiles(max_cap) * P.c2 * 4 * sizeof(float));
+    // the statistics accumulators, one contiguous run zeroed by the forward's first kernel: the backward's two
+    // ping-pong regions, then one forward region per half
+    for (int i = 0; i < 2; ++i) P.bnb_acc[i] = B.take((size_t)bn_acc_doubles(P.c2) * sizeof(double));
+    for (auto& h : P.halves) h.bnf = B.take((size_t)BN_ACC_COPIES * 2 * P.c2 * sizeof(double));
+    P.acc_end = B.top;
     P.bnb_sums = B.take((size_t)P.c2 * 4 * sizeof(float));
     P.rb_scratch = B.take(readout_bwd_scratch_bytes(c->dim_out, P.k_last));
     P.bytes = B.top;
@@ -554,6 +562,20 @@ static int side_stream(hipStream_t main_s, SideStream** out) {
 }
 
 static bool fwd_bf3(const Program& P) { return fwd_bf3_c2(P.c2); }
+// BN-backward statistics by fp64 atomics into accumulator copies, no k_bn_bwd_fin (round 6; HGNN_BN_ACC=0: the
+// per-tile partials and k_bn_bwd_fin).  The sums' order over the tiles is not fixed: the statistics can differ in the
+// last fp64 bits from run to run (a float flip of m1 / m2 once in ~1e9 values), where the fin path is bitwise
+// deterministic.
+static bool bn_acc_on() {
+    static const bool on = env_flag("HGNN_BN_ACC", true);
+    return on;
+}
+// The forward's first kernel zeroes both accumulator regions (k_plan; a CSR batch: the error word's memset)
+static void bn_acc_zero_meta(const Program& P, void* ws, BatchMeta& m) {
+    if (!bn_acc_on()) return;
+    m.zero64 = at<double>(ws, P.bnb_acc[0]);
+    m.zero64_n = (int)((P.acc_end - P.bnb_acc[0]) / sizeof(double));
+}
 // the dA GEMM on the split-bf16 kernel (k_gemm_bf3_fwd with a plain-store epilogue, B = WT's planes)
 static bool da_bf3(const Program& P) {
     static const bool on = env_flag("HGNN_DA_BF3", true);
@@ -599,7 +621,11 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
         }
     }
     size_t plan_tables = 0;
-    if (csr) HGNN_HOST_CHECK(hipMemsetAsync(m.err, 0, sizeof(uint32_t), s));  // dense inputs: k_plan zeroes it
+    bn_acc_zero_meta(P, ws, m);
+    if (csr) {  // dense inputs: k_plan zeroes both
+        HGNN_HOST_CHECK(hipMemsetAsync(m.err, 0, sizeof(uint32_t), s));
+        if (m.zero64) HGNN_HOST_CHECK(hipMemsetAsync(m.zero64, 0, (size_t)m.zero64_n * sizeof(double), s));
+    }
     if (!csr) {
     plan_tables = tables.empty() ? 0 : 1;
     TL(HGNN_K_STRUCT, launch_plan(in->d_N_batch, lg ? in->d_E_batch : nullptr, c->bs, c->nmax, lg ? c->emax : 0, m, s,
@@ -673,12 +699,14 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
         TL(HGNN_K_AGG_FWD, launch_agg_fwd(ag, s));
 
         const DiagIdArgs ida = diag_id_args(P, ws, prm, h);
+        // the BN statistics by fp64 atomics (split-bf16 forward GEMM, training)
+        double* bnf = fwd_bf3(P) && c->training && bn_acc_on() ? at<double>(ws, h.bnf) : nullptr;
         if (fwd_bf3(P))
             TL(HGNN_K_GEMM_FWD, launch_gemm_bf3_fwd(at<float>(ws, h.a), h.kpa, tot, cap, h.kp, at<__bf16>(ws, h.wc3),
                                                     (long long)P.c2 * bf3_ld(h.kp), bf3_ld(h.kp), P.c2,
                                                     at<float>(ws, h.bc), h.relu_from, at<float>(ws, P.feats[h.out].y),
                                                     P.c2, c->training ? at<float>(ws, h.part) : nullptr, s,
-                                                    h.id ? &ida : nullptr));
+                                                    h.id ? &ida : nullptr, bnf));
         else
             TL(HGNN_K_GEMM_FWD, launch_gemm3_fwd(at<float>(ws, h.a), h.kp, tot, cap, h.kp, at<float>(ws, h.wc), h.kp,
                                                  P.c2, at<float>(ws, h.bc), h.relu_from,
@@ -686,6 +714,7 @@ int net_forward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn_
                                                  c->training ? at<float>(ws, h.part) : nullptr, s, lg ? 1 : 0));
 
         BnFwdArgs bf{};
+        bf.acc = bnf;
         bf.part = at<float>(ws, h.part);
         bf.tiles = gemm_fwd_tiles_m(cap);
         bf.c = P.c2;
@@ -890,6 +919,10 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
     // each mid-backward join idles the main stream.)
     bool pending[BWD_NBUF] = {};
     int slot = 0, q = 0;
+    // the walk leaves region H % 2 zeroed; with an odd number of halves region 0 is not, so a second backward of
+    // the same forward (retain_graph) would meet the first one's sums: zeroed here
+    if (bn_acc_on() && P.halves.size() % 2 == 1)
+        HGNN_HOST_CHECK(hipMemsetAsync(at<double>(ws, P.bnb_acc[0]), 0, (size_t)bn_acc_doubles(P.c2) * sizeof(double), s));
     // HGNN_BWD_TAIL=0: the round-4 tail (the last half forks after its dA GEMM, dX unpacked after the join)
     static const bool bwd_tail = env_flag("HGNN_BWD_TAIL", true);
     // The side stream also takes the dense operator gradient (W.requires_grad) of a node
@@ -969,6 +1002,10 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         bb.db = grads[h.pbn_b];
         bb.dbpart = dbp;
         bb.ldy = P.c2p;
+        if (bn_acc_on()) {  // ping-pong: apply4 of this half zeroes the next half's region
+            bb.acc64 = at<double>(ws, P.bnb_acc[q % 2]);
+            bb.acc64_zero = at<double>(ws, P.bnb_acc[(q + 1) % 2]);
+        }
         const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
         const bool ndw = need_dw && !h.edge;
         TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s));

@@ -37,6 +37,7 @@ __global__ void __launch_bounds__(256) k_plan(const int64_t* __restrict__ nb,
         carry[1] = 0;
         *m.err = 0u;  // the call's validation word (this kernel is the first of the forward)
     }
+    for (int i = t; i < m.zero64_n; i += 256) m.zero64[i] = 0.0;
     __syncthreads();
     for (int base = 0; base < bs; base += 256) {
         const int i = base + t;
