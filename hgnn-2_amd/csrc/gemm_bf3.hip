@@ -35,7 +35,8 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
                                                        const int* __restrict__ m_valid, int m_cap, int N, int K,
                                                        float* __restrict__ Y, int ldy, const float* __restrict__ bias,
                                                        int relu_from, float* __restrict__ bn_part,
-                                                       uint64_t* stamps, DiagIdArgs id, double* __restrict__ bn_acc) {
+                                                       uint64_t* stamps, DiagIdArgs id, double* __restrict__ bn_acc,
+                                                       FwdBnFin fin) {
     WaveStamp stamp(stamps);
     __shared__ __attribute__((aligned(16))) char lds[2 * G_STAGE];
     __shared__ float bn_mu[256], bn_sc[256];  // diagonal I / D columns: BN of x per channel
@@ -47,6 +48,18 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
     const int L = blockIdx.x + gridDim.x * blockIdx.y, jj = L >> 3;
     const int by = jj % gridDim.y, bx = (L & 7) + 8 * (jj / gridDim.y);
     const int m0 = bx * G_BM, n0 = by * G_BN;
+    if (M <= 0 && fin.ticket && bn_acc && L == 0) {  // no rows: the finalize of empty statistics (k_bn_finalize's)
+        const float sf = (float)sqrt(1e-5);
+        for (int ch = threadIdx.x; ch < N; ch += G_NT) {
+            fin.mean[ch] = 0.f;
+            fin.std[ch] = sf;
+            if (fin.run_mean) {
+                const float m1 = 1.0f - fin.momentum;
+                fin.run_mean[ch] = __fadd_rn(__fmul_rn(m1, 0.f), __fmul_rn(fin.momentum, fin.run_mean[ch]));
+                fin.run_std[ch] = __fadd_rn(__fmul_rn(m1, sf), __fmul_rn(fin.momentum, fin.run_std[ch]));
+            }
+        }
+    }
     if (m0 >= M) return;
     // staging: A -- 64 rows x 4 chunks of 8 k, one chunk (two float4) per thread, split into the three
     // planes; B -- 3 planes x 64 rows x 4 chunks of 16 B, three per thread
@@ -189,11 +202,51 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
             redd[G_BN + col] = s2;
         }
         __syncthreads();
+        if (!fin.ticket) {
+            if (lane < 32 && wm == 0 && gn < N) {
+                double* dst = bn_acc + (long long)(bx % BN_ACC_COPIES) * 2 * N + gn;
+                atomicAdd(dst, s1 + redd[col]);
+                atomicAdd(dst + N, s2 + redd[G_BN + col]);
+            }
+            return;
+        }
+        // the finalize in the last block: returning atomics (performed before this block's ticket), the ticket, then the
+        // last block reads the sums back with returning atomics (never a stale cache line) and finishes every channel
+        __shared__ int last;
+        __shared__ double sink[G_NT];
+        double chk = 0.0;
         if (lane < 32 && wm == 0 && gn < N) {
             double* dst = bn_acc + (long long)(bx % BN_ACC_COPIES) * 2 * N + gn;
-            atomicAdd(dst, s1 + redd[col]);
-            atomicAdd(dst + N, s2 + redd[G_BN + col]);
+            chk += atomicAdd(dst, s1 + redd[col]);
+            chk += atomicAdd(dst + N, s2 + redd[G_BN + col]);
         }
+        sink[tid] = chk;
+        __syncthreads();
+        if (tid == 0) last = atomicAdd(fin.ticket, 1u) == (unsigned)(ceil_div(M, G_BM) * gridDim.y - 1);
+        __syncthreads();
+        if (!last) return;
+        for (int ch = tid; ch < N; ch += G_NT) {
+            double S = 0.0, Q = 0.0;
+#pragma unroll
+            for (int q = 0; q < BN_ACC_COPIES; ++q) {
+                S += atomicAdd(bn_acc + ((long long)q * 2 + 0) * N + ch, 0.0);
+                Q += atomicAdd(bn_acc + ((long long)q * 2 + 1) * N + ch, 0.0);
+            }
+            // k_bn_finalize's atomic form, bit for bit
+            const double Nr = (double)M;
+            const double mean = Nr > 0.0 ? S / Nr : 0.0;
+            const double var = 1e-5 + (Nr > 0.0 ? fmax(Q / Nr - mean * mean, 0.0) : 0.0);
+            const float mf = (float)mean;
+            const float sf = (float)sqrt(var);
+            fin.mean[ch] = mf;
+            fin.std[ch] = sf;
+            if (fin.run_mean) {
+                const float m1 = 1.0f - fin.momentum;
+                fin.run_mean[ch] = __fadd_rn(__fmul_rn(m1, mf), __fmul_rn(fin.momentum, fin.run_mean[ch]));
+                fin.run_std[ch] = __fadd_rn(__fmul_rn(m1, sf), __fmul_rn(fin.momentum, fin.run_std[ch]));
+            }
+        }
+        if (tid == 0) *fin.ticket = 0u;  // for the next half's GEMM (it follows this kernel's end)
         return;
     }
     if (!bn_part) return;
@@ -233,29 +286,51 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
 // k_gemm_bf3_fwd's tiles, LDS image and product order, but every stage's global loads are issued before the
 // first is used (clamped addresses, zeroed after, so no exec branch splits them): four stages of 12 MFMAs
 // per wave cannot hide a load round trip each, as the forward's one-stage-ahead prefetch asks.  Plain store.
-template <int NST>
+template <int NST, bool BNF>
 __global__ void __launch_bounds__(G_NT) k_gemm_bf3_da(const float* __restrict__ A, int lda,
                                                       const __bf16* __restrict__ B, long long pb, int ldb,
                                                       const int* __restrict__ m_valid, int m_cap, int N, int K,
-                                                      float* __restrict__ Y, int ldy, uint64_t* stamps) {
+                                                      float* __restrict__ Y, int ldy, uint64_t* stamps, DaBnArgs bn) {
     WaveStamp stamp(stamps);
     __shared__ __attribute__((aligned(16))) char lds[2 * G_STAGE];
+    __shared__ float4 tab[BNF ? 128 : 1];
     const int M = m_valid ? *m_valid : m_cap;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv >> 1, wn = wv & 1;
     const int L = blockIdx.x + gridDim.x * blockIdx.y, jj = L >> 3;  // (k_gemm_bf3_fwd's XCD mapping)
     const int by = jj % gridDim.y, bx = (L & 7) + 8 * (jj / gridDim.y);
     const int m0 = bx * G_BM, n0 = by * G_BN;
+    if constexpr (BNF) {
+        // the next half's BN-backward accumulators, zeroed for it (this GEMM runs after this half's statistics)
+        if (bn.zero)
+            for (long long i = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * G_NT + tid; i < bn.zero_n;
+                 i += (long long)gridDim.x * gridDim.y * G_NT)
+                bn.zero[i] = 0.0;
+    }
     if (m0 >= M) return;
     const int arow = tid >> 2, ach = tid & 3, gm = m0 + arow;
-    const float* ap = A + (long long)min(gm, M - 1) * lda;
-    float4 ra[NST][2];
+    // BNF: the A operand dY = BN-backward(dz, y) formed here from the statistics table (k_bn_bwd_part4t), as
+    // k_bn_bwd_apply4 forms it (bn_bwd_dy_inv, bit for bit); the blocks of the first column tile store it for the
+    // dW GEMM.  Otherwise A = dY.
+    float wvb = 0.f;
+    if constexpr (BNF) {
+        for (int c = tid; c < K; c += G_NT) tab[c] = bn.tab[c];
+        wvb = *bn.w;
+        __syncthreads();
+    }
+    const float* ap = (BNF ? bn.dz : A) + (long long)min(gm, M - 1) * lda;
+    const float* yp = BNF ? bn.y + (long long)min(gm, M - 1) * lda : nullptr;
+    float4 ra[NST][2], ry[BNF ? NST : 1][2];
     u32x4 rb[NST][3];
 #pragma unroll
     for (int t = 0; t < NST; ++t) {
         const int k = t * G_BK + 8 * ach;
         ra[t][0] = *reinterpret_cast<const float4*>(ap + min(k, K - 4));
         ra[t][1] = *reinterpret_cast<const float4*>(ap + min(k + 4, K - 4));
+        if constexpr (BNF) {
+            ry[t][0] = *reinterpret_cast<const float4*>(yp + min(k, K - 4));
+            ry[t][1] = *reinterpret_cast<const float4*>(yp + min(k + 4, K - 4));
+        }
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const int e = tid + G_NT * i, pl = e >> 8, row = (e & 255) >> 2, ch = e & 3;
@@ -267,9 +342,26 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_da(const float* __restrict__ 
         char* st = lds + buf * G_STAGE;
         const int k = t * G_BK + 8 * ach;
         const bool v0 = gm < M && k < K, v1 = gm < M && k + 4 < K;
-        const float xv[8] = {v0 ? ra[t][0].x : 0.f, v0 ? ra[t][0].y : 0.f, v0 ? ra[t][0].z : 0.f,
-                             v0 ? ra[t][0].w : 0.f, v1 ? ra[t][1].x : 0.f, v1 ? ra[t][1].y : 0.f,
-                             v1 ? ra[t][1].z : 0.f, v1 ? ra[t][1].w : 0.f};
+        float xv[8] = {v0 ? ra[t][0].x : 0.f, v0 ? ra[t][0].y : 0.f, v0 ? ra[t][0].z : 0.f,
+                       v0 ? ra[t][0].w : 0.f, v1 ? ra[t][1].x : 0.f, v1 ? ra[t][1].y : 0.f,
+                       v1 ? ra[t][1].z : 0.f, v1 ? ra[t][1].w : 0.f};
+        if constexpr (BNF) {
+            const float yv[8] = {ry[t][0].x, ry[t][0].y, ry[t][0].z, ry[t][0].w,
+                                 ry[t][1].x, ry[t][1].y, ry[t][1].z, ry[t][1].w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int ch = min(k + e, K - 1);
+                const float4 tb = tab[ch];
+                xv[e] = (e < 4 ? v0 : v1) ? bn_bwd_dy_inv(yv[e], xv[e], tb.x, tb.y, wvb, tb.z, tb.w, bn.training != 0,
+                                                          ch >= bn.relu_from)
+                                          : 0.f;
+            }
+            if (by == 0 && gm < M) {  // dY for the dW GEMM (row stride ldy_dy)
+                float* q = bn.dy + (long long)gm * bn.ldy + k;
+                if (v0) *reinterpret_cast<float4*>(q) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+                if (v1) *reinterpret_cast<float4*>(q + 4) = make_float4(xv[4], xv[5], xv[6], xv[7]);
+            }
+        }
         bf16x8 p0, p1, p2;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -544,8 +636,12 @@ int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const
 }
 
 int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
-                       int ldb, int n, float* y, int ldy, hipStream_t s) {
+                       int ldb, int n, float* y, int ldy, hipStream_t s, const DaBnArgs* bn) {
     if (m_cap <= 0 || n <= 0) return 0;
+    if (bn && (!bn->dz || !bn->y || !bn->tab || !bn->w || !bn->dy || bn->ldy % 4 || bn->ldy < k || k % 8 ||
+               (reinterpret_cast<uintptr_t>(bn->dz) & 15) || (reinterpret_cast<uintptr_t>(bn->y) & 15) ||
+               (reinterpret_cast<uintptr_t>(bn->dy) & 15) || k > 128))
+        return HGNN_ERR_UNSUPPORTED;
     if (k < 4 || k > 4 * G_BK || lda % 4 || k % 4 || ldb % 8 || pb % 8 || k > lda || bf3_ld(k) > ldb ||
         (reinterpret_cast<uintptr_t>(a) & 15) || (reinterpret_cast<uintptr_t>(b) & 15))
         return HGNN_ERR_UNSUPPORTED;
@@ -553,20 +649,30 @@ int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, i
     const int gx = ceil_div(ceil_div(m_cap, G_BM), 8) * 8;
     const dim3 g(gx, ceil_div(n, G_BN));
     uint64_t* st = clock_stamps((long long)g.x * g.y * (G_NT / 64));
-    switch (ceil_div(k, G_BK)) {
-        case 1: HGNN_KLAUNCH(k_gemm_bf3_da<1>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
-        case 2: HGNN_KLAUNCH(k_gemm_bf3_da<2>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
-        case 3: HGNN_KLAUNCH(k_gemm_bf3_da<3>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
-        default: HGNN_KLAUNCH(k_gemm_bf3_da<4>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
+    const DaBnArgs none{};
+    const DaBnArgs& bb = bn ? *bn : none;
+#define HGNN_DA_LAUNCH(NS, F) \
+    HGNN_KLAUNCH((k_gemm_bf3_da<NS, F>), g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st, bb)
+    switch (ceil_div(k, G_BK) * 2 + (bn ? 1 : 0)) {
+        case 2: HGNN_DA_LAUNCH(1, false); break;
+        case 3: HGNN_DA_LAUNCH(1, true); break;
+        case 4: HGNN_DA_LAUNCH(2, false); break;
+        case 5: HGNN_DA_LAUNCH(2, true); break;
+        case 6: HGNN_DA_LAUNCH(3, false); break;
+        case 7: HGNN_DA_LAUNCH(3, true); break;
+        case 9: HGNN_DA_LAUNCH(4, true); break;
+        default: HGNN_DA_LAUNCH(4, false); break;
     }
+#undef HGNN_DA_LAUNCH
     HGNN_LAUNCH_CHECK();
     return 0;
 }
 
 int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
                         int ldb, int n, const float* bias, int relu_from, float* y, int ldy, float* bn_part,
-                        hipStream_t s, const DiagIdArgs* id, double* bn_acc) {
+                        hipStream_t s, const DiagIdArgs* id, double* bn_acc, const FwdBnFin* fin) {
     if (m_cap <= 0 || n <= 0) return 0;
+    if (fin && (!bn_acc || !fin->mean || !fin->std || !fin->ticket)) return HGNN_ERR_ARG;
     const int kx = id ? 2 * id->c : 0;
     if (id && !diag_id_ok(id, k)) return HGNN_ERR_UNSUPPORTED;
     if (lda % 4 || k % 4 || ldb % 8 || pb % 8 || k - kx > lda || bf3_ld(k) > ldb ||
@@ -577,12 +683,14 @@ int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, 
     const int gx = ceil_div(ceil_div(m_cap, G_BM), 8) * 8;
     const dim3 g(gx, ceil_div(n, G_BN));
     const DiagIdArgs none{};
+    const FwdBnFin nofin{};
+    const FwdBnFin& fb = fin ? *fin : nofin;
     if (id)
         HGNN_KLAUNCH(k_gemm_bf3_fwd<true>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, bias,
-                     relu_from, bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)), *id, bn_acc);
+                     relu_from, bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)), *id, bn_acc, fb);
     else
         HGNN_KLAUNCH(k_gemm_bf3_fwd<false>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, bias,
-                     relu_from, bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)), none, bn_acc);
+                     relu_from, bn_part, clock_stamps((long long)g.x * g.y * (G_NT / 64)), none, bn_acc, fb);
     HGNN_LAUNCH_CHECK();
     return 0;
 }
