@@ -306,139 +306,6 @@ __global__ void __launch_bounds__(256) k_bn_bwd_part4(BnBwdArgs a) {
     }
 }
 
-// The table form of k_bn_bwd_part4 (BnBwdArgs::tab): seven sums per channel by fp64 atomics with return (so every add
-// is performed before the block takes its ticket), and the block that takes the last ticket finishes the statistics:
-// it reads the sums back with returning atomics (performed at the memory side, never a stale cache line), writes the
-// per-channel table, the BN scalar grads and the conv bias grads, and leaves the ticket at zero.
-__global__ void __launch_bounds__(256) k_bn_bwd_part4t(BnBwdArgs a) {
-    WaveStamp stamp(a.stamps);
-    const int tile = blockIdx.x;
-    const int total = *a.total_rows;
-    const int r0 = tile * 64;
-    if (total <= 0 && tile == 0) {  // no rows: nothing to finish but zero gradients (and an identity table)
-        for (int ch = threadIdx.x; ch < a.c; ch += 256) {
-            a.tab[ch] = make_float4(a.mean[ch], 1.0f / a.std[ch], 0.f, 0.f);
-            if (ch < a.split) {
-                if (a.db_lin) a.db_lin[ch] = 0.f;
-            } else if (a.db_relu) {
-                a.db_relu[ch - a.split] = 0.f;
-            }
-        }
-        if (threadIdx.x == 0) {
-            *a.dw = 0.f;
-            *a.db = 0.f;
-        }
-        return;
-    }
-    if (r0 >= total) return;
-    const int r1 = min(total, r0 + 64);
-    const float wv = *a.w;
-    const int L = a.c >> 2, RG = min(256 / L, 64);
-    const int lane = threadIdx.x % L, rg = threadIdx.x / L;
-    constexpr int NS = 7;
-    __shared__ float4 red[NS][256];
-    __shared__ double sink[256];
-    __shared__ int last;
-    float4 s[NS];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) s[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (rg < RG) {
-        float mu[4], isd[4];
-        bool relu[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            mu[i] = a.mean[4 * lane + i];
-            isd[i] = 1.0f / a.std[4 * lane + i];
-            relu[i] = 4 * lane + i >= a.relu_from;
-        }
-        auto acc = [&](float4 dz, float4 yv) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float y = f4c(yv, i);
-                const float h = (y - mu[i]) * isd[i];
-                const float d = f4c(dz, i);
-                const float g = wv * d;
-                const float r = (relu[i] && !(y > 0.f)) ? 0.f : 1.f;
-                f4c(s[0], i) += g;
-                f4c(s[1], i) = fmaf(g, h, f4c(s[1], i));
-                f4c(s[2], i) = fmaf(d, h, f4c(s[2], i));
-                f4c(s[3], i) += d;
-                f4c(s[4], i) = fmaf(r, g, f4c(s[4], i));
-                f4c(s[5], i) += r;
-                f4c(s[6], i) = fmaf(r, h, f4c(s[6], i));
-            }
-        };
-        int r = r0 + rg;
-        for (; r + 3 * RG < r1; r += 4 * RG) {
-            float4 dz[4], yv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const long long i = (long long)(r + u * RG) * a.c + 4 * lane;
-                dz[u] = ld4(a.dz + i);
-                yv[u] = ld4(a.y + i);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc(dz[u], yv[u]);
-        }
-        for (; r < r1; r += RG) {
-            const long long i = (long long)r * a.c + 4 * lane;
-            acc(ld4(a.dz + i), ld4(a.y + i));
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < NS; ++j) red[j][threadIdx.x] = s[j];
-    __syncthreads();
-    double chk = 0.0;
-    for (int ch = threadIdx.x; ch < a.c; ch += 256) {
-        const int l = ch >> 2, comp = ch & 3;
-        double* dst = a.acc64 + (long long)(tile % BN_ACC_COPIES) * BN_ACC_STATS * a.c + ch;
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            float t = 0.f;
-            for (int q = 0; q < RG; ++q) t += f4c(red[j][q * L + l], comp);
-            chk += atomicAdd(dst + (long long)j * a.c, (double)t);  // with return: performed before the ticket
-        }
-    }
-    sink[threadIdx.x] = chk;
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(a.ticket, 1u) == (unsigned)(ceil_div(total, 64) - 1);
-    __syncthreads();
-    if (!last) return;
-    // the last block: every other block's sums are in
-    const float inv_n = total > 0 ? 1.0f / (float)total : 0.f;
-    double t2 = 0.0, t3 = 0.0;
-    for (int ch = threadIdx.x; ch < a.c; ch += 256) {
-        double S[NS];
-#pragma unroll
-        for (int j = 0; j < NS; ++j) S[j] = 0.0;
-#pragma unroll
-        for (int q = 0; q < BN_ACC_COPIES; ++q)
-#pragma unroll
-            for (int j = 0; j < NS; ++j) S[j] += atomicAdd(a.acc64 + ((long long)q * BN_ACC_STATS + j) * a.c + ch, 0.0);
-        const float mu = a.mean[ch], isd = 1.0f / a.std[ch];
-        // m1 / m2 as k_bn_bwd_fin + apply4 round them: the float total times 1 / n in float
-        const float m1 = (float)S[0] * inv_n, m2 = (float)S[1] * inv_n;
-        a.tab[ch] = make_float4(mu, isd, m1, m2);
-        t2 += (double)(float)S[2];
-        t3 += (double)(float)S[3];
-        // sum over the rows of dY = r isd (g - m1 - h m2) (train) or r isd g (eval)
-        const double sb = a.training ? (double)isd * (S[4] - (double)m1 * S[5] - (double)m2 * S[6]) : (double)isd * S[4];
-        if (ch < a.split) {
-            if (a.db_lin) a.db_lin[ch] = (float)sb;
-        } else if (a.db_relu) {
-            a.db_relu[ch - a.split] = (float)sb;
-        }
-    }
-    __shared__ double redd[4];
-    const double T2 = block_sum_d(t2, redd);
-    const double T3 = block_sum_d(t3, redd);
-    if (threadIdx.x == 0) {
-        *a.dw = (float)T2;
-        *a.db = (float)T3;
-        *a.ticket = 0u;  // for the next half (its launch follows this kernel's end)
-    }
-}
-
 // The per-channel statistics of the atomic path: the BN_ACC_COPIES copies of stat j summed in copy order (fixed), as
 // k_bn_bwd_fin rounds its fp64 total to the float it stores
 __device__ __forceinline__ float bn_acc_stat(const double* acc, int c, int j, int ch) {
@@ -455,12 +322,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
     const float inv_n = total > 0 ? 1.0f / (float)total : 0.f;
     // atomic path: the statistics m1 / m2 of every channel from the accumulator copies, once per block into LDS
     __shared__ float sm12[2][1024];
-    if (a.tab) {  // the table form: statistics, scalar grads and bias grads came from part4t's last block
-        if (a.acc64_zero)
-            for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < bn_acc_doubles(a.c);
-                 i += (long long)gridDim.x * blockDim.x)
-                a.acc64_zero[i] = 0.0;
-    } else if (a.acc64) {
+    if (a.acc64) {
         for (int ch = threadIdx.x; ch < a.c; ch += blockDim.x) {
             sm12[0][ch] = bn_acc_stat(a.acc64, a.c, 0, ch);
             sm12[1][ch] = bn_acc_stat(a.acc64, a.c, 1, ch);
@@ -472,7 +334,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
                 a.acc64_zero[i] = 0.0;
         __syncthreads();
     }
-    if (blockIdx.x == 0 && !a.tab) {
+    if (blockIdx.x == 0) {
         __shared__ double redd[4];
         double t1 = 0.0, t2 = 0.0;
         for (int ch = threadIdx.x; ch < a.c; ch += blockDim.x) {
@@ -499,18 +361,10 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int ch = 4 * lane + i;
-            if (a.tab) {
-                const float4 t = a.tab[ch];
-                mu[i] = t.x;
-                isd[i] = t.y;
-                m1[i] = t.z;
-                m2[i] = t.w;
-            } else {
-                mu[i] = a.mean[ch];
-                isd[i] = 1.0f / a.std[ch];
-                m1[i] = (a.acc64 ? sm12[0][ch] : a.sums[ch * 4 + 0]) * inv_n;
-                m2[i] = (a.acc64 ? sm12[1][ch] : a.sums[ch * 4 + 1]) * inv_n;
-            }
+            mu[i] = a.mean[ch];
+            isd[i] = 1.0f / a.std[ch];
+            m1[i] = (a.acc64 ? sm12[0][ch] : a.sums[ch * 4 + 0]) * inv_n;
+            m2[i] = (a.acc64 ? sm12[1][ch] : a.sums[ch * 4 + 1]) * inv_n;
             relu[i] = ch >= a.relu_from;
         }
         auto one = [&](long long i, float4 yv, float4 dz) {
@@ -551,7 +405,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply4(BnBwdArgs a) {
             one(i, ld4(a.y + i), ld4(a.dz + i));
         }
     }
-    if (a.dbpart && !a.tab) {
+    if (a.dbpart) {
         red[threadIdx.x] = cs;
         __syncthreads();
         for (int ch = threadIdx.x; ch < a.c; ch += 256) {
@@ -1109,26 +963,13 @@ static void bn2_launch(const BnBwdArgs& a, hipStream_t s) {
     HGNN_KLAUNCH(k_bn_bwd_apply2<L>, dim3(t2), dim3(BN2_THREADS), 0, s, a);
 }
 
-// whether launch_bn_backward takes the table form (BnBwdArgs::tab) for these arguments
-bool bn_bwd_table_path(const BnBwdArgs& a, int apply) {
-    const bool v4 = bn_vec4(a) && (a.ldy == 0 || a.ldy == a.c);
-    const bool few = ceil_div(a.cap_rows, BN2_ROWS) <= 192;
-    if (apply && v4 && bn2_enabled() && few && bn_bwd_tiles(a.cap_rows) > 0 && (a.c == 4 || a.c == 8 || a.c == 16))
-        return false;
-    if (apply && v4 && bn_bwd_tiles(a.cap_rows) > 0 && bn2_wide_enabled() && few &&
-        (a.c == 64 || a.c == 128 || a.c == 256))
-        return false;
-    return a.acc64 && a.tab && a.ticket && v4 && a.c <= 1024 && bn_bwd_tiles(a.cap_rows) > 0;
-}
-
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     const int tiles = bn_bwd_tiles(a.cap_rows);
     // the paths without the atomic statistics still hand the next half a zeroed accumulator region
     const bool acc_path =
-        bn_bwd_table_path(a, apply) ||
-        (a.acc64 && bn_vec4(a) && (a.ldy == 0 || a.ldy == a.c) && apply && a.c <= 1024 &&
-         !(bn2_enabled() && ceil_div(a.cap_rows, BN2_ROWS) <= 192 && (a.c == 4 || a.c == 8 || a.c == 16)) &&
-         !(bn2_wide_enabled() && ceil_div(a.cap_rows, BN2_ROWS) <= 192 && (a.c == 64 || a.c == 128 || a.c == 256)));
+        a.acc64 && bn_vec4(a) && (a.ldy == 0 || a.ldy == a.c) && apply && a.c <= 1024 &&
+        !(bn2_enabled() && ceil_div(a.cap_rows, BN2_ROWS) <= 192 && (a.c == 4 || a.c == 8 || a.c == 16)) &&
+        !(bn2_wide_enabled() && ceil_div(a.cap_rows, BN2_ROWS) <= 192 && (a.c == 64 || a.c == 128 || a.c == 256));
     if (a.acc64_zero && !acc_path)
         HGNN_HOST_CHECK(hipMemsetAsync(a.acc64_zero, 0, (size_t)bn_acc_doubles(a.c) * sizeof(double), s));
     if (a.ldy != 0 && a.ldy < a.c) return HGNN_ERR_ARG;
@@ -1155,20 +996,14 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     }
     BnBwdArgs as = a;  // a stamp slot per launch (stamp-mode clock only)
     // the atomic statistics (acc64): part4 -> apply4, no k_bn_bwd_fin
-    const bool tabp = bn_bwd_table_path(a, apply);
-    const bool acc = tabp || (a.acc64 && v4 && apply && a.c <= 1024);
+    const bool acc = a.acc64 && v4 && apply && a.c <= 1024;
     if (!acc) {
         as.acc64 = nullptr;
         as.acc64_zero = nullptr;
     }
-    if (!tabp) {
-        as.tab = nullptr;
-        as.ticket = nullptr;
-    }
     if (tiles > 0) {
         as.stamps = v4 ? clock_stamps((long long)tiles * 4) : nullptr;
-        if (as.tab) HGNN_KLAUNCH(k_bn_bwd_part4t, dim3(tiles), dim3(256), 0, s, as);
-        else if (v4) HGNN_KLAUNCH(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, as);
+        if (v4) HGNN_KLAUNCH(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, as);
         else HGNN_KLAUNCH(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
     }
     HGNN_LAUNCH_CHECK();

@@ -286,51 +286,30 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
 // k_gemm_bf3_fwd's tiles, LDS image and product order, but every stage's global loads are issued before the
 // first is used (clamped addresses, zeroed after, so no exec branch splits them): four stages of 12 MFMAs
 // per wave cannot hide a load round trip each, as the forward's one-stage-ahead prefetch asks.  Plain store.
-template <int NST, bool BNF>
+template <int NST>
 __global__ void __launch_bounds__(G_NT) k_gemm_bf3_da(const float* __restrict__ A, int lda,
                                                       const __bf16* __restrict__ B, long long pb, int ldb,
                                                       const int* __restrict__ m_valid, int m_cap, int N, int K,
-                                                      float* __restrict__ Y, int ldy, uint64_t* stamps, DaBnArgs bn) {
+                                                      float* __restrict__ Y, int ldy, uint64_t* stamps) {
     WaveStamp stamp(stamps);
     __shared__ __attribute__((aligned(16))) char lds[2 * G_STAGE];
-    __shared__ float4 tab[BNF ? 128 : 1];
     const int M = m_valid ? *m_valid : m_cap;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv >> 1, wn = wv & 1;
     const int L = blockIdx.x + gridDim.x * blockIdx.y, jj = L >> 3;  // (k_gemm_bf3_fwd's XCD mapping)
     const int by = jj % gridDim.y, bx = (L & 7) + 8 * (jj / gridDim.y);
     const int m0 = bx * G_BM, n0 = by * G_BN;
-    if constexpr (BNF) {
-        // the next half's BN-backward accumulators, zeroed for it (this GEMM runs after this half's statistics)
-        if (bn.zero)
-            for (long long i = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * G_NT + tid; i < bn.zero_n;
-                 i += (long long)gridDim.x * gridDim.y * G_NT)
-                bn.zero[i] = 0.0;
-    }
     if (m0 >= M) return;
     const int arow = tid >> 2, ach = tid & 3, gm = m0 + arow;
-    // BNF: the A operand dY = BN-backward(dz, y) formed here from the statistics table (k_bn_bwd_part4t), as
-    // k_bn_bwd_apply4 forms it (bn_bwd_dy_inv, bit for bit); the blocks of the first column tile store it for the
-    // dW GEMM.  Otherwise A = dY.
-    float wvb = 0.f;
-    if constexpr (BNF) {
-        for (int c = tid; c < K; c += G_NT) tab[c] = bn.tab[c];
-        wvb = *bn.w;
-        __syncthreads();
-    }
-    const float* ap = (BNF ? bn.dz : A) + (long long)min(gm, M - 1) * lda;
-    const float* yp = BNF ? bn.y + (long long)min(gm, M - 1) * lda : nullptr;
-    float4 ra[NST][2], ry[BNF ? NST : 1][2];
+    const float* ap = A + (long long)min(gm, M - 1) * lda;
+    float4 ra[NST][2];
     u32x4 rb[NST][3];
 #pragma unroll
     for (int t = 0; t < NST; ++t) {
         const int k = t * G_BK + 8 * ach;
         ra[t][0] = *reinterpret_cast<const float4*>(ap + min(k, K - 4));
         ra[t][1] = *reinterpret_cast<const float4*>(ap + min(k + 4, K - 4));
-        if constexpr (BNF) {
-            ry[t][0] = *reinterpret_cast<const float4*>(yp + min(k, K - 4));
-            ry[t][1] = *reinterpret_cast<const float4*>(yp + min(k + 4, K - 4));
-        }
+
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const int e = tid + G_NT * i, pl = e >> 8, row = (e & 255) >> 2, ch = e & 3;
@@ -342,26 +321,9 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_da(const float* __restrict__ 
         char* st = lds + buf * G_STAGE;
         const int k = t * G_BK + 8 * ach;
         const bool v0 = gm < M && k < K, v1 = gm < M && k + 4 < K;
-        float xv[8] = {v0 ? ra[t][0].x : 0.f, v0 ? ra[t][0].y : 0.f, v0 ? ra[t][0].z : 0.f,
-                       v0 ? ra[t][0].w : 0.f, v1 ? ra[t][1].x : 0.f, v1 ? ra[t][1].y : 0.f,
-                       v1 ? ra[t][1].z : 0.f, v1 ? ra[t][1].w : 0.f};
-        if constexpr (BNF) {
-            const float yv[8] = {ry[t][0].x, ry[t][0].y, ry[t][0].z, ry[t][0].w,
-                                 ry[t][1].x, ry[t][1].y, ry[t][1].z, ry[t][1].w};
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int ch = min(k + e, K - 1);
-                const float4 tb = tab[ch];
-                xv[e] = (e < 4 ? v0 : v1) ? bn_bwd_dy_inv(yv[e], xv[e], tb.x, tb.y, wvb, tb.z, tb.w, bn.training != 0,
-                                                          ch >= bn.relu_from)
-                                          : 0.f;
-            }
-            if (by == 0 && gm < M) {  // dY for the dW GEMM (row stride ldy_dy)
-                float* q = bn.dy + (long long)gm * bn.ldy + k;
-                if (v0) *reinterpret_cast<float4*>(q) = make_float4(xv[0], xv[1], xv[2], xv[3]);
-                if (v1) *reinterpret_cast<float4*>(q + 4) = make_float4(xv[4], xv[5], xv[6], xv[7]);
-            }
-        }
+        const float xv[8] = {v0 ? ra[t][0].x : 0.f, v0 ? ra[t][0].y : 0.f, v0 ? ra[t][0].z : 0.f,
+                             v0 ? ra[t][0].w : 0.f, v1 ? ra[t][1].x : 0.f, v1 ? ra[t][1].y : 0.f,
+                             v1 ? ra[t][1].z : 0.f, v1 ? ra[t][1].w : 0.f};
         bf16x8 p0, p1, p2;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -636,12 +598,8 @@ int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const
 }
 
 int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
-                       int ldb, int n, float* y, int ldy, hipStream_t s, const DaBnArgs* bn) {
+                       int ldb, int n, float* y, int ldy, hipStream_t s) {
     if (m_cap <= 0 || n <= 0) return 0;
-    if (bn && (!bn->dz || !bn->y || !bn->tab || !bn->w || !bn->dy || bn->ldy % 4 || bn->ldy < k || k % 8 ||
-               (reinterpret_cast<uintptr_t>(bn->dz) & 15) || (reinterpret_cast<uintptr_t>(bn->y) & 15) ||
-               (reinterpret_cast<uintptr_t>(bn->dy) & 15) || k > 128))
-        return HGNN_ERR_UNSUPPORTED;
     if (k < 4 || k > 4 * G_BK || lda % 4 || k % 4 || ldb % 8 || pb % 8 || k > lda || bf3_ld(k) > ldb ||
         (reinterpret_cast<uintptr_t>(a) & 15) || (reinterpret_cast<uintptr_t>(b) & 15))
         return HGNN_ERR_UNSUPPORTED;
@@ -649,21 +607,12 @@ int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, i
     const int gx = ceil_div(ceil_div(m_cap, G_BM), 8) * 8;
     const dim3 g(gx, ceil_div(n, G_BN));
     uint64_t* st = clock_stamps((long long)g.x * g.y * (G_NT / 64));
-    const DaBnArgs none{};
-    const DaBnArgs& bb = bn ? *bn : none;
-#define HGNN_DA_LAUNCH(NS, F) \
-    HGNN_KLAUNCH((k_gemm_bf3_da<NS, F>), g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st, bb)
-    switch (ceil_div(k, G_BK) * 2 + (bn ? 1 : 0)) {
-        case 2: HGNN_DA_LAUNCH(1, false); break;
-        case 3: HGNN_DA_LAUNCH(1, true); break;
-        case 4: HGNN_DA_LAUNCH(2, false); break;
-        case 5: HGNN_DA_LAUNCH(2, true); break;
-        case 6: HGNN_DA_LAUNCH(3, false); break;
-        case 7: HGNN_DA_LAUNCH(3, true); break;
-        case 9: HGNN_DA_LAUNCH(4, true); break;
-        default: HGNN_DA_LAUNCH(4, false); break;
+    switch (ceil_div(k, G_BK)) {
+        case 1: HGNN_KLAUNCH(k_gemm_bf3_da<1>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
+        case 2: HGNN_KLAUNCH(k_gemm_bf3_da<2>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
+        case 3: HGNN_KLAUNCH(k_gemm_bf3_da<3>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
+        default: HGNN_KLAUNCH(k_gemm_bf3_da<4>, g, dim3(G_NT), 0, s, a, lda, b, pb, ldb, m_valid, m_cap, n, k, y, ldy, st); break;
     }
-#undef HGNN_DA_LAUNCH
     HGNN_LAUNCH_CHECK();
     return 0;
 }

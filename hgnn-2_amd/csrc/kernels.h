@@ -176,22 +176,8 @@ struct DiagIdArgs {
     const float2* diag;    // per row (v_0, v_1) of the diagonal entry (AggFwdArgs::diag)
     BnView bn;             // BN of the producer of x (mean != null)
 };
-// BN backward folded into the dA GEMM (k_bn_bwd_part4t's table): A = dY formed at staging from dz / y [M][lda] and
-// tab[k] = (mean, 1 / std, m1, m2) as k_bn_bwd_apply4 forms it; the first column tile's blocks store dY to dy [M][ldy]
-// (the dW GEMM's operand); zero / zero_n: the next half's BN accumulators, zeroed by the grid
-struct DaBnArgs {
-    const float* dz;
-    const float* y;
-    const float4* tab;
-    const float* w;
-    int relu_from, training;
-    float* dy;
-    int ldy;
-    double* zero;
-    long long zero_n;
-};
 int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, int k, const __bf16* b, long long pb,
-                       int ldb, int n, float* y, int ldy, hipStream_t s, const DaBnArgs* bn = nullptr);
+                       int ldb, int n, float* y, int ldy, hipStream_t s);
 // (id: the diagonal I / D columns, k counts them; null = none)
 // The BN finalize done by the forward GEMM's last block (ticket; zero on entry, left zero): mean / std of the 2d
 // channels from the fp64 sums and the running statistics update, as k_bn_finalize's atomic form computes them
@@ -408,24 +394,12 @@ struct BnBwdArgs {
     // half's region) for the call after it.  Other paths zero acc64_zero with a memset.
     double* acc64;
     double* acc64_zero;
-    // optional, with acc64 (the "table" form, k_bn_bwd_part4t): part4's blocks add seven sums per channel (the four
-    // statistics and, for the conv bias gradients, sum r g, sum r, sum r h with r = relu'), and the block that
-    // finishes last (ticket, zero on entry and left zero) turns them into tab[c] = (mean, 1 / std, m1, m2), the BN
-    // scalar grads dw / db and the conv bias grads db_lin[c < split], db_relu[c >= split] (= sum over the rows of dY,
-    // algebraically) -- dY itself is then formed where it is read (apply4 on the table, or the fused dA GEMM)
-    float4* tab;
-    unsigned* ticket;
-    float* db_lin;
-    float* db_relu;
-    int split;
     uint64_t* stamps;  // the launch's stamp slot under a stamp-mode clock (common.h WaveStamp), else null
 };
-constexpr int BN_ACC_COPIES = 8, BN_ACC_STATS = 8;  // (7 used by the table form, 4 otherwise)
+constexpr int BN_ACC_COPIES = 8, BN_ACC_STATS = 4;
 __host__ __device__ inline long long bn_acc_doubles(int c) { return (long long)BN_ACC_COPIES * BN_ACC_STATS * c; }
 // apply = 0: only the statistics (part + fin)
 int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply = 1);
-// whether launch_bn_backward takes the table form for these arguments (then the conv bias grads come from it)
-bool bn_bwd_table_path(const BnBwdArgs& a, int apply = 1);
 __host__ __device__ inline int bn_bwd_tiles(int cap_rows) { return (cap_rows + 63) / 64; }
 // k_bn_bwd_part / part4 -> k_bn_bwd_fin partials: float4 {sum g, sum g h, sum dz h, sum dz} per (channel,
 // 64-row tile), channel-major [c][tiles] so the fin's per-channel loads are contiguous over the tiles

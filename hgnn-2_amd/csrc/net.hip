@@ -66,9 +66,8 @@ struct Program {
     int entry_stride_w = 4;
     size_t da = 0, slabs = 0, bnb_part = 0, bnb_sums = 0, rb_scratch = 0;
     size_t bnb_acc[2] = {};  // BN-backward statistics accumulators (BnBwdArgs::acc64), ping-pong over the walk
-    size_t acc_end = 0;      // end of the accumulator run (bnb_acc[0] .. the halves' bnf, the ticket)
-    size_t bnb_ticket = 0, bnb_tab = 0;  // the table form of the BN backward (BnBwdArgs::tab / ticket)
-    size_t fwd_ticket = 0;               // the forward GEMM's last-block finalize (FwdBnFin)
+    size_t acc_end = 0;      // end of the accumulator run (bnb_acc[0] .. the halves' bnf, the forward ticket)
+    size_t fwd_ticket = 0;  // the forward GEMM's last-block finalize (FwdBnFin)
     int nbuf = 0;  // ring length: min(halves, BWD_NBUF)
     size_t dyk[BWD_NBUF] = {}, dbk[BWD_NBUF] = {}, dak[BWD_NBUF] = {};
     size_t bytes = 0;
@@ -310,10 +309,8 @@ Program build_program(const hgnn_net_config* c) {
     // ping-pong regions, then one forward region per half
     for (int i = 0; i < 2; ++i) P.bnb_acc[i] = B.take((size_t)bn_acc_doubles(P.c2) * sizeof(double));
     for (auto& h : P.halves) h.bnf = B.take((size_t)BN_ACC_COPIES * 2 * P.c2 * sizeof(double));
-    P.bnb_ticket = B.take(sizeof(unsigned));
     P.fwd_ticket = B.take(sizeof(unsigned));
     P.acc_end = B.top;
-    P.bnb_tab = B.take((size_t)P.c2 * sizeof(float4));
     P.bnb_sums = B.take((size_t)P.c2 * 4 * sizeof(float));
     P.rb_scratch = B.take(readout_bwd_scratch_bytes(c->dim_out, P.k_last));
     P.bytes = B.top;
@@ -575,20 +572,10 @@ static bool bn_acc_on() {
     static const bool on = env_flag("HGNN_BN_ACC", true);
     return on;
 }
-// the table form of the BN backward (BnBwdArgs::tab, k_bn_bwd_part4t; HGNN_BN_TAB=0: part4 + apply4 on the sums)
-static bool bn_tab_on() {
-    static const bool on = env_flag("HGNN_BN_TAB", false);
-    return on;
-}
 // the forward BN finalize in the forward GEMM's last block (FwdBnFin; HGNN_BN_FWD_FIN=0: k_bn_finalize): 1.093 vs
 // 1.106 ms median, five of five alternating pairs
 static bool bn_fwd_fin_on() {
     static const bool on = env_flag("HGNN_BN_FWD_FIN", true);
-    return on;
-}
-// the BN-backward apply folded into the dA GEMM's staging (DaBnArgs; HGNN_BN_FUSE_DA=0: k_bn_bwd_apply4 on the table)
-static bool bn_fuse_da_on() {
-    static const bool on = env_flag("HGNN_BN_FUSE_DA", true);
     return on;
 }
 // The forward's first kernel zeroes both accumulator regions (k_plan; a CSR batch: the error word's memset)
@@ -1036,23 +1023,11 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         if (bn_acc_on()) {  // ping-pong: apply4 of this half zeroes the next half's region
             bb.acc64 = at<double>(ws, P.bnb_acc[q % 2]);
             bb.acc64_zero = at<double>(ws, P.bnb_acc[(q + 1) % 2]);
-            if (bn_tab_on()) {  // the table form: statistics and bias grads finished by part4's last block
-                bb.tab = at<float4>(ws, P.bnb_tab);
-                bb.ticket = at<unsigned>(ws, P.bnb_ticket);
-                bb.db_lin = grads[h.pb_lin];
-                bb.db_relu = grads[h.pb_relu];
-                bb.split = P.d;
-            }
         }
 
         const bool ng = needs_grad(h.gin), np = needs_grad(h.pin);
         const bool ndw = need_dw && !h.edge;
-        // the apply folded into the dA GEMM (the table form, the split-bf16 dA at 2d <= 128, even 2d): part4t only here
-        const bool fused = bn_fuse_da_on() && da_bf3(P) && P.c2p == P.c2 && P.c2 % 8 == 0 && bn_bwd_table_path(bb, 0) &&
-                           (ng || np || ndw);
-        // the conv bias grads: from the table form (as launched), else the dW reduction sums apply4's tile partials
-        if (bn_bwd_table_path(bb, fused ? 0 : 1)) dbp = nullptr;
-        TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s, fused ? 0 : 1));
+        TL(HGNN_K_BN_BWD, launch_bn_backward(bb, s));
 
         if (!ng && !np && !ndw) {
             TRY(fork_dw(h, cap, tot, dyb, dbp, false, nullptr));
@@ -1063,26 +1038,11 @@ int net_backward(const hgnn_net_config* c, const hgnn_net_inputs* in, const hgnn
         float* da = at<float>(ws, ndw_side && P.dak[slot] ? P.dak[slot] : P.da);
         // the last half of the walk (no dense dW, which reads dA) forks before its dA GEMM: the side stream's
         // dW + reduce is the step's tail there, nothing on the main stream follows to overlap it
-        // (with the fused apply dY only exists once the dA GEMM has run: no early fork)
-        const bool early = side && hi == 0 && !ndw && bwd_tail && !fused;
+        const bool early = side && hi == 0 && !ndw && bwd_tail;
         if (early) TRY(fork_dw(h, cap, tot, dyb, dbp, false, nullptr));
-        DaBnArgs dbn{};
-        if (fused) {
-            dbn.dz = at<float>(ws, P.feats[h.out].grad);
-            dbn.y = at<float>(ws, P.feats[h.out].y);
-            dbn.tab = at<float4>(ws, P.bnb_tab);
-            dbn.w = prm[h.pbn_w];
-            dbn.relu_from = h.relu_from;
-            dbn.training = c->training;
-            dbn.dy = dyb;
-            dbn.ldy = P.c2p;
-            dbn.zero = bb.acc64_zero;
-            dbn.zero_n = bn_acc_doubles(P.c2);
-        }
         if (da_bf3(P))
-            TL(HGNN_K_GEMM_DA, launch_gemm_bf3_da(fused ? dbn.dz : dyb, fused ? P.c2 : P.c2p, tot, cap, P.c2p,
-                                                  at<__bf16>(ws, h.wt3), (long long)h.k * bf3_ld(P.c2p), bf3_ld(P.c2p),
-                                                  h.k, da, h.kp, s, fused ? &dbn : nullptr));
+            TL(HGNN_K_GEMM_DA, launch_gemm_bf3_da(dyb, P.c2p, tot, cap, P.c2p, at<__bf16>(ws, h.wt3),
+                                                  (long long)h.k * bf3_ld(P.c2p), bf3_ld(P.c2p), h.k, da, h.kp, s));
         else
             TL(HGNN_K_GEMM_DA, launch_gemm3_da(dyb, P.c2p, tot, cap, P.c2p, at<float>(ws, h.wt), P.c2p, h.k, da, h.kp,
                                                s));

@@ -34,9 +34,10 @@ GROUPS = {
                      "HGNN_FWD_G5": "0"},
     "alt_a": {"HGNN_DW_RING": "2", "HGNN_AGG_RPW": "1", "HGNN_BN_BWD2": "1", "HGNN_EXTRACT_REG": "0",
               "HGNN_DWD_GRID": "0", "HGNN_BWD_TAIL": "0", "HGNN_EVENT_FENCE": "1", "HGNN_READOUT_ROW": "0",
-              "HGNN_SERIAL_BWD": "1", "HGNN_DW_NARROW": "0"},
+              "HGNN_SERIAL_BWD": "1", "HGNN_DW_NARROW": "0", "HGNN_BN_ACC": "0"},
     "alt_b": {"HGNN_DW_RING": "3", "HGNN_AGG_RPW": "4", "HGNN_SIDE": "0", "HGNN_EXTRACT_REG": "0",
-              "HGNN_EXTRACT_LDS": "0", "HGNN_BN_BWD2": "0", "HGNN_EXEC_GRAPH": "0", "HGNN_EXTRACT_SPLIT": "1"},
+              "HGNN_EXTRACT_LDS": "0", "HGNN_BN_BWD2": "0", "HGNN_EXEC_GRAPH": "0", "HGNN_EXTRACT_SPLIT": "1",
+              "HGNN_BN_FWD_FIN": "0"},
 }
 
 
