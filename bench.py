@@ -31,6 +31,30 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "hgnn-2_amd"))
 sys.path.insert(0, REPO)
 
+
+def _dp_hw_queues():
+    """With a process group (N > 1, or --force-dp 1), at least 8 hardware queues per process (set before HIP starts).
+    The HIP runtime maps a process's streams round-robin onto GPU_MAX_HW_QUEUES queues (4 by default); the streams of
+    an RCCL process group then push the executor's weight-gradient side stream onto the main stream's queue, which
+    serialises the two: 1.31-1.33 vs 1.06-1.09 ms per step with an idle group at 4 vs 8 queues (tools/dp_ab.py,
+    DESIGN.md §8 round 6).  The N = 1 run keeps the box's setting."""
+    argv = " ".join(sys.argv[1:])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    gpus = 1
+    for i, a in enumerate(sys.argv):
+        if a == "--gpus" and i + 1 < len(sys.argv):
+            gpus = int(sys.argv[i + 1])
+        elif a.startswith("--gpus="):
+            gpus = int(a.split("=", 1)[1])
+    force = "--force-dp 1" in argv or "--force-dp=1" in argv
+    if world > 1 or gpus > 1 or force:
+        cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+        if cur < 8:
+            os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
+
+_dp_hw_queues()
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -536,6 +560,7 @@ def main():
             "collective": ("rccl" if backend == "nccl" else backend) if (world > 1 or force_dp) else None,
         },
         "rank_ms_per_step": rank_ms,
+        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
         "comm": comm,
         "attribution": attribution,
         "roofline": roof,

@@ -542,6 +542,9 @@ static int side_stream(hipStream_t main_s, SideStream** out) {
             for (int i = 0; i <= BWD_NBUF; ++i) (void)hipEventDestroy(ss.join[i]);
         }
         ss = SideStream{};
+        // (the HIP runtime maps a process's streams round-robin onto GPU_MAX_HW_QUEUES hardware queues: with an RCCL
+        // process group's streams this one can land on the main stream's queue and run serialised with it -- 8 queues
+        // avoid it; a high- or low-priority side stream made the host's launches slow, round 6)
         HGNN_HOST_CHECK(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
         // fork / join events without the system-scope fence of a record (hipEventDisableSystemFence): the two
         // streams are on one device, so the producing kernel's end-of-kernel release and the consumer's

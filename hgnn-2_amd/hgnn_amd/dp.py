@@ -140,6 +140,10 @@ class LayerBucketAllReduce:
     gradients into the flat buffer and all-reduces it in one collective after the backward.
     """
 
+    HW_QUEUE_NOTE = ("hgnn_amd.dp: GPU_MAX_HW_QUEUES is {} -- with a process group's streams the executor's side stream "
+                     "can share the main stream's hardware queue and run serialised with it (~20 % per step); set "
+                     "GPU_MAX_HW_QUEUES=8 before the process starts HIP (DESIGN.md §6)")
+
     def __init__(self, model, group=None, sync_running=True, force=False, single=False):
         self.model = model
         # single: one collective over the whole buffer after the backward instead of one per layer (fewer host-side
@@ -189,6 +193,11 @@ class LayerBucketAllReduce:
         self.ptrs = [v.data_ptr() for v in self.views]
         # RCCL (and NCCL) average in the collective itself; gloo sums, then the buffer is divided
         self.avg = None
+        import os
+        import warnings
+        q = os.environ.get("GPU_MAX_HW_QUEUES")
+        if dev.type == "cuda" and (q is None or (q.isdigit() and int(q) < 8)):
+            warnings.warn(self.HW_QUEUE_NOTE.format(q or "unset (4)"), RuntimeWarning, stacklevel=2)
         # set by the executor's backward (net._grad_targets): True when the gradients went to fresh
         # tensors (some p.grad present), i.e. no per-layer events were recorded this step
         self.fresh = False
