@@ -432,13 +432,37 @@ __device__ __forceinline__ void dw_ring_body(char* lds, const float* __restrict_
     }
     constexpr int NC = VIRT ? 4 : 1;
     float ra[PD][4], rb[PD][4], rc[PD][NC];
-    auto load = [&](float (&xa)[4], float (&xb)[4], float (&xc)[NC], int k0) {
+    // the aggregate columns (not VIRT): buffer loads through a descriptor re-based on the stage's first row, whose
+    // record count ends at the chunk's last row -- the range check returns 0 for rows past kend and for the
+    // out-of-range columns (their lane offset is 2^31, past any record count), so the per-lane offsets are
+    // loop-invariant and neither a row clamp nor the masks at the split are needed (the clamped form spent 25 of
+    // its ~100 VALU instructions per stage on 64-bit row addresses)
+    unsigned voa[4], vob[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const long long gk = min(k0 + 4 * rq + i, kend - 1);
-            xa[i] = ap[gk * lda];
-            xb[i] = bp[gk * ldbb];
-            if constexpr (VIRT) xc[i] = cp[2 * gk];
+    for (int i = 0; i < 4; ++i) {
+        voa[i] = am ? (unsigned)(((4 * rq + i) * lda + m0 + col) * 4) : 0x80000000u;
+        vob[i] = bn ? (unsigned)(((4 * rq + i) * ldb + n - kx) * 4) : 0x80000000u;
+    }
+    auto load = [&](float (&xa)[4], float (&xb)[4], float (&xc)[NC], int k0) {
+        if constexpr (VIRT) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const long long gk = min(k0 + 4 * rq + i, kend - 1);
+                xa[i] = ap[gk * lda];
+                xb[i] = bp[gk * ldbb];
+                xc[i] = cp[2 * gk];
+            }
+        } else {
+            const int rows = max(kend - k0, 0);
+            const auto sa = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A) + (long long)k0 * lda, 0,
+                                                              rows * lda * 4, 0x00020000);
+            const auto sb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B) + (long long)k0 * ldb, 0,
+                                                              rows * ldb * 4, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xa[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(sa, (int)voa[i], 0, 0));
+                xb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(sb, (int)vob[i], 0, 0));
+            }
         }
     };
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -448,15 +472,15 @@ __device__ __forceinline__ void dw_ring_body(char* lds, const float* __restrict_
         bf16x4 p[3], q[3];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const bool in = k0 + 4 * rq + i < kend;
+            const bool in = !VIRT || (k0 + 4 * rq + i < kend);  // VIRT: clamped loads, masked here
             __bf16 x, y, z;
-            split3(in && am ? xa[i] : 0.f, x, y, z);
+            split3(in && (!VIRT || am) ? xa[i] : 0.f, x, y, z);
             p[0][i] = x;
             p[1][i] = y;
             p[2][i] = z;
             float bv = xb[i];
             if constexpr (VIRT) bv = fmaf(xc[i], bn_z_s(bv, mu, sc, bb), 0.f);  // the aggregation's value
-            split3(in && bn ? bv : 0.f, x, y, z);
+            split3(in && (!VIRT || bn) ? bv : 0.f, x, y, z);
             q[0][i] = x;
             q[1][i] = y;
             q[2][i] = z;
@@ -566,7 +590,8 @@ int launch_gemm_bf3_dw(const float* dy, int lddy, const float* a, int lda, const
                        int k, int nz, float* slabs, int xcd, hipStream_t s, const DiagIdArgs* id) {
     if (r_cap <= 0) return 0;
     if (nz <= 0) return HGNN_ERR_ARG;
-    if ((long long)r_cap * (lda > lddy ? lda : lddy) >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    // the ring's buffer descriptors hold a chunk's bytes in a 31-bit record count
+    if ((long long)r_cap * (lda > lddy ? lda : lddy) >= (1ll << 29)) return HGNN_ERR_UNSUPPORTED;
     // diagonal I / D columns: whole 128-column output tiles (kx a multiple of 128), the ring kernel
     if (id && (!diag_id_ok(id, k) || (2 * id->c) % 128 || (long long)r_cap * id->ldx >= (1ll << 31)))
         return HGNN_ERR_UNSUPPORTED;
