@@ -29,6 +29,35 @@ constexpr int G_STAGE = 6 * G_PLANE;                  // A planes, then B planes
 
 __device__ __forceinline__ int swz(int row, int ch) { return row * G_ROWB + 16 * (ch ^ ((row >> 2) & 3)); }
 
+// The staging loads of the forward and dA GEMMs through buffer descriptors: A's records end at row M, B's at the
+// third plane's row N; a masked load (column past K or past the plane row, weight row past N) takes the lane
+// offset 2^31, past both record counts, and the range check returns zeros -- no exec branch around a load and
+// no select at the split.  The launchers keep (m_cap + 64) lda and 3 pb below 2^29 elements.
+struct BufOps {
+    __amdgpu_buffer_rsrc_t sa, sb;
+    unsigned arow_off;  // bytes of the thread's A row
+    int ldb, N, n0;
+    long long pb;
+    __device__ BufOps(const float* A, int lda, int M, int gm, const __bf16* B, long long pb_, int ldb_, int N_, int n0_)
+        : ldb(ldb_), N(N_), n0(n0_), pb(pb_) {
+        sa = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), 0, M * lda * 4, 0x00020000);
+        sb = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(B), 0, (int)((2 * pb_ + (long long)N_ * ldb_) * 2),
+                                               0x00020000);
+        arow_off = (unsigned)(gm * lda) * 4u;
+    }
+    // four floats of the thread's A row from column k (a multiple of 4)
+    __device__ __forceinline__ float4 a4(int k, bool ok) const {
+        const unsigned o = ok ? arow_off + 4u * (unsigned)k : 0x80000000u;
+        return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(sa, (int)o, 0, 0));
+    }
+    // element e of the stage's B image (plane e >> 8, row (e & 255) >> 2, chunk e & 3) of the stage at k0
+    __device__ __forceinline__ u32x4 b8(int e, int k0) const {
+        const int pl = e >> 8, row = (e & 255) >> 2, kb = k0 + 8 * (e & 3), gn = n0 + row;
+        const unsigned o = (gn < N && kb < ldb) ? (unsigned)((pl * pb + (long long)gn * ldb + kb) * 2) : 0x80000000u;
+        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(sb, (int)o, 0, 0));
+    }
+};
+
 template <bool ID>
 __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__ A, int lda,
                                                        const __bf16* __restrict__ B, long long pb, int ldb,
@@ -80,6 +109,7 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
     }
     float4 ra[2];
     u32x4 rb[3];
+    const BufOps bo(A, lda, M, m0 + arow, B, pb, ldb, N, n0);
     auto load = [&](int k0) {
         const int k = k0 + 8 * ach, gm = m0 + arow;
         if (ID && k0 < kx) {
@@ -88,17 +118,11 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
             ra[0] = gm < M ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
             ra[1] = gm < M ? *reinterpret_cast<const float4*>(xp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
-            const float* ap = A + (long long)gm * lda + (k - kx);
-            ra[0] = (gm < M && k < K) ? *reinterpret_cast<const float4*>(ap) : make_float4(0.f, 0.f, 0.f, 0.f);
-            ra[1] = (gm < M && k + 4 < K) ? *reinterpret_cast<const float4*>(ap + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            ra[0] = bo.a4(k - kx, k < K);
+            ra[1] = bo.a4(k - kx + 4, k + 4 < K);
         }
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int e = tid + G_NT * i, pl = e >> 8, row = (e & 255) >> 2, ch = e & 3;
-            const int kb = k0 + 8 * ch, gn = n0 + row;
-            rb[i] = (gn < N && kb < ldb) ? *reinterpret_cast<const u32x4*>(B + pl * pb + (long long)gn * ldb + kb)
-                                         : u32x4{0u, 0u, 0u, 0u};
-        }
+        for (int i = 0; i < 3; ++i) rb[i] = bo.b8(tid + G_NT * i, k0);
     };
     auto store = [&](int buf, int k0) {
         char* st = lds + buf * G_STAGE;
@@ -300,30 +324,22 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_da(const float* __restrict__ 
     const int by = jj % gridDim.y, bx = (L & 7) + 8 * (jj / gridDim.y);
     const int m0 = bx * G_BM, n0 = by * G_BN;
     if (m0 >= M) return;
-    const int arow = tid >> 2, ach = tid & 3, gm = m0 + arow;
-    const float* ap = A + (long long)min(gm, M - 1) * lda;
+    const int arow = tid >> 2, ach = tid & 3;
+    const BufOps bo(A, lda, M, m0 + arow, B, pb, ldb, N, n0);
     float4 ra[NST][2];
     u32x4 rb[NST][3];
 #pragma unroll
     for (int t = 0; t < NST; ++t) {
         const int k = t * G_BK + 8 * ach;
-        ra[t][0] = *reinterpret_cast<const float4*>(ap + min(k, K - 4));
-        ra[t][1] = *reinterpret_cast<const float4*>(ap + min(k + 4, K - 4));
-
+        ra[t][0] = bo.a4(k, k < K);
+        ra[t][1] = bo.a4(k + 4, k + 4 < K);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int e = tid + G_NT * i, pl = e >> 8, row = (e & 255) >> 2, ch = e & 3;
-            const int kb = t * G_BK + 8 * ch, gn = min(n0 + row, N - 1);
-            rb[t][i] = *reinterpret_cast<const u32x4*>(B + pl * pb + (long long)gn * ldb + min(kb, ldb - 8));
-        }
+        for (int i = 0; i < 3; ++i) rb[t][i] = bo.b8(tid + G_NT * i, t * G_BK);
     }
     auto store = [&](int buf, int t) {
         char* st = lds + buf * G_STAGE;
-        const int k = t * G_BK + 8 * ach;
-        const bool v0 = gm < M && k < K, v1 = gm < M && k + 4 < K;
-        const float xv[8] = {v0 ? ra[t][0].x : 0.f, v0 ? ra[t][0].y : 0.f, v0 ? ra[t][0].z : 0.f,
-                             v0 ? ra[t][0].w : 0.f, v1 ? ra[t][1].x : 0.f, v1 ? ra[t][1].y : 0.f,
-                             v1 ? ra[t][1].z : 0.f, v1 ? ra[t][1].w : 0.f};
+        const float xv[8] = {ra[t][0].x, ra[t][0].y, ra[t][0].z, ra[t][0].w,
+                             ra[t][1].x, ra[t][1].y, ra[t][1].z, ra[t][1].w};
         bf16x8 p0, p1, p2;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -339,9 +355,7 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_da(const float* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const int e = tid + G_NT * i, pl = e >> 8, row = (e & 255) >> 2, ch = e & 3;
-            const bool ok = n0 + row < N && t * G_BK + 8 * ch < ldb;
-            const u32x4 z = {0u, 0u, 0u, 0u};
-            *reinterpret_cast<u32x4*>(st + (3 + pl) * G_PLANE + swz(row, ch)) = ok ? rb[t][i] : z;
+            *reinterpret_cast<u32x4*>(st + (3 + pl) * G_PLANE + swz(row, ch)) = rb[t][i];
         }
     };
     f32x16 acc, tacc;
@@ -577,6 +591,11 @@ __global__ void __launch_bounds__(D_NT) k_gemm_bf3_tn_ring(const float* __restri
     dw_ring_body<PD, false>(lds, A, lda, B, ldb, slabs, M, N, m0, n0, bz, kbeg, kend, id, kx);
 }
 
+// BufOps' 32-bit byte offsets: the rows a block can name (m_cap + 64) and the three weight planes below 2^29 elements
+bool bufops_ok(int m_cap, int lda, long long pb, int ldb, int n) {
+    return (long long)(m_cap + G_BM) * lda < (1ll << 29) && 3 * pb < (1ll << 29) && (long long)n * ldb <= pb;
+}
+
 // the diagonal I / D columns' contract (DiagIdArgs): 2c a multiple of 32, c <= 256, float4-aligned x rows
 bool diag_id_ok(const DiagIdArgs* id, int k) {
     return id->x && id->diag && id->bn.mean && id->bn.std && id->bn.w && id->bn.b && id->c > 0 && id->c <= 256 &&
@@ -628,7 +647,7 @@ int launch_gemm_bf3_da(const float* a, int lda, const int* m_valid, int m_cap, i
     if (k < 4 || k > 4 * G_BK || lda % 4 || k % 4 || ldb % 8 || pb % 8 || k > lda || bf3_ld(k) > ldb ||
         (reinterpret_cast<uintptr_t>(a) & 15) || (reinterpret_cast<uintptr_t>(b) & 15))
         return HGNN_ERR_UNSUPPORTED;
-    if ((long long)m_cap * lda * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    if (!bufops_ok(m_cap, lda, pb, ldb, n)) return HGNN_ERR_UNSUPPORTED;
     const int gx = ceil_div(ceil_div(m_cap, G_BM), 8) * 8;
     const dim3 g(gx, ceil_div(n, G_BN));
     uint64_t* st = clock_stamps((long long)g.x * g.y * (G_NT / 64));
@@ -652,7 +671,7 @@ int launch_gemm_bf3_fwd(const float* a, int lda, const int* m_valid, int m_cap, 
     if (lda % 4 || k % 4 || ldb % 8 || pb % 8 || k - kx > lda || bf3_ld(k) > ldb ||
         (reinterpret_cast<uintptr_t>(a) & 15) || (reinterpret_cast<uintptr_t>(b) & 15))
         return HGNN_ERR_UNSUPPORTED;
-    if ((long long)m_cap * lda * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
+    if (!bufops_ok(m_cap, lda, pb, ldb, n)) return HGNN_ERR_UNSUPPORTED;
     if (id && (long long)m_cap * id->ldx * 4 >= (1ll << 31)) return HGNN_ERR_UNSUPPORTED;
     const int gx = ceil_div(ceil_div(m_cap, G_BM), 8) * 8;
     const dim3 g(gx, ceil_div(n, G_BN));
