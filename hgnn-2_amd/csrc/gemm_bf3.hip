@@ -158,11 +158,7 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
     const int r31 = lane & 31, h = lane >> 5;
     const int frow = wm * 32 + r31, fcol = wn * 32 + r31;
     if constexpr (ID) __syncthreads();  // the BN table
-    load(0);
-    store(0, 0);
-    __syncthreads();
-    if (nt > 1) load(G_BK);
-    for (int t = 0; t < nt; ++t) {
+    auto mma = [&](int t) {
         const char* st = lds + (t & 1) * G_STAGE;
 #pragma unroll
         for (int r = 0; r < 16; ++r) tacc[r] = 0.f;
@@ -183,13 +179,22 @@ __global__ void __launch_bounds__(G_NT) k_gemm_bf3_fwd(const float* __restrict__
             tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], tacc, 0, 0, 0);
             tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], tacc, 0, 0, 0);
         }
+    };
+    load(0);
+    store(0, 0);
+    __syncthreads();
+    load(G_BK);  // (past K: zeros, unused)
+    // a branch-free body (the loads past K read zeros through the range check), so the split of stage t + 1 and the
+    // MFMAs of stage t share one scheduling region; the last stage after the loop
+    for (int t = 0; t + 1 < nt; ++t) {
+        mma(t);
+        store((t + 1) & 1, (t + 1) * G_BK);
+        load((t + 2) * G_BK);
         acc += tacc;  // per-stage partial sums added to acc (fma chains of G_BK terms, as the fp32 GEMMs)
-        if (t + 1 < nt) {
-            store((t + 1) & 1, (t + 1) * G_BK);
-            if (t + 2 < nt) load((t + 2) * G_BK);
-        }
         __syncthreads();
     }
+    mma(nt - 1);
+    acc += tacc;
     // epilogue (k_gemm3 E3_FWD's): bias, ReLU, store, BN partials (count, mean, M2) per 64-row tile.
     // C/D layout of the 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
     float* red = reinterpret_cast<float*>(lds);  // free: the main loop ended with a barrier
