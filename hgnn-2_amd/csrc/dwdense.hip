@@ -55,22 +55,38 @@ __device__ __forceinline__ void dw_stage(const DwDenseArgs& a, int b, int off, i
         else return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)o, 0, 0));
     };
     auto el = [](vt& v, int q) -> float& { return reinterpret_cast<float*>(&v)[q]; };
-    const int g_n = npad * J * FV, x_n = npad * FV;
+    const int JFV = J * FV, g_n = npad * JFV, x_n = npad * FV;
     constexpr int U = 8;
+    // element i = (row n, column c) of the G image walked by carries: i advances by 256 per load, so (n, c)
+    // advances by (dn, dc) plus a carry -- the per-element division by the runtime J FV cost ~20 VALU each
+    const int dn = 256 / JFV, dc = 256 - dn * JFV;
+    int cn = (int)threadIdx.x / JFV, cc = (int)threadIdx.x - cn * JFV;
     // G rows (the dA slices): all U loads of a round issued before any is used, offsets by select
     for (int base = 0; base < g_n; base += 256 * U) {
         vt v[U];
+        int nn[U], ccs[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            nn[u] = cn;
+            ccs[u] = cc;
+            cc += dc;
+            cn += dn;
+            if (cc >= JFV) {
+                cc -= JFV;
+                ++cn;
+            }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int i = base + u * 256 + threadIdx.x;
-            const int n = i / (J * FV), rem = i - n * (J * FV), j = rem / FV, f = (rem % FV) * V;
+            const int n = nn[u], rem = ccs[u], j = rem / FV, f = (rem % FV) * V;
             const bool live = i < g_n && n < nb && f < fc;
             v[u] = ld(rg, live ? (unsigned)((long long)(off + n) * a.lda + (j0 + j) * F + f0 + f) * 4u : OOB);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int i = base + u * 256 + threadIdx.x;
-            const int n = i / (J * FV), rem = i - n * (J * FV), j = rem / FV, f = (rem % FV) * V;
+            const int n = nn[u], rem = ccs[u], j = rem / FV, f = (rem % FV) * V;
             if (i < g_n) {
                 const bool pad_row = Rs != nullptr && n >= nb && n < nmax;
                 float* d = Gs + n * GP + j * FC + f;
