@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc_$C -o run \
-      -- python3 bench.py --steps 3 --warmup 2 --cpu-baseline 0 --roofline 0 > gpurun_out/pmc_$C.log 2>&1
+      -- python3 bench.py --steps 3 --warmup 2 --settle-s 0 --attribution 0 --cpu-baseline 0 --roofline 0 > gpurun_out/pmc_$C.log 2>&1
   rc=$?; echo "pmc $C rc=$rc"; tail -2 gpurun_out/pmc_$C.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 done

@@ -15,7 +15,7 @@ bash tools/pmc.sh > /dev/null || exit $?
 echo "pmc traffic ok"
 C="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS"
 timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc_sq -o run \
-    -- python3 bench.py --steps 3 --warmup 2 --cpu-baseline 0 --roofline 0 --fwd-line 0 > gpurun_out/pmc_sq.log 2>&1 || exit $?
+    -- python3 bench.py --steps 3 --warmup 2 --settle-s 0 --attribution 0 --cpu-baseline 0 --roofline 0 --fwd-line 0 > gpurun_out/pmc_sq.log 2>&1 || exit $?
 python3 tools/pmc_sq_summary.py gpurun_out/pmc_sq > gpurun_out/pmc_sq_summary.txt || exit $?
 echo "pmc sq ok"
 for cfg in cfg3 cfg5; do
