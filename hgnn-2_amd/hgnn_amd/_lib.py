@@ -28,8 +28,8 @@ DEVERR = {
     0x10: "CCN vertex degree above the compiled bound (1024 for CCN-1D, 256 for CCN-2D)",
     0x20: "CCN adjacency pattern is not symmetric (the batched CCN backward needs A_ij > 0 <=> A_ji > 0)",
     0x40: ("operator slice 0 or 1 (graph_operators' I and D, functions/operators.py:19-23) holds an off-diagonal "
-           "entry; the executor takes these two slices as diagonal -- HGNN_DIAG_ID=0 aggregates them as general "
-           "slices"),
+           "entry, which the opt-in HGNN_DIAG_ID=1 form (these two slices taken as diagonal) cannot take -- unset "
+           "HGNN_DIAG_ID (the default aggregates them as general slices)"),
 }
 
 
