@@ -477,13 +477,19 @@ def main():
     roof = None
     roof_hbm = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    ktr = os.path.join(REPO, "profiles", "kernel_trace.json")
+    trace_note = ("committed profile (profiles/kernel_trace.json: rocprofv3 --kernel-trace of an earlier run of this "
+                  "step, tools/trace_step.py), not measured in this run; frac_trace = the same work over that launch time")
     traffic_note = ("committed profile (profiles/pmc_traffic.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of an earlier "
                     "run of this step), not measured in this run")
     if timed:
         counts = RF.batch_counts(W.detach(), WL, Pm, Pd, Nb, Eb)
         ms, n = timer_ms[dominant]
-        roof = RF.roofline_entry(dominant, ms, n, counts, args.order, 5, args.d, args.layers, args.steps, pmc_path=pmc)
+        roof = RF.roofline_entry(dominant, ms, n, counts, args.order, 5, args.d, args.layers, args.steps, pmc_path=pmc,
+                                 trace_path=ktr)
         roof["traffic_source"] = traffic_note
+        if "frac_trace" in roof:
+            roof["trace_source"] = trace_note
         roof["timed_in"] = (f"a region of its own: {args.steps} eager steps, every wave of this class's launches "
                             "stamping s_memrealtime at entry and exit (a launch = last exit - first entry; no "
                             "events in the stream); each aggregation class in another such region")
@@ -491,11 +497,12 @@ def main():
         roof_hbm = {}
         for k in hbm_classes:
             kms, kn = timer_ms[k]
-            e = RF.roofline_entry(k, kms, kn, counts, args.order, 5, args.d, args.layers, args.steps, pmc_path=pmc)
+            e = RF.roofline_entry(k, kms, kn, counts, args.order, 5, args.d, args.layers, args.steps, pmc_path=pmc,
+                                  trace_path=ktr)
             roof_hbm[RF.NAMES[k]] = {x: e[x] for x in (
                 "bound", "achieved", "peak", "unit", "frac", "traffic", "algorithmic_bytes_per_launch",
                 "launches_per_step", "avg_launch_us", "requested_bytes_per_launch", "requested_gbs",
-                "requested_frac", "traffic_gbs", "traffic_frac") if x in e}
+                "requested_frac", "traffic_gbs", "traffic_frac", "trace_avg_launch_us", "frac_trace") if x in e}
             roof_hbm[RF.NAMES[k]]["traffic_source"] = traffic_note
 
     # forward-only line (config "cfg2f"): the north star's HBM target is stated on the batched

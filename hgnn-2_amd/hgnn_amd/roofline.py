@@ -212,7 +212,25 @@ def pmc_traffic(kcls, path):
     return tot / n if n else None
 
 
-def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, steps, jt=3, pmc_path=None):
+def trace_avg_us(kcls, path):
+    """Average launch duration (us) of class kcls in a committed rocprofv3 kernel trace of the bench step
+    (tools/trace_step.py --json: per kernel avg_us and launches per step), launch-weighted; None if absent."""
+    import json
+    import os
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        rows = json.load(fh)
+    tot = n = 0.0
+    for name, r in rows.items():
+        if _in_class(kcls, name):
+            tot += r["avg_us"] * r["launches_per_step"]
+            n += r["launches_per_step"]
+    return tot / n if n else None
+
+
+def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, steps, jt=3, pmc_path=None,
+                   trace_path=None):
     """bench.py 'roofline' object for a kernel class measured over `steps` steps."""
     fl, by = class_work(kcls, counts, order, f_in, d, n_layers, jt)
     sec = max(ms_total / 1e3, 1e-12)
@@ -234,6 +252,12 @@ def roofline_entry(kcls, ms_total, launches, counts, order, f_in, d, n_layers, s
         # the HBM bytes the PMC counters saw per launch, over the same per-launch time
         extra["traffic_gbs"] = round(traffic / avg_s / 1e9, 1)
         extra["traffic_frac"] = round(traffic / avg_s / 1e9 / PEAK_HBM_GBS, 4)
+    tr = trace_avg_us(kcls, trace_path)
+    if tr is not None:
+        # the same algorithmic work over the kernel trace's launch time (rocprofv3's dispatch end includes the
+        # end-of-kernel write-back that the in-kernel stamps leave out)
+        extra["trace_avg_launch_us"] = round(tr, 3)
+        extra["frac_trace"] = round(achieved / peak * (avg_s * 1e6) / tr, 4)
     if kcls in (K_AGG_FWD, K_AGG_BWD):
         rq = agg_requested_bytes(kcls, counts, order, f_in, d, n_layers, jt)
         rq_gbs = rq * steps / sec / 1e9

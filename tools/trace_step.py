@@ -2,7 +2,7 @@
 """Per-step view of a rocprofv3 kernel trace of bench.py: per-kernel time per step, and the
 busy / idle split of the GPU timeline (union of kernel intervals over the last steps).
 
-usage: python tools/trace_step.py gpurun_out/prof/run_kernel_trace.csv [steps_in_trace]
+usage: python tools/trace_step.py gpurun_out/prof/run_kernel_trace.csv [steps_in_trace] [out.json]
 """
 import csv
 import sys
@@ -51,3 +51,8 @@ for sid in sorted({q for _, _, _, q in win}):
     print(f"  stream {sid}: {len(iv) / nstep:.0f} launches/step, busy {b / 1e3 / nstep:.1f} us/step")
 for n, t in sorted(tot.items(), key=lambda kv: -kv[1]):
     print(f"{t / nstep:9.1f} us/step {cnt[n] / nstep:5.1f} launches  {t / cnt[n]:7.1f} us avg  {n[:90]}")
+if len(sys.argv) > 3:  # JSON: per kernel, its average launch and launches per step (bench.py's roofline cross-check)
+    import json
+    with open(sys.argv[3], "w") as fh:
+        json.dump({n: {"avg_us": round(t / cnt[n], 3), "launches_per_step": round(cnt[n] / nstep, 3)}
+                   for n, t in tot.items()}, fh, indent=1)
