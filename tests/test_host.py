@@ -271,3 +271,25 @@ def test_spec_params_and_checked_params_cache():
     m.layer0.cv1.weight = torch.nn.Parameter(torch.zeros(16, 3, 1))
     with pytest.raises(RuntimeError, match="conv weight"):
         N._checked_params(m._spec(dev), 5, 3, dev)
+
+
+def test_roofline_trace_cross_check(tmp_path):
+    """bench.py's frac_trace: the stamp-timed algorithmic rate rescaled to the committed kernel trace's launch
+    time of the class (launch-weighted over its kernels), absent without a trace file."""
+    import json
+    from hgnn_amd import roofline as RF
+    path = tmp_path / "kernel_trace.json"
+    path.write_text(json.dumps({
+        "k_gemm_bf3_tn_ring<4, false>": {"avg_us": 40.0, "launches_per_step": 6.0},
+        "k_gemm_bf3_tn_ring<4, true>": {"avg_us": 20.0, "launches_per_step": 2.0},
+        "k_agg_fwd_rpw<3, 2, 2, true, 2, 0>": {"avg_us": 16.0, "launches_per_step": 8.0},
+    }))
+    assert RF.trace_avg_us(RF.K_GEMM_DW, str(path)) == 35.0
+    assert RF.trace_avg_us(RF.K_AGG_FWD, str(path)) == 16.0
+    assert RF.trace_avg_us(RF.K_GEMM_DA, str(path)) is None
+    assert RF.trace_avg_us(RF.K_GEMM_DW, str(tmp_path / "absent.json")) is None
+    counts = dict(nodes=9530, edges=22750, nnz_w=40000, nnz_wl=90000, nnz_p=45500)  # batch_counts' layout
+    e = RF.roofline_entry(RF.K_GEMM_DW, 8 * 30e-3, 8, counts, 2, 5, 64, 5, 1, trace_path=str(path))
+    assert e["avg_launch_us"] == 30.0 and e["trace_avg_launch_us"] == 35.0
+    assert abs(e["frac_trace"] - e["frac"] * 30.0 / 35.0) < 1e-3
+    assert "frac_trace" not in RF.roofline_entry(RF.K_GEMM_DW, 8 * 30e-3, 8, counts, 2, 5, 64, 5, 1)
