@@ -1003,10 +1003,8 @@ int launch_bn_backward(const BnBwdArgs& a, hipStream_t s, int apply) {
     }
     if (tiles > 0) {
         as.stamps = v4 ? clock_stamps((long long)tiles * 4) : nullptr;
-        // HGNN_DIAG_SKIP_PART4=1: timing-only diagnostic (wrong statistics): what the statistics launch costs in the step
-        static const bool skip4 = [] { const char* e = getenv("HGNN_DIAG_SKIP_PART4"); return e && e[0] == '1'; }();
-        if (v4 && !(skip4 && acc)) HGNN_KLAUNCH(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, as);
-        else if (!v4) HGNN_KLAUNCH(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
+        if (v4) HGNN_KLAUNCH(k_bn_bwd_part4, dim3(tiles), dim3(256), 0, s, as);
+        else HGNN_KLAUNCH(k_bn_bwd_part, dim3(tiles), dim3(256), 0, s, a);
     }
     HGNN_LAUNCH_CHECK();
     if (!acc) {
